@@ -1,0 +1,168 @@
+/*
+ * phc.h — C ABI of libphc_hip.so, the MI355X-native hot path of the PHC imitation
+ * rollout + PPO step (howird/puffer-phc).
+ *
+ * Conventions:
+ *   - every pointer is a device pointer owned by the caller (PyTorch caching allocator);
+ *     the library never allocates on the hot path and never frees;
+ *   - every call is stream-ordered on `stream` (a hipStream_t passed as void*), returns 0
+ *     or a negative PHC_E* code and never throws; phc_last_error() gives a thread-local
+ *     message for the last failing call;
+ *   - tensors are dense, C-contiguous float32 unless stated; quaternions are xyzw;
+ *   - rigid-body records are 13 floats: pos(3) rot(4) vel(3) ang_vel(3) (the Isaac Gym
+ *     rigid-body state layout, puffer_phc/envs/humanoid_phc.py:542-549).
+ *
+ * Each entry point names the reference interface it replaces.
+ */
+#ifndef PHC_H_
+#define PHC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PHC_NUM_BODIES 24
+#define PHC_NUM_DOF 69
+#define PHC_BODY_STRIDE 13
+#define PHC_SELF_OBS 358
+#define PHC_TASK_OBS 576
+#define PHC_OBS_DIM 934
+#define PHC_AMP_OBS_STEP 196
+#define PHC_STATS_SLOTS 16
+
+enum {
+  PHC_OK = 0,
+  PHC_EINVAL = -1,  /* bad argument (null pointer, size, alignment) */
+  PHC_ELAUNCH = -2, /* kernel launch failed */
+};
+
+/* Packed motion library (MotionLibBase.load_motions packing, puffer_phc/motion_lib.py:396-419).
+ * frames[f, b, :] = gts(3) grs(4) gvs(3) gavs(3); one 1248-byte record per frame. */
+typedef struct phc_motion_lib {
+  const float *frames;          /* [F, 24, 13] */
+  const float *local_rot;       /* [F, 24, 4]  lrs */
+  const float *dof_vel;         /* [F, 23, 3]  dvs */
+  const float *motion_len;      /* [M] seconds, (nf-1)/fps */
+  const float *motion_dt;       /* [M] 1/fps */
+  const int64_t *num_frames;    /* [M] */
+  const int64_t *length_starts; /* [M] exclusive cumsum of num_frames */
+  int64_t num_motions;
+  int64_t num_frames_total;
+} phc_motion_lib;
+
+/* Reference-state output of phc_motion_state (get_motion_state's dict, motion_lib.py:612-626). */
+typedef struct phc_ref_state {
+  float *body;    /* [n, 24, 13] rg_pos, rb_rot, body_vel, body_ang_vel */
+  float *dof_pos; /* [n, 69] (nullable) */
+  float *dof_vel; /* [n, 69] (nullable) */
+} phc_ref_state;
+
+/* Per-env device buffers of HumanoidPHC + PHCPufferEnv (humanoid_phc.py:498-618,
+ * clean_pufferl/env.py:41-60). */
+typedef struct phc_env_buffers {
+  int64_t num_envs;
+  float *rigid_body_state;    /* [N, 24, 13] sim rigid bodies (read by step, written by reset) */
+  float *root_state;          /* [N, 13] actor root state (written by reset; nullable) */
+  float *dof_state;           /* [N, 69, 2] (pos, vel) */
+  const float *dof_force;     /* [N, 69] */
+  int16_t *progress;          /* [N] progress_buf */
+  int64_t *motion_ids;        /* [N] _sampled_motion_ids */
+  float *motion_start_times;  /* [N] */
+  float *motion_start_offset; /* [N] _motion_start_times_offset */
+  float *global_offset;       /* [N, 3] */
+  float *obs;                 /* [N, 934] obs_buf */
+  float *rew;                 /* [N] rew_buf */
+  float *reward_raw;          /* [N, 5] pos, rot, vel, ang_vel, power */
+  uint8_t *reset;             /* [N] reset_buf (bool) */
+  uint8_t *terminate;         /* [N] _terminate_buf (bool) */
+  uint8_t *terminals;         /* [N] PHCPufferEnv.terminals */
+  uint8_t *truncations;       /* [N] PHCPufferEnv.truncations */
+  uint8_t *masks;             /* [N] PHCPufferEnv.masks */
+  float *episode_return;      /* [N] */
+  int32_t *episode_length;    /* [N] */
+  double *stats;              /* [phc_stats_blocks(N), PHC_STATS_SLOTS] per-block log sums */
+} phc_env_buffers;
+
+/* Step constants: RewardConfig (config.py:23-36), EnvConfig power coef / early termination
+ * (config.py:79-101), termination distances and reset bodies (humanoid_phc.py:235-253). */
+typedef struct phc_step_params {
+  float dt; /* control dt as float32 (2/60) */
+  float k_pos, k_rot, k_vel, k_ang_vel;
+  float w_pos, w_rot, w_vel, w_ang_vel;
+  float power_coef;     /* 0.0005 */
+  int32_t use_power_reward;
+  int32_t enable_early_termination;
+  int32_t use_mean_termination;  /* eval mode: mean body distance vs termination_distance[first] */
+  uint32_t reset_body_mask;      /* bit b set = body b counts for termination */
+  float termination_distance[PHC_NUM_BODIES];
+} phc_step_params;
+
+/* Number of per-block statistics rows phc_env_step writes for `num_envs` envs. */
+int64_t phc_stats_blocks(int64_t num_envs);
+
+/* R6+R7: MotionLibBase.get_motion_state (puffer_phc/motion_lib.py:549-626).  offset nullable. */
+int phc_motion_state(const phc_motion_lib *lib, const int64_t *motion_ids, const float *motion_times,
+                     const float *offset, int64_t n, phc_ref_state *out, void *stream);
+
+/* R6,R7,R9-R12,R14 fused: HumanoidPHC.step post-physics (humanoid_phc.py:136-146 ->
+ * _compute_reward :1228-1303, _compute_reset :1311-1333, _compute_observations :935-959)
+ * plus PHCPufferEnv.step bookkeeping (clean_pufferl/env.py:103-140).  Increments progress. */
+int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                 void *stream);
+
+/* R15: HumanoidPHC.reset(env_ids) with StateInit.Random (humanoid_phc.py:90-103, 663-778,
+ * 843-929 + motion_lib.py:526-535) for every env whose flag in `env_mask` is set (env_mask
+ * nullable = use env->reset).  `phase` [N] holds the uniform draws (nullable = counter-based
+ * in-kernel RNG keyed by seed/counter).  Rewrites sim state, progress, start times, offsets,
+ * reset/terminate flags and the env's obs row. */
+int phc_reset_envs(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                   const uint8_t *env_mask, const float *phase, uint64_t seed, uint64_t counter,
+                   void *stream);
+
+/* R13: clip(a,-1,1), pd = offset + scale*a, frozen dofs = 0
+ * (clean_pufferl/env.py:91-93, humanoid_phc.py:106-128, 1216-1226). */
+int phc_actions_to_pd(const float *actions, float *pd_target, int64_t n, const float *offset,
+                      const float *scale, const uint8_t *frozen, void *stream);
+
+/* Physics stand-in (NOT a reference interface; BASELINE configs[1] "physics stubbed"):
+ * writes rigid bodies = reference state at the env's next control time + N(0, sigma) noise,
+ * dof_vel = reference dof vel + noise, dof_force = noise * force_scale. */
+int phc_physics_replay(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                       float pos_sigma, float force_scale, uint64_t seed, uint64_t counter, void *stream);
+
+/* R3-R5: load-time FK + velocities (poselib_skeleton.py:518-619, 1230-1251; motion_lib.py:119-140)
+ * for `num_motions` clips packed back to back.  quat_global f64 [F,24,4], root_trans f64 [F,3],
+ * starts/counts int64 [num_motions], fps float [num_motions].  Writes lib frames/local_rot/
+ * dof_vel.  workspace: phc_fk_workspace_bytes(F) bytes. */
+size_t phc_fk_workspace_bytes(int64_t num_frames_total);
+int phc_fk_motions(const double *quat_global, const double *root_trans, const int64_t *starts,
+                   const int64_t *counts, const float *fps, int64_t num_motions, int64_t num_frames_total,
+                   const int64_t *parents, const float *local_translation, const double *gauss_weights,
+                   int32_t gauss_radius, float *frames, float *local_rot, float *dof_vel, void *workspace,
+                   void *stream);
+
+/* R20: compute_gae (puffer_phc/c_gae.pyx:11-32) as a parallel affine scan.
+ * workspace: phc_gae_workspace_bytes(n) bytes. */
+size_t phc_gae_workspace_bytes(int64_t n);
+int phc_gae(const float *dones, const float *values, const float *rewards, int64_t n, float gamma,
+            float lam, float *advantages, void *workspace, void *stream);
+
+/* R17: RunningNorm.update / forward (puffer_phc/policies/running_norm.py:15-34).
+ * mean/var [cols], count [1] are updated in place; workspace: phc_rms_workspace_bytes(rows, cols). */
+size_t phc_rms_workspace_bytes(int64_t rows, int64_t cols);
+int phc_rms_update(const float *x, int64_t rows, int64_t cols, float *mean, float *var, float *count,
+                   void *workspace, void *stream);
+int phc_rms_normalize(const float *x, float *y, int64_t rows, int64_t cols, const float *mean,
+                      const float *var, float eps, float clip, void *stream);
+
+/* Library version and last error (thread-local). */
+int phc_version(void);
+const char *phc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHC_H_ */

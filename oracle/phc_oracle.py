@@ -262,15 +262,16 @@ def gaussian_weights(sigma=2.0, truncate=4.0):
 
 def gaussian_filter_time(x, sigma=2.0):
     """Correlate along axis 0 with mode='nearest', accumulating in float64 in scipy's
-    symmetric order: w0*x[t] + sum_j (x[t+j] + x[t-j]) * w_j; cast back to x.dtype."""
+    symmetric order (far pairs first): w0*x[t] + sum_{j=r..1} (x[t-j] + x[t+j]) * w_j; cast
+    back to x.dtype.  Bit-exact with scipy.ndimage.gaussian_filter1d."""
     w = gaussian_weights(sigma)
     r = (len(w) - 1) // 2
     T = x.shape[0]
     xd = x.astype(np.float64)
     idx = np.arange(T)
     out = xd * w[r]
-    for j in range(1, r + 1):
-        out = out + (xd[np.minimum(idx + j, T - 1)] + xd[np.maximum(idx - j, 0)]) * w[r + j]
+    for j in range(r, 0, -1):
+        out = out + (xd[np.maximum(idx - j, 0)] + xd[np.minimum(idx + j, T - 1)]) * w[r - j]
     return out.astype(x.dtype)
 
 

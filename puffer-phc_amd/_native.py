@@ -1,0 +1,334 @@
+"""ctypes binding of libphc_hip.so (include/phc.h) on PyTorch-ROCm tensors.
+
+PyTorch is plumbing here: it owns device memory and streams.  Every op validates shape,
+dtype, device and contiguity (raising ValueError like the reference's
+gymtorch.unwrap_tensor, gymtorch/gymtorch/wrapper.py:47-56) and then calls the C ABI on the
+current HIP stream.  There is no CPU fallback: if the library cannot be loaded, importing
+any op raises.
+"""
+
+import ctypes
+import os
+
+import torch
+
+_LIB_PATH = os.environ.get(
+    "PHC_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libphc_hip.so")
+)
+
+NUM_BODIES = 24
+NUM_DOF = 69
+BODY_STRIDE = 13
+OBS_DIM = 934
+STATS_SLOTS = 16
+
+c_i64 = ctypes.c_int64
+c_vp = ctypes.c_void_p
+
+
+class MotionLibC(ctypes.Structure):
+    _fields_ = [("frames", c_vp), ("local_rot", c_vp), ("dof_vel", c_vp), ("motion_len", c_vp),
+                ("motion_dt", c_vp), ("num_frames", c_vp), ("length_starts", c_vp),
+                ("num_motions", c_i64), ("num_frames_total", c_i64)]
+
+
+class RefStateC(ctypes.Structure):
+    _fields_ = [("body", c_vp), ("dof_pos", c_vp), ("dof_vel", c_vp)]
+
+
+class EnvBuffersC(ctypes.Structure):
+    _fields_ = [("num_envs", c_i64), ("rigid_body_state", c_vp), ("root_state", c_vp), ("dof_state", c_vp),
+                ("dof_force", c_vp), ("progress", c_vp), ("motion_ids", c_vp), ("motion_start_times", c_vp),
+                ("motion_start_offset", c_vp), ("global_offset", c_vp), ("obs", c_vp), ("rew", c_vp),
+                ("reward_raw", c_vp), ("reset", c_vp), ("terminate", c_vp), ("terminals", c_vp),
+                ("truncations", c_vp), ("masks", c_vp), ("episode_return", c_vp), ("episode_length", c_vp),
+                ("stats", c_vp)]
+
+
+class StepParamsC(ctypes.Structure):
+    _fields_ = [("dt", ctypes.c_float), ("k_pos", ctypes.c_float), ("k_rot", ctypes.c_float),
+                ("k_vel", ctypes.c_float), ("k_ang_vel", ctypes.c_float), ("w_pos", ctypes.c_float),
+                ("w_rot", ctypes.c_float), ("w_vel", ctypes.c_float), ("w_ang_vel", ctypes.c_float),
+                ("power_coef", ctypes.c_float), ("use_power_reward", ctypes.c_int32),
+                ("enable_early_termination", ctypes.c_int32), ("use_mean_termination", ctypes.c_int32),
+                ("reset_body_mask", ctypes.c_uint32), ("termination_distance", ctypes.c_float * NUM_BODIES)]
+
+
+_EXPORTS = {
+    "phc_version": (ctypes.c_int, []),
+    "phc_last_error": (ctypes.c_char_p, []),
+    "phc_stats_blocks": (c_i64, [c_i64]),
+    "phc_motion_state": (ctypes.c_int, [ctypes.POINTER(MotionLibC), c_vp, c_vp, c_vp, c_i64,
+                                         ctypes.POINTER(RefStateC), c_vp]),
+    "phc_env_step": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
+                                     ctypes.POINTER(StepParamsC), c_vp]),
+    "phc_reset_envs": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
+                                       ctypes.POINTER(StepParamsC), c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint64,
+                                       c_vp]),
+    "phc_actions_to_pd": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "phc_physics_replay": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
+                                           ctypes.POINTER(StepParamsC), ctypes.c_float, ctypes.c_float,
+                                           ctypes.c_uint64, ctypes.c_uint64, c_vp]),
+    "phc_fk_workspace_bytes": (ctypes.c_size_t, [c_i64]),
+    "phc_fk_motions": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
+                                       ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "phc_gae_workspace_bytes": (ctypes.c_size_t, [c_i64]),
+    "phc_gae": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_vp, c_vp, c_vp]),
+    "phc_rms_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
+    "phc_rms_update": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "phc_rms_normalize": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, ctypes.c_float,
+                                          c_vp]),
+}
+
+
+def load_library(path=_LIB_PATH):
+    """Load libphc_hip.so and declare every exported symbol; raises if absent."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libphc_hip.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (there is no CPU fallback for the PHC hot path)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = load_library()
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = lib().phc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(t, dtype, shape=None, name="tensor", nullable=False):
+    if t is None:
+        if nullable:
+            return None
+        raise ValueError(f"{name} must not be None")
+    if not isinstance(t, torch.Tensor):
+        raise ValueError(f"{name} must be a torch.Tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected dtype {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a device (cuda/HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    return t.data_ptr()
+
+
+def _stream(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+# ------------------------------------------------------------------ structs --
+def motion_lib_struct(frames, local_rot, dof_vel, motion_len, motion_dt, num_frames, length_starts):
+    F = frames.shape[0]
+    M = motion_len.shape[0]
+    return MotionLibC(
+        _ptr(frames, torch.float32, (F, NUM_BODIES, BODY_STRIDE), "frames"),
+        _ptr(local_rot, torch.float32, (F, NUM_BODIES, 4), "local_rot"),
+        _ptr(dof_vel, torch.float32, (F, NUM_BODIES - 1, 3), "dof_vel"),
+        _ptr(motion_len, torch.float32, (M,), "motion_len"),
+        _ptr(motion_dt, torch.float32, (M,), "motion_dt"),
+        _ptr(num_frames, torch.int64, (M,), "num_frames"),
+        _ptr(length_starts, torch.int64, (M,), "length_starts"),
+        M, F)
+
+
+def step_params_struct(dt, reward, power_coef, use_power_reward, enable_early_termination, use_mean,
+                       reset_body_ids, termination_distances):
+    p = StepParamsC()
+    p.dt = float(dt)
+    p.k_pos, p.k_rot, p.k_vel, p.k_ang_vel = reward.k_pos, reward.k_rot, reward.k_vel, reward.k_ang_vel
+    p.w_pos, p.w_rot, p.w_vel, p.w_ang_vel = reward.w_pos, reward.w_rot, reward.w_vel, reward.w_ang_vel
+    p.power_coef = float(power_coef)
+    p.use_power_reward = int(bool(use_power_reward))
+    p.enable_early_termination = int(bool(enable_early_termination))
+    p.use_mean_termination = int(bool(use_mean))
+    mask = 0
+    for b in reset_body_ids:
+        mask |= 1 << int(b)
+    p.reset_body_mask = mask
+    td = [float(x) for x in termination_distances]
+    if len(td) != NUM_BODIES:
+        raise ValueError("termination_distances must have 24 entries")
+    for i, x in enumerate(td):
+        p.termination_distance[i] = x
+    return p
+
+
+def env_struct(num_envs, rigid_body_state, root_state, dof_state, dof_force, progress, motion_ids, start_times,
+               start_offset, global_offset, obs, rew, reward_raw, reset, terminate, terminals=None, truncations=None,
+               masks=None, episode_return=None, episode_length=None, stats=None):
+    N = num_envs
+    u8 = torch.uint8
+    return EnvBuffersC(
+        N,
+        _ptr(rigid_body_state, torch.float32, (N, NUM_BODIES, BODY_STRIDE), "rigid_body_state"),
+        _ptr(root_state, torch.float32, (N, BODY_STRIDE), "root_state", nullable=True),
+        _ptr(dof_state, torch.float32, (N, NUM_DOF, 2), "dof_state"),
+        _ptr(dof_force, torch.float32, (N, NUM_DOF), "dof_force"),
+        _ptr(progress, torch.int16, (N,), "progress"),
+        _ptr(motion_ids, torch.int64, (N,), "motion_ids"),
+        _ptr(start_times, torch.float32, (N,), "motion_start_times"),
+        _ptr(start_offset, torch.float32, (N,), "motion_start_offset"),
+        _ptr(global_offset, torch.float32, (N, 3), "global_offset"),
+        _ptr(obs, torch.float32, (N, OBS_DIM), "obs"),
+        _ptr(rew, torch.float32, (N,), "rew"),
+        _ptr(reward_raw, torch.float32, (N, 5), "reward_raw"),
+        _ptr(_as_u8(reset), u8, (N,), "reset"),
+        _ptr(_as_u8(terminate), u8, (N,), "terminate"),
+        _ptr(_as_u8(terminals), u8, (N,), "terminals", nullable=True),
+        _ptr(_as_u8(truncations), u8, (N,), "truncations", nullable=True),
+        _ptr(_as_u8(masks), u8, (N,), "masks", nullable=True),
+        _ptr(episode_return, torch.float32, (N,), "episode_return", nullable=True),
+        _ptr(episode_length, torch.int32, (N,), "episode_length", nullable=True),
+        _ptr(stats, torch.float64, (lib().phc_stats_blocks(N), STATS_SLOTS), "stats", nullable=True),
+    )
+
+
+def _as_u8(t):
+    """bool tensors are passed as their uint8 storage (same bytes, 0/1)."""
+    if t is None:
+        return None
+    if t.dtype == torch.bool:
+        return t.view(torch.uint8)
+    return t
+
+
+# ---------------------------------------------------------------------- ops --
+def motion_state(mlib, motion_ids, motion_times, offset=None, want_dof=True):
+    """R6+R7 (motion_lib.py:549-626).  Returns body [n,24,13], dof_pos/dof_vel [n,69]."""
+    n = motion_ids.shape[0]
+    dev = motion_ids.device
+    body = torch.empty((n, NUM_BODIES, BODY_STRIDE), dtype=torch.float32, device=dev)
+    dof_pos = torch.empty((n, NUM_DOF), dtype=torch.float32, device=dev) if want_dof else None
+    dof_vel = torch.empty((n, NUM_DOF), dtype=torch.float32, device=dev) if want_dof else None
+    out = RefStateC(body.data_ptr(), dof_pos.data_ptr() if want_dof else None,
+                    dof_vel.data_ptr() if want_dof else None)
+    rc = lib().phc_motion_state(ctypes.byref(mlib), _ptr(motion_ids, torch.int64, (n,), "motion_ids"),
+                                _ptr(motion_times, torch.float32, (n,), "motion_times"),
+                                _ptr(offset, torch.float32, (n, 3), "offset", nullable=True), n,
+                                ctypes.byref(out), _stream())
+    _check(rc, "phc_motion_state")
+    return body, dof_pos, dof_vel
+
+
+def env_step(env_c, mlib, params):
+    _check(lib().phc_env_step(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(params), _stream()),
+           "phc_env_step")
+
+
+def reset_envs(env_c, mlib, params, mask=None, phase=None, seed=0, counter=0, num_envs=None):
+    n = env_c.num_envs
+    _check(lib().phc_reset_envs(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(params),
+                                _ptr(_as_u8(mask), torch.uint8, (n,), "mask", nullable=True),
+                                _ptr(phase, torch.float32, (n,), "phase", nullable=True),
+                                ctypes.c_uint64(seed), ctypes.c_uint64(counter), _stream()),
+           "phc_reset_envs")
+
+
+def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):
+    _check(lib().phc_physics_replay(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(params),
+                                    float(pos_sigma), float(force_scale), ctypes.c_uint64(seed),
+                                    ctypes.c_uint64(counter), _stream()),
+           "phc_physics_replay")
+
+
+def actions_to_pd(actions, pd_out, offset, scale, frozen):
+    n = actions.shape[0]
+    _check(lib().phc_actions_to_pd(_ptr(actions, torch.float32, (n, NUM_DOF), "actions"),
+                                   _ptr(pd_out, torch.float32, (n, NUM_DOF), "pd_target"), n,
+                                   _ptr(offset, torch.float32, (NUM_DOF,), "offset"),
+                                   _ptr(scale, torch.float32, (NUM_DOF,), "scale"),
+                                   _ptr(_as_u8(frozen), torch.uint8, (NUM_DOF,), "frozen", nullable=True),
+                                   _stream()),
+           "phc_actions_to_pd")
+
+
+def fk_motions(quat_global, root_trans, starts, counts, fps, parents, local_translation, gauss_weights):
+    """R3-R5: returns (frames [F,24,13], local_rot [F,24,4], dof_vel [F,23,3])."""
+    F = quat_global.shape[0]
+    M = starts.shape[0]
+    dev = quat_global.device
+    frames = torch.empty((F, NUM_BODIES, BODY_STRIDE), dtype=torch.float32, device=dev)
+    lrs = torch.empty((F, NUM_BODIES, 4), dtype=torch.float32, device=dev)
+    dvs = torch.empty((F, NUM_BODIES - 1, 3), dtype=torch.float32, device=dev)
+    ws = torch.empty(int(lib().phc_fk_workspace_bytes(F)), dtype=torch.uint8, device=dev)
+    radius = (gauss_weights.shape[0] - 1) // 2
+    rc = lib().phc_fk_motions(
+        _ptr(quat_global, torch.float64, (F, NUM_BODIES, 4), "quat_global"),
+        _ptr(root_trans, torch.float64, (F, 3), "root_trans"),
+        _ptr(starts, torch.int64, (M,), "starts"), _ptr(counts, torch.int64, (M,), "counts"),
+        _ptr(fps, torch.float32, (M,), "fps"), M, F,
+        _ptr(parents, torch.int64, (NUM_BODIES,), "parents"),
+        _ptr(local_translation, torch.float32, (NUM_BODIES, 3), "local_translation"),
+        _ptr(gauss_weights, torch.float64, None, "gauss_weights"), radius,
+        frames.data_ptr(), lrs.data_ptr(), dvs.data_ptr(), ws.data_ptr(), _stream())
+    _check(rc, "phc_fk_motions")
+    return frames, lrs, dvs
+
+
+class GAE:
+    """compute_gae (c_gae.pyx:11-32) on device with a cached workspace."""
+
+    def __init__(self):
+        self._ws = None
+
+    def __call__(self, dones, values, rewards, gamma, lam, out=None):
+        n = rewards.shape[0]
+        need = int(lib().phc_gae_workspace_bytes(n))
+        if self._ws is None or self._ws.numel() < need or self._ws.device != rewards.device:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=rewards.device)
+        if out is None:
+            out = torch.empty_like(rewards)
+        rc = lib().phc_gae(_ptr(dones, torch.float32, (n,), "dones"), _ptr(values, torch.float32, (n,), "values"),
+                           _ptr(rewards, torch.float32, (n,), "rewards"), n, float(gamma), float(lam),
+                           _ptr(out, torch.float32, (n,), "advantages"), self._ws.data_ptr(), _stream())
+        _check(rc, "phc_gae")
+        return out
+
+
+_gae = GAE()
+
+
+def compute_gae(dones, values, rewards, gamma, lam, out=None):
+    return _gae(dones, values, rewards, gamma, lam, out)
+
+
+def rms_update(x, mean, var, count, workspace=None):
+    rows, cols = x.shape
+    need = int(lib().phc_rms_workspace_bytes(rows, cols))
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
+    rc = lib().phc_rms_update(_ptr(x, torch.float32, (rows, cols), "x"), rows, cols,
+                              _ptr(mean, torch.float32, None, "running_mean"),
+                              _ptr(var, torch.float32, None, "running_var"),
+                              _ptr(count, torch.float32, (1,), "count"), workspace.data_ptr(), _stream())
+    _check(rc, "phc_rms_update")
+    return workspace
+
+
+def rms_normalize(x, mean, var, eps=1e-5, clip=10.0, out=None):
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    rc = lib().phc_rms_normalize(_ptr(x, torch.float32, (rows, cols), "x"),
+                                 _ptr(out, torch.float32, (rows, cols), "out"), rows, cols,
+                                 _ptr(mean, torch.float32, None, "running_mean"),
+                                 _ptr(var, torch.float32, None, "running_var"), float(eps), float(clip), _stream())
+    _check(rc, "phc_rms_normalize")
+    return out

@@ -1,0 +1,129 @@
+"""PHCPufferEnv drop-in (puffer_phc/clean_pufferl/env.py:22-195): the pufferlib.PufferEnv
+protocol over HumanoidPHC, with every per-step buffer on the device.
+
+The reference moves actions D->H->D (np.clip + torch.from_numpy, :91-93) and finds resets
+with torch.nonzero / .tolist() (:114-121).  Here `step` accepts device (or numpy) actions,
+the fused step kernel writes terminals / truncations / masks / episode return and length,
+and terminated envs are re-initialised by a kernel that reads reset_buf on the device.
+Episode statistics accumulate in per-workgroup float64 rows and are reduced on the host only
+every `log_interval` ticks (the reference's logging cadence, :145-162).
+"""
+
+import functools
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..envs.humanoid_phc import HumanoidPHC
+
+
+def env_creator(name="puffer_phc"):
+    return functools.partial(make, name)
+
+
+def make(cfg, motion_data=None):
+    return PHCPufferEnv(cfg, motion_data=motion_data)
+
+
+class PHCPufferEnv:
+    def __init__(self, cfg, motion_data=None, physics=None):
+        self.render_mode = "native"
+        self.cfg = cfg
+        self.env = HumanoidPHC(cfg, motion_data=motion_data, physics=physics)
+        self.driver_env = self
+        self.single_observation_space = self.env.single_observation_space
+        self.single_action_space = self.env.single_action_space
+        self.amp_observation_space = self.env.amp_observation_space if cfg.use_amp_obs else None
+        N, dev = self.num_agents, cfg.device
+        self.observations = self.env.obs_buf
+        self.rewards = self.env.rew_buf
+        self.terminals = torch.zeros(N, dtype=torch.bool, device=dev)
+        self.truncations = torch.zeros(N, dtype=torch.bool, device=dev)
+        self.masks = torch.ones(N, dtype=torch.bool, device=dev)
+        self.actions = torch.zeros((N, *self.single_action_space.shape), dtype=torch.float32, device=dev)
+        self.episode_returns = torch.zeros(N, dtype=torch.float32, device=dev)
+        self.episode_lengths = torch.zeros(N, dtype=torch.int32, device=dev)
+        self.stats = torch.zeros((_native.lib().phc_stats_blocks(N), _native.STATS_SLOTS), dtype=torch.float64,
+                                 device=dev)
+        self.env.attach_puffer_buffers(self.terminals, self.truncations, self.masks, self.episode_returns,
+                                       self.episode_lengths, self.stats)
+        self.env_ids = torch.arange(N, device=dev)
+        self.episode_count = 0
+        self.tick = 0
+        self._pending = None
+
+    @property
+    def num_agents(self):
+        return self.cfg.num_envs
+
+    @property
+    def agents_per_batch(self):
+        return self.num_agents
+
+    def reset(self, seed=None):
+        self.tick = 0
+        self.env.reset()
+        self.amp_obs = self.env.amp_obs if self.cfg.use_amp_obs else None
+        self.rewards.zero_()
+        self.terminals.zero_()
+        self.truncations.zero_()
+        self.masks.fill_(True)
+        self.actions.zero_()
+        self.stats.zero_()
+        return self.observations, []
+
+    def step(self, actions):
+        if isinstance(actions, np.ndarray):
+            self.actions.copy_(torch.from_numpy(actions))
+        elif actions.data_ptr() != self.actions.data_ptr():
+            self.actions.copy_(actions)
+        # clipping happens inside phc_actions_to_pd (cfg.clip_actions is always honoured)
+        self.env.step(self.actions)
+        rew = self.rewards.clone()
+        self.env.reset_done()
+        self.amp_obs = self.env.amp_obs if self.cfg.use_amp_obs else None
+        info = []
+        self.tick += 1
+        if self.tick % self.cfg.log_interval == 0:
+            info = self.mean_and_log()
+        return self.observations, rew, self.terminals, self.truncations, info
+
+    def mean_and_log(self):
+        """Host reduction of the per-block statistics (clean_pufferl/env.py:145-188)."""
+        s = self.stats.sum(0).cpu().numpy()
+        self.stats.zero_()
+        n_ep = s[7]
+        self.episode_count += int(n_ep)
+        denom = self.cfg.log_interval * self.num_agents
+        info = {
+            "rew_body_pos": s[0] / denom,
+            "rew_body_rot": s[1] / denom,
+            "rew_lin_vel": s[2] / denom,
+            "rew_ang_vel": s[3] / denom,
+            "rew_power": s[4] / denom,
+        }
+        if n_ep > 0:
+            info.update(episode_return=s[5] / n_ep, episode_length=s[6] / n_ep, truncated_rate=s[8] / n_ep)
+        return [info]
+
+    # -------------------------------------------- pufferlib vecenv protocol --
+    def async_reset(self, seed=None):
+        obs, _ = self.reset(seed)
+        self._pending = (obs, self.rewards, self.terminals, self.truncations, [], self.env_ids, self.masks)
+
+    def send(self, actions):
+        obs, rew, term, trunc, info = self.step(actions)
+        self._pending = (obs, rew, term, trunc, info, self.env_ids, self.masks)
+
+    def recv(self):
+        return self._pending
+
+    def render(self):
+        return self.env.render()
+
+    def close(self):
+        self.env.close()
+
+    def fetch_amp_obs_demo(self):
+        return self.env.fetch_amp_obs_demo()

@@ -1,0 +1,176 @@
+// phc_common.h — shared host/device plumbing of libphc_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <string>
+
+#include "phc.h"
+#include "phc_quat.h"
+
+namespace phc {
+
+// thread-local message of the last failing call (phc_last_error)
+void set_error(const char *fmt, ...);
+int check_launch(const char *what);
+
+#define PHC_REQUIRE(cond, ...)        \
+  do {                                \
+    if (!(cond)) {                    \
+      ::phc::set_error(__VA_ARGS__);  \
+      return PHC_EINVAL;              \
+    }                                 \
+  } while (0)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kBodies = PHC_NUM_BODIES;
+constexpr int kRec = PHC_BODY_STRIDE;  // floats per rigid-body record
+constexpr int kObs = PHC_OBS_DIM;
+constexpr int kGroup = 32;             // lanes per env: one lane per body, 24 of 32 active
+constexpr int kBlock = 256;            // 4 waves, 8 envs per workgroup
+constexpr int kEnvsPerBlock = kBlock / kGroup;
+
+// ---------------------------------------------------------------- records --
+struct BodyRec {
+  v3 p;
+  q4 r;
+  v3 v;
+  v3 av;
+};
+
+__device__ __forceinline__ BodyRec load_body(const float *__restrict__ q) {
+  BodyRec b;
+  b.p = {q[0], q[1], q[2]};
+  b.r = {q[3], q[4], q[5], q[6]};
+  b.v = {q[7], q[8], q[9]};
+  b.av = {q[10], q[11], q[12]};
+  return b;
+}
+
+__device__ __forceinline__ void store_body(float *__restrict__ q, const BodyRec &b) {
+  q[0] = b.p.x; q[1] = b.p.y; q[2] = b.p.z;
+  q[3] = b.r.x; q[4] = b.r.y; q[5] = b.r.z; q[6] = b.r.w;
+  q[7] = b.v.x; q[8] = b.v.y; q[9] = b.v.z;
+  q[10] = b.av.x; q[11] = b.av.y; q[12] = b.av.z;
+}
+
+// ------------------------------------------------- motion lib (device view) --
+struct LibView {
+  const float *frames;
+  const float *local_rot;
+  const float *dof_vel;
+  const float *motion_len;
+  const float *motion_dt;
+  const int64_t *num_frames;
+  const int64_t *length_starts;
+};
+
+inline LibView lib_view(const phc_motion_lib *l) {
+  return {l->frames, l->local_rot, l->dof_vel, l->motion_len, l->motion_dt, l->num_frames, l->length_starts};
+}
+
+struct MotionScalars {
+  float len, dt;
+  int64_t nf, start;
+};
+
+__device__ __forceinline__ MotionScalars load_motion(const LibView &l, int64_t mid) {
+  return {l.motion_len[mid], l.motion_dt[mid], l.num_frames[mid], l.length_starts[mid]};
+}
+
+struct Blend {
+  int64_t f0, f1;  // absolute (flat) frame rows
+  float b;
+};
+
+__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+
+// motion_lib.py:655-665 _calc_frame_blend (bit-exact with -ffp-contract=off)
+__device__ __forceinline__ Blend frame_blend(float time, const MotionScalars &m) {
+  float phase = clamp01(time / m.len);
+  if (time < 0.0f) time = 0.0f;
+  const int64_t f0 = (int64_t)(phase * (float)(m.nf - 1));
+  const int64_t f1 = f0 + 1 < m.nf - 1 ? f0 + 1 : m.nf - 1;
+  const float b = clamp01((time - (float)f0 * m.dt) / m.dt);
+  return {m.start + f0, m.start + f1, b};
+}
+
+// motion_lib.py:597-610: lerp of pos (+offset) / vel / ang vel, slerp of global rotation
+__device__ __forceinline__ BodyRec ref_body(const float *__restrict__ frames, const Blend &bl, int body,
+                                            const v3 *offset) {
+  const BodyRec a = load_body(frames + (bl.f0 * kBodies + body) * kRec);
+  const BodyRec c = load_body(frames + (bl.f1 * kBodies + body) * kRec);
+  const float t = bl.b;
+  const float s = 1.0f - t;
+  BodyRec o;
+  o.p = {s * a.p.x + t * c.p.x, s * a.p.y + t * c.p.y, s * a.p.z + t * c.p.z};
+  if (offset) o.p = vadd(o.p, *offset);
+  o.v = {s * a.v.x + t * c.v.x, s * a.v.y + t * c.v.y, s * a.v.z + t * c.v.z};
+  o.av = {s * a.av.x + t * c.av.x, s * a.av.y + t * c.av.y, s * a.av.z + t * c.av.z};
+  o.r = slerp(a.r, c.r, t);
+  return o;
+}
+
+// dof_pos of body `body` (>=1): exp map of slerped local rotation (motion_lib.py:605-606, 670-673)
+__device__ __forceinline__ v3 ref_dof_pos(const float *__restrict__ lrs, const Blend &bl, int body) {
+  const float *a = lrs + (bl.f0 * kBodies + body) * 4;
+  const float *c = lrs + (bl.f1 * kBodies + body) * 4;
+  const q4 r = slerp(q4{a[0], a[1], a[2], a[3]}, q4{c[0], c[1], c[2], c[3]}, bl.b);
+  return quat_to_exp_map(r);
+}
+
+// dof_vel of body `body` (>=1): lerp of dvs rows (motion_lib.py:603)
+__device__ __forceinline__ v3 ref_dof_vel(const float *__restrict__ dvs, const Blend &bl, int body) {
+  const float *a = dvs + (bl.f0 * (kBodies - 1) + (body - 1)) * 3;
+  const float *c = dvs + (bl.f1 * (kBodies - 1) + (body - 1)) * 3;
+  const float t = bl.b, s = 1.0f - t;
+  return {s * a[0] + t * c[0], s * a[1] + t * c[1], s * a[2] + t * c[2]};
+}
+
+// -------------------------------------------------------------- group ops --
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int m = kGroup / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, kGroup);
+  return v;
+}
+__device__ __forceinline__ float group_bcast(float v) { return __shfl(v, 0, kGroup); }
+
+// ------------------------------------------------------------ observation --
+// One body's slices of the 934-float observation (common.py:23-103 self obs with
+// local_root_obs/root_height_obs/upright; common.py:107-176 imitation obs v6, time_steps 1).
+__device__ __forceinline__ void write_obs_body(float *__restrict__ o, int b, const BodyRec &s, v3 root_p, q4 hinv,
+                                               q4 hrot, const BodyRec &ref) {
+  float t6[6];
+  if (b == 0) {
+    o[0] = root_p.z;
+  } else {
+    const v3 lp = my_quat_rotate(hinv, vsub(s.p, root_p));
+    float *d = o + 1 + 3 * (b - 1);
+    d[0] = lp.x; d[1] = lp.y; d[2] = lp.z;
+  }
+  quat_to_tan_norm(quat_mul(hinv, s.r), t6);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) o[70 + 6 * b + k] = t6[k];
+  v3 x = my_quat_rotate(hinv, s.v);
+  o[214 + 3 * b] = x.x; o[215 + 3 * b] = x.y; o[216 + 3 * b] = x.z;
+  x = my_quat_rotate(hinv, s.av);
+  o[286 + 3 * b] = x.x; o[287 + 3 * b] = x.y; o[288 + 3 * b] = x.z;
+  // task obs
+  x = my_quat_rotate(hinv, vsub(ref.p, s.p));
+  o[358 + 3 * b] = x.x; o[359 + 3 * b] = x.y; o[360 + 3 * b] = x.z;
+  quat_to_tan_norm(quat_mul(quat_mul(hinv, quat_mul(ref.r, quat_conj(s.r))), hrot), t6);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) o[430 + 6 * b + k] = t6[k];
+  x = my_quat_rotate(hinv, vsub(ref.v, s.v));
+  o[574 + 3 * b] = x.x; o[575 + 3 * b] = x.y; o[576 + 3 * b] = x.z;
+  x = my_quat_rotate(hinv, vsub(ref.av, s.av));
+  o[646 + 3 * b] = x.x; o[647 + 3 * b] = x.y; o[648 + 3 * b] = x.z;
+  x = my_quat_rotate(hinv, vsub(ref.p, root_p));
+  o[718 + 3 * b] = x.x; o[719 + 3 * b] = x.y; o[720 + 3 * b] = x.z;
+  quat_to_tan_norm(quat_mul(hinv, ref.r), t6);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) o[790 + 6 * b + k] = t6[k];
+}
+
+}  // namespace phc

@@ -1,0 +1,194 @@
+// phc_quat.h — device quaternion/transform math for the PHC hot path (gfx950).
+//
+// Every function follows the reference's TorchScript expression order
+// (puffer_phc/torch_utils.py) so that, compiled with -ffp-contract=off, each IEEE
+// add/mul/div/sqrt rounds exactly as torch-CPU's separate elementwise kernels do; only
+// libm transcendentals (acos/atan2/sin/cos/exp) differ, by ulps.  Quaternions are xyzw.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace phc {
+
+template <typename T> struct Q4 { T x, y, z, w; };
+template <typename T> struct V3 { T x, y, z; };
+
+using q4 = Q4<float>;
+using v3 = V3<float>;
+
+template <typename T> __device__ __forceinline__ V3<T> vsub(V3<T> a, V3<T> b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+template <typename T> __device__ __forceinline__ V3<T> vadd(V3<T> a, V3<T> b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+
+// torch_utils.py:55-75 — the 8-multiply quaternion product.
+template <typename T>
+__device__ __forceinline__ Q4<T> quat_mul(Q4<T> a, Q4<T> b) {
+  const T ww = (a.z + a.x) * (b.x + b.y);
+  const T yy = (a.w - a.y) * (b.w + b.z);
+  const T zz = (a.w + a.y) * (b.w - b.z);
+  const T xx = ww + yy + zz;
+  const T qq = T(0.5) * (xx + (a.z - a.x) * (b.x - b.y));
+  const T w = qq - ww + (a.z - a.y) * (b.y - b.z);
+  const T x = qq - xx + (a.x + a.w) * (b.x + b.w);
+  const T y = qq - yy + (a.w - a.x) * (b.y + b.z);
+  const T z = qq - zz + (a.z + a.y) * (b.w - b.x);
+  return {x, y, z, w};
+}
+
+// torch_utils.py:79-82
+template <typename T> __device__ __forceinline__ Q4<T> quat_conj(Q4<T> a) { return {-a.x, -a.y, -a.z, a.w}; }
+
+// torch.norm(p=2, dim=-1) over 3 / 4 elements: sequential sum of squares, then sqrt.
+template <typename T> __device__ __forceinline__ T norm3(V3<T> v) {
+  T s = v.x * v.x;
+  s = s + v.y * v.y;
+  s = s + v.z * v.z;
+  return sqrt(s);
+}
+template <typename T> __device__ __forceinline__ T norm4(Q4<T> q) {
+  T s = q.x * q.x;
+  s = s + q.y * q.y;
+  s = s + q.z * q.z;
+  s = s + q.w * q.w;
+  return sqrt(s);
+}
+
+// torch_utils.py:174-179 quat_unit
+template <typename T> __device__ __forceinline__ Q4<T> quat_unit(Q4<T> q) {
+  T n = norm4(q);
+  n = n < T(1e-9) ? T(1e-9) : n;
+  return {q.x / n, q.y / n, q.z / n, q.w / n};
+}
+
+// torch_utils.py:154-161 quat_pos (a sign flip by an exact +-1 factor) then quat_unit.
+template <typename T> __device__ __forceinline__ Q4<T> quat_normalize(Q4<T> q) {
+  if (q.w < T(0)) q = {-q.x, -q.y, -q.z, -q.w};
+  return quat_unit(q);
+}
+
+template <typename T> __device__ __forceinline__ Q4<T> quat_mul_norm(Q4<T> a, Q4<T> b) {
+  return quat_normalize(quat_mul(a, b));
+}
+
+// torch_utils.py:273-279 — rotation through the full quaternion product.
+template <typename T> __device__ __forceinline__ V3<T> quat_rotate(Q4<T> r, V3<T> v) {
+  const Q4<T> o = {v.x, v.y, v.z, T(0)};
+  const Q4<T> t = quat_mul(quat_mul(r, o), quat_conj(r));
+  return {t.x, t.y, t.z};
+}
+
+// torch_utils.py:283-291 my_quat_rotate: a + b + c.
+__device__ __forceinline__ v3 my_quat_rotate(q4 q, v3 v) {
+  const float s = 2.0f * (q.w * q.w) - 1.0f;
+  const v3 a = {v.x * s, v.y * s, v.z * s};
+  const float cx = q.y * v.z - q.z * v.y;
+  const float cy = q.z * v.x - q.x * v.z;
+  const float cz = q.x * v.y - q.y * v.x;
+  const v3 b = {cx * q.w * 2.0f, cy * q.w * 2.0f, cz * q.w * 2.0f};
+  const float dot = q.x * v.x + q.y * v.y + q.z * v.z;
+  const v3 c = {q.x * dot * 2.0f, q.y * dot * 2.0f, q.z * dot * 2.0f};
+  return {a.x + b.x + c.x, a.y + b.y + c.y, a.z + b.z + c.z};
+}
+
+// torch_utils.py:294-307 quat_to_tan_norm: rotate x-axis and z-axis.
+__device__ __forceinline__ void quat_to_tan_norm(q4 q, float out[6]) {
+  const v3 t = my_quat_rotate(q, v3{1.0f, 0.0f, 0.0f});
+  const v3 n = my_quat_rotate(q, v3{0.0f, 0.0f, 1.0f});
+  out[0] = t.x; out[1] = t.y; out[2] = t.z;
+  out[3] = n.x; out[4] = n.y; out[5] = n.z;
+}
+
+// torch_utils.py:50-51
+__device__ __forceinline__ float normalize_angle(float x) { return atan2f(sinf(x), cosf(x)); }
+
+// torch_utils.py:86-106 quat_to_angle_axis: NaN lanes masked exactly like torch.where.
+__device__ __forceinline__ float quat_angle_masked(q4 q, float *sin_theta_out) {
+  const float sin_theta = sqrtf(1.0f - q.w * q.w);
+  *sin_theta_out = sin_theta;
+  if (!(fabsf(sin_theta) > 1e-5f)) return 0.0f;
+  return normalize_angle(2.0f * acosf(q.w));
+}
+
+__device__ __forceinline__ v3 quat_to_exp_map(q4 q) {
+  float s;
+  const float angle = quat_angle_masked(q, &s);
+  if (!(fabsf(s) > 1e-5f)) return {0.0f, 0.0f, 0.0f};  // angle 0 times default axis (0,0,1)
+  const v3 axis = {q.x / s, q.y / s, q.z / s};
+  return {angle * axis.x, angle * axis.y, angle * axis.z};
+}
+
+// torch_utils.py:110-131 slerp (branch order reproduces the two torch.where overrides).
+__device__ __forceinline__ q4 slerp(q4 q0, q4 q1, float t) {
+  float c = q0.x * q1.x + q0.y * q1.y + q0.z * q1.z + q0.w * q1.w;
+  if (c < 0.0f) q1 = {-q1.x, -q1.y, -q1.z, -q1.w};
+  c = fabsf(c);
+  if (fabsf(c) >= 1.0f) return q0;
+  const float sin_half = sqrtf(1.0f - c * c);
+  if (fabsf(sin_half) < 0.001f)
+    return {0.5f * q0.x + 0.5f * q1.x, 0.5f * q0.y + 0.5f * q1.y, 0.5f * q0.z + 0.5f * q1.z,
+            0.5f * q0.w + 0.5f * q1.w};
+  const float half = acosf(c);
+  const float ra = sinf((1.0f - t) * half) / sin_half;
+  const float rb = sinf(t * half) / sin_half;
+  return {ra * q0.x + rb * q1.x, ra * q0.y + rb * q1.y, ra * q0.z + rb * q1.z, ra * q0.w + rb * q1.w};
+}
+
+// torch_utils.py:354-358 quat_from_angle_axis with axis = +z (normalize(z) == z exactly).
+__device__ __forceinline__ q4 quat_from_angle_z(float angle) {
+  const float theta = angle / 2.0f;
+  const float s = sinf(theta);
+  const q4 q = {0.0f * s, 0.0f * s, 1.0f * s, cosf(theta)};
+  return quat_unit(q);
+}
+
+// torch_utils.py:334-365 exp_map_to_quat
+__device__ __forceinline__ q4 exp_map_to_quat(v3 e) {
+  float angle = norm3(e);
+  v3 axis = {e.x / angle, e.y / angle, e.z / angle};
+  angle = normalize_angle(angle);
+  if (!(fabsf(angle) > 1e-5f)) {
+    angle = 0.0f;
+    axis = {0.0f, 0.0f, 1.0f};
+  }
+  const float theta = angle / 2.0f;
+  float n = norm3(axis);
+  n = n < 1e-9f ? 1e-9f : n;
+  const float s = sinf(theta);
+  const q4 q = {axis.x / n * s, axis.y / n * s, axis.z / n * s, cosf(theta)};
+  return quat_unit(q);
+}
+
+// torch_utils.py:369-408 heading from the rotated x-axis; returns heading angle.
+__device__ __forceinline__ float calc_heading(q4 q) {
+  const v3 d = my_quat_rotate(q, v3{1.0f, 0.0f, 0.0f});
+  return atan2f(d.y, d.x);
+}
+
+// torch_utils.py:219-228 quat_angle_axis (float64 use at load time): angle in [0, pi].
+__device__ __forceinline__ void quat_angle_axis_d(Q4<double> x, double *angle, V3<double> *axis) {
+  double s = 2.0 * (x.w * x.w) - 1.0;
+  s = s < -1.0 ? -1.0 : (s > 1.0 ? 1.0 : s);
+  *angle = acos(s);
+  double n = norm3(V3<double>{x.x, x.y, x.z});
+  n = n < 1e-9 ? 1e-9 : n;
+  *axis = {x.x / n, x.y / n, x.z / n};
+}
+
+// Counter-based RNG (splitmix64 finaliser): uniform float in [0, 1) with 24 random bits.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float uniform01(unsigned long long seed, unsigned long long counter,
+                                           unsigned long long idx) {
+  const unsigned long long h = mix64(seed ^ mix64(counter * 0xD1B54A32D192ED03ull ^ mix64(idx)));
+  return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ float normal01(unsigned long long seed, unsigned long long counter,
+                                          unsigned long long idx) {
+  const float u1 = uniform01(seed, counter, 2 * idx) + (1.0f / 33554432.0f);
+  const float u2 = uniform01(seed, counter, 2 * idx + 1);
+  return sqrtf(-2.0f * logf(u1)) * cosf(6.28318530718f * u2);
+}
+
+}  // namespace phc

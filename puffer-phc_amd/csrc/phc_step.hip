@@ -1,0 +1,444 @@
+// phc_step.hip — per-step env kernels: motion state, fused obs/reward/reset (+PufferEnv
+// bookkeeping), reset of terminated envs, action->PD, and the replay physics stand-in.
+//
+// Work decomposition (MI355X): one 32-lane half-wave per env, lane b = body b (24 of 32
+// lanes active), 8 envs per 256-thread workgroup.  Per-env reductions (reward means,
+// termination any/mean, power) are 5-step butterflies inside the half-wave; the only
+// cross-env traffic is the per-workgroup logging row.  Each env reads its 24 rigid-body
+// records and the 4 reference frame rows it blends (t and t+dt) straight from HBM and
+// writes its 934-float observation row once.
+#include "phc_common.h"
+
+namespace phc {
+
+struct StepConsts {
+  float dt;
+  float k_pos, k_rot, k_vel, k_ang;
+  float w_pos, w_rot, w_vel, w_ang;
+  float power_coef;
+  int use_power;
+  int enable_et;
+  int use_mean;
+  unsigned reset_mask;
+  float td[kBodies];
+  float td_first;     // termination_distance[first reset body] (eval mean rule)
+  float inv_nreset;   // 1 / number of reset bodies
+};
+
+static StepConsts make_consts(const phc_step_params *p) {
+  StepConsts c;
+  c.dt = p->dt;
+  c.k_pos = p->k_pos; c.k_rot = p->k_rot; c.k_vel = p->k_vel; c.k_ang = p->k_ang_vel;
+  c.w_pos = p->w_pos; c.w_rot = p->w_rot; c.w_vel = p->w_vel; c.w_ang = p->w_ang_vel;
+  c.power_coef = p->power_coef;
+  c.use_power = p->use_power_reward;
+  c.enable_et = p->enable_early_termination;
+  c.use_mean = p->use_mean_termination;
+  c.reset_mask = p->reset_body_mask & 0xFFFFFFu;
+  int n = 0, first = -1;
+  for (int b = 0; b < kBodies; ++b) {
+    c.td[b] = p->termination_distance[b];
+    if (c.reset_mask & (1u << b)) {
+      if (first < 0) first = b;
+      ++n;
+    }
+  }
+  c.td_first = first >= 0 ? p->termination_distance[first] : 0.0f;
+  c.inv_nreset = n > 0 ? 1.0f / (float)n : 0.0f;
+  return c;
+}
+
+struct EnvView {
+  int64_t n;
+  float *rb;
+  float *root;
+  float *dof_state;
+  const float *dof_force;
+  int16_t *progress;
+  int64_t *motion_ids;
+  float *start;
+  float *start_off;
+  float *goff;
+  float *obs;
+  float *rew;
+  float *raw;
+  uint8_t *reset;
+  uint8_t *term;
+  uint8_t *terminals;
+  uint8_t *truncs;
+  uint8_t *masks;
+  float *ep_ret;
+  int32_t *ep_len;
+  double *stats;
+};
+
+static EnvView env_view(const phc_env_buffers *e) {
+  return {e->num_envs, e->rigid_body_state, e->root_state, e->dof_state, e->dof_force, e->progress,
+          e->motion_ids, e->motion_start_times, e->motion_start_offset, e->global_offset, e->obs, e->rew,
+          e->reward_raw, e->reset, e->terminate, e->terminals, e->truncations, e->masks, e->episode_return,
+          e->episode_length, e->stats};
+}
+
+// ------------------------------------------------------------ motion state --
+__global__ __launch_bounds__(kBlock) void k_motion_state(LibView l, const int64_t *__restrict__ ids,
+                                                         const float *__restrict__ times,
+                                                         const float *__restrict__ offset, int64_t n,
+                                                         float *__restrict__ body, float *__restrict__ dof_pos,
+                                                         float *__restrict__ dof_vel) {
+  const int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kGroup;
+  const int b = threadIdx.x % kGroup;
+  if (i >= n || b >= kBodies) return;
+  const MotionScalars m = load_motion(l, ids[i]);
+  const Blend bl = frame_blend(times[i], m);
+  v3 off;
+  if (offset) off = {offset[3 * i], offset[3 * i + 1], offset[3 * i + 2]};
+  const BodyRec r = ref_body(l.frames, bl, b, offset ? &off : nullptr);
+  store_body(body + (i * kBodies + b) * kRec, r);
+  if (b >= 1) {
+    if (dof_pos) {
+      const v3 d = ref_dof_pos(l.local_rot, bl, b);
+      float *q = dof_pos + i * PHC_NUM_DOF + 3 * (b - 1);
+      q[0] = d.x; q[1] = d.y; q[2] = d.z;
+    }
+    if (dof_vel) {
+      const v3 d = ref_dof_vel(l.dof_vel, bl, b);
+      float *q = dof_vel + i * PHC_NUM_DOF + 3 * (b - 1);
+      q[0] = d.x; q[1] = d.y; q[2] = d.z;
+    }
+  }
+}
+
+// --------------------------------------------------------------- env step --
+// Post-physics part of HumanoidPHC.step (humanoid_phc.py:136-146):
+//   progress += 1; reward with the reference at t (:1228-1303); reset at t (:1311-1333);
+//   obs with the reference at t+dt (:935-959, 1061-1112); then PHCPufferEnv.step's
+//   terminals/truncations/masks and episode return/length (clean_pufferl/env.py:103-140).
+__global__ __launch_bounds__(kBlock) void k_env_step(EnvView e, LibView l, StepConsts c) {
+  __shared__ double sh_stats[kEnvsPerBlock][10];
+  const int g = threadIdx.x / kGroup;
+  const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + g;
+  const int lane = threadIdx.x % kGroup;
+  const bool valid = env < e.n;
+  const bool active = lane < kBodies;
+  const int b = active ? lane : 0;
+  const int64_t ei = valid ? env : 0;
+
+  // per-env scalars (broadcast loads: every lane of the half-wave reads the same word)
+  const int prog = (int)e.progress[ei] + 1;
+  const float st = e.start[ei];
+  const float so = e.start_off[ei];
+  const v3 go = {e.goff[3 * ei], e.goff[3 * ei + 1], e.goff[3 * ei + 2]};
+  const MotionScalars m = load_motion(l, e.motion_ids[ei]);
+  const float t = (float)prog * c.dt + st + so;
+  const float t1 = (float)(prog + 1) * c.dt + st + so;
+  const Blend bl0 = frame_blend(t, m);
+  const Blend bl1 = frame_blend(t1, m);
+
+  const BodyRec s = load_body(e.rb + (ei * kBodies + b) * kRec);
+  const BodyRec ref0 = ref_body(l.frames, bl0, b, &go);
+  const BodyRec ref1 = ref_body(l.frames, bl1, b, &go);
+
+  // root (body 0) broadcast from lane 0
+  const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
+  const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
+
+  // ---- reward terms (common.py:271-322) ----
+  const v3 dp = vsub(ref0.p, s.p);
+  float e_pos = dp.x * dp.x;
+  e_pos = e_pos + dp.y * dp.y;
+  e_pos = (e_pos + dp.z * dp.z) / 3.0f;
+  float sin_t;
+  const float ang = quat_angle_masked(quat_mul(ref0.r, quat_conj(s.r)), &sin_t);
+  float e_rot = ang * ang;
+  const v3 dv = vsub(ref0.v, s.v);
+  float e_vel = dv.x * dv.x;
+  e_vel = e_vel + dv.y * dv.y;
+  e_vel = (e_vel + dv.z * dv.z) / 3.0f;
+  const v3 da = vsub(ref0.av, s.av);
+  float e_ang = da.x * da.x;
+  e_ang = e_ang + da.y * da.y;
+  e_ang = (e_ang + da.z * da.z) / 3.0f;
+  // ---- termination distance (common.py:326-364) ----
+  const float dist = norm3(vsub(s.p, ref0.p));
+  const bool counted = active && ((c.reset_mask >> b) & 1u);
+  float fall = (counted && dist > c.td[b]) ? 1.0f : 0.0f;
+  float dsum = counted ? dist : 0.0f;
+  // ---- power (humanoid_phc.py:1295-1303): lane j < 23 owns dofs 3j..3j+2 ----
+  float pw = 0.0f;
+  if (lane < kBodies - 1) {
+    const float *f = e.dof_force + ei * PHC_NUM_DOF + 3 * lane;
+    const float *ds = e.dof_state + (ei * PHC_NUM_DOF + 3 * lane) * 2;
+    pw = fabsf(f[0] * ds[1]);
+    pw = pw + fabsf(f[1] * ds[3]);
+    pw = pw + fabsf(f[2] * ds[5]);
+  }
+  if (!active) e_pos = e_rot = e_vel = e_ang = 0.0f;
+  e_pos = group_sum(e_pos);
+  e_rot = group_sum(e_rot);
+  e_vel = group_sum(e_vel);
+  e_ang = group_sum(e_ang);
+  fall = group_sum(fall);
+  dsum = group_sum(dsum);
+  pw = group_sum(pw);
+
+  // ---- observation at t+dt ----
+  const float hd = calc_heading(root_r);
+  const q4 hinv = quat_from_angle_z(-hd);
+  const q4 hrot = quat_from_angle_z(hd);
+  if (valid && active) write_obs_body(e.obs + ei * kObs, b, s, root_p, hinv, hrot, ref1);
+
+  double st_row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (valid && lane == 0) {
+    const float inv24 = 1.0f / (float)kBodies;
+    const float r_pos = expf(-c.k_pos * (e_pos / (float)kBodies));
+    const float r_rot = expf(-c.k_rot * (e_rot / (float)kBodies));
+    const float r_vel = expf(-c.k_vel * (e_vel / (float)kBodies));
+    const float r_ang = expf(-c.k_ang * (e_ang / (float)kBodies));
+    (void)inv24;
+    float rew = c.w_pos * r_pos + c.w_rot * r_rot + c.w_vel * r_vel + c.w_ang * r_ang;
+    float pr = 0.0f;
+    if (c.use_power) {
+      pr = -c.power_coef * pw;
+      if (prog <= 3) pr = 0.0f;
+      rew = rew + pr;
+    }
+    e.rew[ei] = rew;
+    float *raw = e.raw + ei * 5;
+    raw[0] = r_pos; raw[1] = r_rot; raw[2] = r_vel; raw[3] = r_ang; raw[4] = pr;
+
+    const bool pass_time = t >= m.len;
+    bool terminated = false;
+    if (c.enable_et) {
+      const bool fallen = c.use_mean ? (dsum * c.inv_nreset > c.td_first) : (fall > 0.0f);
+      terminated = fallen && (prog > 1);
+    }
+    const bool reset = pass_time || terminated;
+    e.progress[ei] = (int16_t)prog;
+    e.reset[ei] = reset;
+    e.term[ei] = terminated;
+    // PHCPufferEnv.step bookkeeping
+    const bool trunc = reset && !terminated;
+    if (e.terminals) e.terminals[ei] = terminated;
+    if (e.truncs) e.truncs[ei] = trunc;
+    if (e.masks) e.masks[ei] = !trunc;
+    if (e.ep_ret) {
+      float ret = e.ep_ret[ei];
+      int len = e.ep_len[ei];
+      if (reset) {
+        st_row[5] = ret;
+        st_row[6] = len;
+        st_row[7] = 1.0;
+        st_row[8] = trunc ? 1.0 : 0.0;
+        st_row[9] = terminated ? 1.0 : 0.0;
+        ret = 0.0f;
+        len = 0;
+      }
+      e.ep_ret[ei] = ret + rew;
+      e.ep_len[ei] = len + 1;
+    }
+    st_row[0] = r_pos; st_row[1] = r_rot; st_row[2] = r_vel; st_row[3] = r_ang; st_row[4] = pr;
+  }
+  if (e.stats) {
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 10; ++k) sh_stats[g][k] = st_row[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 10) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < kEnvsPerBlock; ++j) acc += sh_stats[j][threadIdx.x];
+      e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] += acc;
+    }
+  }
+}
+
+// ------------------------------------------------------------- env reset --
+// HumanoidPHC.reset(env_ids) for StateInit.Random: sample_time_interval, reference state
+// with the env's previous global offset written into the sim buffers (_set_env_state),
+// counters cleared (_reset_env_tensors), offsets cleared (_reset_ref_state_init), then the
+// env's observation at progress 0 (obs time dt + start).
+__global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, StepConsts c,
+                                                       const uint8_t *__restrict__ mask,
+                                                       const float *__restrict__ phase, unsigned long long seed,
+                                                       unsigned long long counter) {
+  const int64_t env = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kGroup;
+  const int lane = threadIdx.x % kGroup;
+  if (env >= e.n) return;
+  if (!(mask ? mask[env] : e.reset[env])) return;  // uniform per half-wave
+  const bool active = lane < kBodies;
+  const int b = active ? lane : 0;
+
+  const int64_t mid = e.motion_ids[env];
+  const MotionScalars m = load_motion(l, mid);
+  const float u = phase ? phase[env] : uniform01(seed, counter, (unsigned long long)env);
+  const float fps_step = 1.0f / 30.0f;  // motion_lib.py:532 curr_fps
+  const float mt = (float)(int64_t)((u * m.len) / fps_step) * fps_step;
+  const v3 go_old = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
+  const Blend bl = frame_blend(mt, m);
+  const BodyRec s = ref_body(l.frames, bl, b, &go_old);
+  if (active) {
+    store_body(e.rb + (env * kBodies + b) * kRec, s);
+    if (b == 0 && e.root) store_body(e.root + env * kRec, s);
+    if (b >= 1) {
+      const v3 dp = ref_dof_pos(l.local_rot, bl, b);
+      const v3 dv = ref_dof_vel(l.dof_vel, bl, b);
+      float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+      d[0] = dp.x; d[1] = dv.x; d[2] = dp.y; d[3] = dv.y; d[4] = dp.z; d[5] = dv.z;
+    }
+  }
+  // observation of the reset env: progress 0, start = mt, offsets 0
+  const float t1 = (float)(0 + 1) * c.dt + mt + 0.0f;
+  const Blend bl1 = frame_blend(t1, m);
+  const v3 zero = {0.0f, 0.0f, 0.0f};
+  const BodyRec ref1 = ref_body(l.frames, bl1, b, &zero);
+  const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
+  const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
+  const float hd = calc_heading(root_r);
+  const q4 hinv = quat_from_angle_z(-hd);
+  const q4 hrot = quat_from_angle_z(hd);
+  if (active) write_obs_body(e.obs + env * kObs, b, s, root_p, hinv, hrot, ref1);
+  if (lane == 0) {
+    e.progress[env] = 0;
+    e.reset[env] = 0;
+    e.term[env] = 0;
+    e.goff[3 * env] = 0.0f; e.goff[3 * env + 1] = 0.0f; e.goff[3 * env + 2] = 0.0f;
+    e.start[env] = mt;
+    e.start_off[env] = 0.0f;
+  }
+}
+
+// --------------------------------------------------------- physics stand-in --
+__global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l, StepConsts c, float sigma,
+                                                           float force_scale, unsigned long long seed,
+                                                           unsigned long long counter) {
+  const int64_t env = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kGroup;
+  const int lane = threadIdx.x % kGroup;
+  if (env >= e.n || lane >= kBodies) return;
+  const int b = lane;
+  const int prog = (int)e.progress[env] + 1;
+  const float t = (float)prog * c.dt + e.start[env] + e.start_off[env];
+  const MotionScalars m = load_motion(l, e.motion_ids[env]);
+  const Blend bl = frame_blend(t, m);
+  const v3 go = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
+  BodyRec s = ref_body(l.frames, bl, b, &go);
+  const unsigned long long base = (unsigned long long)(env * kBodies + b) * 16ull;
+  s.p.x += sigma * normal01(seed, counter, base + 0);
+  s.p.y += sigma * normal01(seed, counter, base + 1);
+  s.p.z += sigma * normal01(seed, counter, base + 2);
+  q4 r = {s.r.x + sigma * normal01(seed, counter, base + 3), s.r.y + sigma * normal01(seed, counter, base + 4),
+          s.r.z + sigma * normal01(seed, counter, base + 5), s.r.w + sigma * normal01(seed, counter, base + 6)};
+  s.r = quat_unit(r);
+  s.v.x += 10.0f * sigma * normal01(seed, counter, base + 7);
+  s.v.y += 10.0f * sigma * normal01(seed, counter, base + 8);
+  s.v.z += 10.0f * sigma * normal01(seed, counter, base + 9);
+  s.av.x += 20.0f * sigma * normal01(seed, counter, base + 10);
+  s.av.y += 20.0f * sigma * normal01(seed, counter, base + 11);
+  s.av.z += 20.0f * sigma * normal01(seed, counter, base + 12);
+  store_body(e.rb + (env * kBodies + b) * kRec, s);
+  if (b >= 1) {
+    const v3 dv = ref_dof_vel(l.dof_vel, bl, b);
+    float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+    d[1] = dv.x + 10.0f * sigma * normal01(seed, counter, base + 13);
+    d[3] = dv.y + 10.0f * sigma * normal01(seed, counter, base + 14);
+    d[5] = dv.z + 10.0f * sigma * normal01(seed, counter, base + 15);
+    float *f = const_cast<float *>(e.dof_force) + env * PHC_NUM_DOF + 3 * (b - 1);
+    f[0] = force_scale * normal01(seed ^ 0xF0F0ull, counter, base + 0);
+    f[1] = force_scale * normal01(seed ^ 0xF0F0ull, counter, base + 1);
+    f[2] = force_scale * normal01(seed ^ 0xF0F0ull, counter, base + 2);
+  }
+}
+
+// --------------------------------------------------------------- actions --
+__global__ __launch_bounds__(kBlock) void k_actions_to_pd(const float *__restrict__ a, float *__restrict__ pd,
+                                                          int64_t total, const float *__restrict__ off,
+                                                          const float *__restrict__ scale,
+                                                          const uint8_t *__restrict__ frozen) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= total) return;
+  const int d = (int)(i % PHC_NUM_DOF);
+  float x = a[i];
+  x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+  pd[i] = (frozen && frozen[d]) ? 0.0f : off[d] + scale[d] * x;
+}
+
+static int grid_envs(int64_t n) { return (int)((n + kEnvsPerBlock - 1) / kEnvsPerBlock); }
+
+static int check_lib(const phc_motion_lib *l) {
+  PHC_REQUIRE(l && l->frames && l->motion_len && l->motion_dt && l->num_frames && l->length_starts,
+              "motion lib: null tensor");
+  PHC_REQUIRE(l->num_motions > 0, "motion lib: no motions");
+  return PHC_OK;
+}
+
+static int check_env(const phc_env_buffers *e) {
+  PHC_REQUIRE(e && e->num_envs > 0, "env: num_envs must be > 0");
+  PHC_REQUIRE(e->rigid_body_state && e->dof_state && e->dof_force && e->progress && e->motion_ids &&
+                  e->motion_start_times && e->motion_start_offset && e->global_offset && e->obs && e->rew &&
+                  e->reward_raw && e->reset && e->terminate,
+              "env: null buffer");
+  PHC_REQUIRE((e->episode_return == nullptr) == (e->episode_length == nullptr),
+              "env: episode_return and episode_length must both be set or both null");
+  return PHC_OK;
+}
+
+}  // namespace phc
+
+using namespace phc;
+
+extern "C" int64_t phc_stats_blocks(int64_t num_envs) { return num_envs <= 0 ? 0 : grid_envs(num_envs); }
+
+extern "C" int phc_motion_state(const phc_motion_lib *lib, const int64_t *ids, const float *times,
+                                const float *offset, int64_t n, phc_ref_state *out, void *stream) {
+  if (int rc = check_lib(lib)) return rc;
+  PHC_REQUIRE(out && out->body && ids && times, "motion_state: null argument");
+  if (n <= 0) return PHC_OK;
+  hipLaunchKernelGGL(k_motion_state, dim3(grid_envs(n)), dim3(kBlock), 0, as_stream(stream), lib_view(lib), ids,
+                     times, offset, n, out->body, out->dof_pos, out->dof_vel);
+  return check_launch("motion_state");
+}
+
+extern "C" int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                            void *stream) {
+  if (int rc = check_env(env)) return rc;
+  if (int rc = check_lib(lib)) return rc;
+  PHC_REQUIRE(p && p->dt > 0.0f, "env_step: bad params");
+  hipLaunchKernelGGL(k_env_step, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
+                     env_view(env), lib_view(lib), make_consts(p));
+  return check_launch("env_step");
+}
+
+extern "C" int phc_reset_envs(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                              const uint8_t *mask, const float *phase, uint64_t seed, uint64_t counter,
+                              void *stream) {
+  if (int rc = check_env(env)) return rc;
+  if (int rc = check_lib(lib)) return rc;
+  PHC_REQUIRE(lib->local_rot && lib->dof_vel, "reset_envs: motion lib needs local_rot and dof_vel");
+  PHC_REQUIRE(p && p->dt > 0.0f, "reset_envs: bad params");
+  hipLaunchKernelGGL(k_reset_envs, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
+                     env_view(env), lib_view(lib), make_consts(p), mask, phase, (unsigned long long)seed,
+                     (unsigned long long)counter);
+  return check_launch("reset_envs");
+}
+
+extern "C" int phc_physics_replay(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                                  float pos_sigma, float force_scale, uint64_t seed, uint64_t counter,
+                                  void *stream) {
+  if (int rc = check_env(env)) return rc;
+  if (int rc = check_lib(lib)) return rc;
+  PHC_REQUIRE(lib->dof_vel, "physics_replay: motion lib needs dof_vel");
+  hipLaunchKernelGGL(k_physics_replay, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
+                     env_view(env), lib_view(lib), make_consts(p), pos_sigma, force_scale,
+                     (unsigned long long)seed, (unsigned long long)counter);
+  return check_launch("physics_replay");
+}
+
+extern "C" int phc_actions_to_pd(const float *actions, float *pd, int64_t n, const float *offset,
+                                 const float *scale, const uint8_t *frozen, void *stream) {
+  PHC_REQUIRE(actions && pd && offset && scale, "actions_to_pd: null argument");
+  if (n <= 0) return PHC_OK;
+  const int64_t total = n * PHC_NUM_DOF;
+  hipLaunchKernelGGL(k_actions_to_pd, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     as_stream(stream), actions, pd, total, offset, scale, frozen);
+  return check_launch("actions_to_pd");
+}
