@@ -84,6 +84,7 @@ typedef struct phc_env_buffers {
   float *episode_return;      /* [N] */
   int32_t *episode_length;    /* [N] */
   double *stats;              /* [phc_stats_blocks(N), PHC_STATS_SLOTS] per-block log sums */
+  uint32_t *rng_counter;      /* [N] per-env counter of the counter-based RNG (nullable) */
 } phc_env_buffers;
 
 /* Step constants: RewardConfig (config.py:23-36), EnvConfig power coef / early termination
@@ -98,6 +99,8 @@ typedef struct phc_step_params {
   int32_t use_mean_termination;  /* eval mode: mean body distance vs termination_distance[first] */
   uint32_t reset_body_mask;      /* bit b set = body b counts for termination */
   float termination_distance[PHC_NUM_BODIES];
+  int32_t auto_reset;            /* phc_env_step also re-initialises envs that reset (R15 fused) */
+  uint64_t seed;                 /* RNG seed of the reset time draw (with env->rng_counter) */
 } phc_step_params;
 
 /* Number of per-block statistics rows phc_env_step writes for `num_envs` envs. */
@@ -109,7 +112,11 @@ int phc_motion_state(const phc_motion_lib *lib, const int64_t *motion_ids, const
 
 /* R6,R7,R9-R12,R14 fused: HumanoidPHC.step post-physics (humanoid_phc.py:136-146 ->
  * _compute_reward :1228-1303, _compute_reset :1311-1333, _compute_observations :935-959)
- * plus PHCPufferEnv.step bookkeeping (clean_pufferl/env.py:103-140).  Increments progress. */
+ * plus PHCPufferEnv.step bookkeeping (clean_pufferl/env.py:103-140).  Increments progress.
+ * With p->auto_reset, envs whose reset flag comes up are re-initialised in the same launch
+ * exactly as phc_reset_envs would (PHCPufferEnv.step's env.reset(reset_indices), :114-116):
+ * their obs row is the post-reset observation and reset/terminate read back as 0, while
+ * terminals/truncations/masks/episode stats keep this step's outcome. */
 int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
                  void *stream);
 

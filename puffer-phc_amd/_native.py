@@ -42,7 +42,7 @@ class EnvBuffersC(ctypes.Structure):
                 ("motion_start_offset", c_vp), ("global_offset", c_vp), ("obs", c_vp), ("rew", c_vp),
                 ("reward_raw", c_vp), ("reset", c_vp), ("terminate", c_vp), ("terminals", c_vp),
                 ("truncations", c_vp), ("masks", c_vp), ("episode_return", c_vp), ("episode_length", c_vp),
-                ("stats", c_vp)]
+                ("stats", c_vp), ("rng_counter", c_vp)]
 
 
 class StepParamsC(ctypes.Structure):
@@ -51,7 +51,8 @@ class StepParamsC(ctypes.Structure):
                 ("w_rot", ctypes.c_float), ("w_vel", ctypes.c_float), ("w_ang_vel", ctypes.c_float),
                 ("power_coef", ctypes.c_float), ("use_power_reward", ctypes.c_int32),
                 ("enable_early_termination", ctypes.c_int32), ("use_mean_termination", ctypes.c_int32),
-                ("reset_body_mask", ctypes.c_uint32), ("termination_distance", ctypes.c_float * NUM_BODIES)]
+                ("reset_body_mask", ctypes.c_uint32), ("termination_distance", ctypes.c_float * NUM_BODIES),
+                ("auto_reset", ctypes.c_int32), ("seed", ctypes.c_uint64)]
 
 
 _EXPORTS = {
@@ -149,8 +150,10 @@ def motion_lib_struct(frames, local_rot, dof_vel, motion_len, motion_dt, num_fra
 
 
 def step_params_struct(dt, reward, power_coef, use_power_reward, enable_early_termination, use_mean,
-                       reset_body_ids, termination_distances):
+                       reset_body_ids, termination_distances, auto_reset=False, seed=0):
     p = StepParamsC()
+    p.auto_reset = int(bool(auto_reset))
+    p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     p.dt = float(dt)
     p.k_pos, p.k_rot, p.k_vel, p.k_ang_vel = reward.k_pos, reward.k_rot, reward.k_vel, reward.k_ang_vel
     p.w_pos, p.w_rot, p.w_vel, p.w_ang_vel = reward.w_pos, reward.w_rot, reward.w_vel, reward.w_ang_vel
@@ -172,7 +175,7 @@ def step_params_struct(dt, reward, power_coef, use_power_reward, enable_early_te
 
 def env_struct(num_envs, rigid_body_state, root_state, dof_state, dof_force, progress, motion_ids, start_times,
                start_offset, global_offset, obs, rew, reward_raw, reset, terminate, terminals=None, truncations=None,
-               masks=None, episode_return=None, episode_length=None, stats=None):
+               masks=None, episode_return=None, episode_length=None, stats=None, rng_counter=None):
     N = num_envs
     u8 = torch.uint8
     return EnvBuffersC(
@@ -197,6 +200,7 @@ def env_struct(num_envs, rigid_body_state, root_state, dof_state, dof_force, pro
         _ptr(episode_return, torch.float32, (N,), "episode_return", nullable=True),
         _ptr(episode_length, torch.int32, (N,), "episode_length", nullable=True),
         _ptr(stats, torch.float64, (lib().phc_stats_blocks(N), STATS_SLOTS), "stats", nullable=True),
+        _ptr(rng_counter, torch.int32, (N,), "rng_counter", nullable=True),
     )
 
 

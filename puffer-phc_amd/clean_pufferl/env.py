@@ -78,10 +78,11 @@ class PHCPufferEnv:
             self.actions.copy_(torch.from_numpy(actions))
         elif actions.data_ptr() != self.actions.data_ptr():
             self.actions.copy_(actions)
-        # clipping happens inside phc_actions_to_pd (cfg.clip_actions is always honoured)
-        self.env.step(self.actions)
-        rew = self.rewards.clone()
-        self.env.reset_done()
+        # clipping happens inside phc_actions_to_pd (cfg.clip_actions is always honoured);
+        # the fused kernel also performs the env.reset(reset_indices) of :114-116, which leaves
+        # rew_buf untouched, so no defensive copy of the rewards is needed
+        self.env.step(self.actions, auto_reset=True)
+        rew = self.rewards
         self.amp_obs = self.env.amp_obs if self.cfg.use_amp_obs else None
         info = []
         self.tick += 1

@@ -1,5 +1,6 @@
 // phc_step.hip — per-step env kernels: motion state, fused obs/reward/reset (+PufferEnv
-// bookkeeping), reset of terminated envs, action->PD, and the replay physics stand-in.
+// bookkeeping, + optional in-launch re-initialisation of envs that reset), explicit env
+// reset, action->PD, and the replay physics stand-in.
 //
 // Work decomposition (MI355X): one 32-lane half-wave per env, lane b = body b (24 of 32
 // lanes active), 8 envs per 256-thread workgroup.  Per-env reductions (reward means,
@@ -23,6 +24,7 @@ struct StepConsts {
   float td[kBodies];
   float td_first;     // termination_distance[first reset body] (eval mean rule)
   float inv_nreset;   // 1 / number of reset bodies
+  unsigned long long seed;
 };
 
 static StepConsts make_consts(const phc_step_params *p) {
@@ -45,6 +47,7 @@ static StepConsts make_consts(const phc_step_params *p) {
   }
   c.td_first = first >= 0 ? p->termination_distance[first] : 0.0f;
   c.inv_nreset = n > 0 ? 1.0f / (float)n : 0.0f;
+  c.seed = p->seed;
   return c;
 }
 
@@ -70,13 +73,14 @@ struct EnvView {
   float *ep_ret;
   int32_t *ep_len;
   double *stats;
+  uint32_t *rng;
 };
 
 static EnvView env_view(const phc_env_buffers *e) {
   return {e->num_envs, e->rigid_body_state, e->root_state, e->dof_state, e->dof_force, e->progress,
           e->motion_ids, e->motion_start_times, e->motion_start_offset, e->global_offset, e->obs, e->rew,
           e->reward_raw, e->reset, e->terminate, e->terminals, e->truncations, e->masks, e->episode_return,
-          e->episode_length, e->stats};
+          e->episode_length, e->stats, e->rng_counter};
 }
 
 // ------------------------------------------------------------ motion state --
@@ -108,11 +112,91 @@ __global__ __launch_bounds__(kBlock) void k_motion_state(LibView l, const int64_
   }
 }
 
+// ------------------------------------------------------------- env reset --
+// HumanoidPHC.reset(env_ids) for one env (StateInit.Random): sample_time_interval
+// (motion_lib.py:526-535), the reference state with the env's previous global offset written
+// into the sim buffers (_set_env_state, humanoid_phc.py:899-929), counters cleared
+// (_reset_env_tensors :745-778) and offsets cleared (_reset_ref_state_init :692-729).
+// Returns this lane's new rigid-body record; the caller then computes the obs at dt + mt.
+__device__ __forceinline__ BodyRec reset_env_state(const EnvView &e, const LibView &l, int64_t env, int lane,
+                                                   const MotionScalars &m, float u, float *mt_out) {
+  const bool active = lane < kBodies;
+  const int b = active ? lane : 0;
+  const float fps_step = 1.0f / 30.0f;  // motion_lib.py:532 curr_fps
+  const float mt = (float)(int64_t)((u * m.len) / fps_step) * fps_step;
+  const v3 go_old = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
+  const Blend bl = frame_blend(mt, m);
+  const BodyRec s = ref_body(l.frames, bl, b, &go_old);
+  if (active) {
+    store_body(e.rb + (env * kBodies + b) * kRec, s);
+    if (b == 0 && e.root) store_body(e.root + env * kRec, s);
+    if (b >= 1) {
+      const v3 dp = ref_dof_pos(l.local_rot, bl, b);
+      const v3 dv = ref_dof_vel(l.dof_vel, bl, b);
+      float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+      d[0] = dp.x; d[1] = dv.x; d[2] = dp.y; d[3] = dv.y; d[4] = dp.z; d[5] = dv.z;
+    }
+  }
+  *mt_out = mt;
+  return s;
+}
+
+__device__ __forceinline__ void reset_env_counters(const EnvView &e, int64_t env, float mt) {
+  e.progress[env] = 0;
+  e.reset[env] = 0;
+  e.term[env] = 0;
+  e.goff[3 * env] = 0.0f; e.goff[3 * env + 1] = 0.0f; e.goff[3 * env + 2] = 0.0f;
+  e.start[env] = mt;
+  e.start_off[env] = 0.0f;
+}
+
+__device__ __forceinline__ float reset_draw(const EnvView &e, int64_t env, unsigned long long seed,
+                                            unsigned long long counter) {
+  const unsigned long long ctr = e.rng ? (unsigned long long)e.rng[env] : counter;
+  return uniform01(seed, ctr, (unsigned long long)env);
+}
+
+// Observation of one env from its sim state (this lane's body) and the reference at `t1`.
+__device__ __forceinline__ void env_obs(const EnvView &e, const LibView &l, int64_t env, int lane,
+                                        const MotionScalars &m, const BodyRec &s, float t1, v3 off, bool write) {
+  const bool active = lane < kBodies;
+  const int b = active ? lane : 0;
+  const BodyRec ref1 = ref_body(l.frames, frame_blend(t1, m), b, &off);
+  const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
+  const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
+  const float hd = calc_heading(root_r);
+  const q4 hinv = quat_from_angle_z(-hd);
+  const q4 hrot = quat_from_angle_z(hd);
+  if (write && active) write_obs_body(e.obs + env * kObs, b, s, root_p, hinv, hrot, ref1);
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, StepConsts c,
+                                                       const uint8_t *__restrict__ mask,
+                                                       const float *__restrict__ phase, unsigned long long seed,
+                                                       unsigned long long counter) {
+  const int64_t env = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kGroup;
+  const int lane = threadIdx.x % kGroup;
+  if (env >= e.n) return;
+  if (!(mask ? mask[env] : e.reset[env])) return;  // uniform per half-wave
+  const MotionScalars m = load_motion(l, e.motion_ids[env]);
+  const float u = phase ? phase[env] : reset_draw(e, env, seed, counter);
+  float mt;
+  const BodyRec s = reset_env_state(e, l, env, lane, m, u, &mt);
+  // obs of the reset env: progress 0, start = mt, offsets 0 (humanoid_phc.py:1061-1065)
+  env_obs(e, l, env, lane, m, s, (float)(0 + 1) * c.dt + mt + 0.0f, v3{0.0f, 0.0f, 0.0f}, true);
+  if (lane == 0) {
+    reset_env_counters(e, env, mt);
+    if (e.rng && !phase) e.rng[env] += 1u;
+  }
+}
+
 // --------------------------------------------------------------- env step --
 // Post-physics part of HumanoidPHC.step (humanoid_phc.py:136-146):
 //   progress += 1; reward with the reference at t (:1228-1303); reset at t (:1311-1333);
 //   obs with the reference at t+dt (:935-959, 1061-1112); then PHCPufferEnv.step's
-//   terminals/truncations/masks and episode return/length (clean_pufferl/env.py:103-140).
+//   terminals/truncations/masks and episode return/length (clean_pufferl/env.py:103-140)
+//   and, with AUTO, the env.reset(reset_indices) of the envs that came up for reset.
+template <bool AUTO>
 __global__ __launch_bounds__(kBlock) void k_env_step(EnvView e, LibView l, StepConsts c) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
   const int g = threadIdx.x / kGroup;
@@ -130,17 +214,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(EnvView e, LibView l, StepC
   const v3 go = {e.goff[3 * ei], e.goff[3 * ei + 1], e.goff[3 * ei + 2]};
   const MotionScalars m = load_motion(l, e.motion_ids[ei]);
   const float t = (float)prog * c.dt + st + so;
-  const float t1 = (float)(prog + 1) * c.dt + st + so;
   const Blend bl0 = frame_blend(t, m);
-  const Blend bl1 = frame_blend(t1, m);
 
-  const BodyRec s = load_body(e.rb + (ei * kBodies + b) * kRec);
+  BodyRec s = load_body(e.rb + (ei * kBodies + b) * kRec);
   const BodyRec ref0 = ref_body(l.frames, bl0, b, &go);
-  const BodyRec ref1 = ref_body(l.frames, bl1, b, &go);
-
-  // root (body 0) broadcast from lane 0
-  const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
-  const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
 
   // ---- reward terms (common.py:271-322) ----
   const v3 dp = vsub(ref0.p, s.p);
@@ -181,41 +258,31 @@ __global__ __launch_bounds__(kBlock) void k_env_step(EnvView e, LibView l, StepC
   dsum = group_sum(dsum);
   pw = group_sum(pw);
 
-  // ---- observation at t+dt ----
-  const float hd = calc_heading(root_r);
-  const q4 hinv = quat_from_angle_z(-hd);
-  const q4 hrot = quat_from_angle_z(hd);
-  if (valid && active) write_obs_body(e.obs + ei * kObs, b, s, root_p, hinv, hrot, ref1);
+  // every lane holds the totals: the per-env decisions are uniform over the half-wave
+  const float r_pos = expf(-c.k_pos * (e_pos / (float)kBodies));
+  const float r_rot = expf(-c.k_rot * (e_rot / (float)kBodies));
+  const float r_vel = expf(-c.k_vel * (e_vel / (float)kBodies));
+  const float r_ang = expf(-c.k_ang * (e_ang / (float)kBodies));
+  float rew = c.w_pos * r_pos + c.w_rot * r_rot + c.w_vel * r_vel + c.w_ang * r_ang;
+  float pr = 0.0f;
+  if (c.use_power) {
+    pr = -c.power_coef * pw;
+    if (prog <= 3) pr = 0.0f;
+    rew = rew + pr;
+  }
+  const bool pass_time = t >= m.len;
+  bool terminated = false;
+  if (c.enable_et) {
+    const bool fallen = c.use_mean ? (dsum * c.inv_nreset > c.td_first) : (fall > 0.0f);
+    terminated = fallen && (prog > 1);
+  }
+  const bool reset = pass_time || terminated;
 
   double st_row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (valid && lane == 0) {
-    const float inv24 = 1.0f / (float)kBodies;
-    const float r_pos = expf(-c.k_pos * (e_pos / (float)kBodies));
-    const float r_rot = expf(-c.k_rot * (e_rot / (float)kBodies));
-    const float r_vel = expf(-c.k_vel * (e_vel / (float)kBodies));
-    const float r_ang = expf(-c.k_ang * (e_ang / (float)kBodies));
-    (void)inv24;
-    float rew = c.w_pos * r_pos + c.w_rot * r_rot + c.w_vel * r_vel + c.w_ang * r_ang;
-    float pr = 0.0f;
-    if (c.use_power) {
-      pr = -c.power_coef * pw;
-      if (prog <= 3) pr = 0.0f;
-      rew = rew + pr;
-    }
     e.rew[ei] = rew;
     float *raw = e.raw + ei * 5;
     raw[0] = r_pos; raw[1] = r_rot; raw[2] = r_vel; raw[3] = r_ang; raw[4] = pr;
-
-    const bool pass_time = t >= m.len;
-    bool terminated = false;
-    if (c.enable_et) {
-      const bool fallen = c.use_mean ? (dsum * c.inv_nreset > c.td_first) : (fall > 0.0f);
-      terminated = fallen && (prog > 1);
-    }
-    const bool reset = pass_time || terminated;
-    e.progress[ei] = (int16_t)prog;
-    e.reset[ei] = reset;
-    e.term[ei] = terminated;
     // PHCPufferEnv.step bookkeeping
     const bool trunc = reset && !terminated;
     if (e.terminals) e.terminals[ei] = terminated;
@@ -238,6 +305,26 @@ __global__ __launch_bounds__(kBlock) void k_env_step(EnvView e, LibView l, StepC
     }
     st_row[0] = r_pos; st_row[1] = r_rot; st_row[2] = r_vel; st_row[3] = r_ang; st_row[4] = pr;
   }
+
+  // ---- observation (and in-launch reset) ----
+  float t1 = (float)(prog + 1) * c.dt + st + so;
+  v3 off1 = go;
+  if (AUTO && valid && reset) {
+    float mt;
+    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull), &mt);
+    t1 = (float)(0 + 1) * c.dt + mt + 0.0f;
+    off1 = {0.0f, 0.0f, 0.0f};
+    if (lane == 0) {
+      reset_env_counters(e, ei, mt);
+      if (e.rng) e.rng[ei] += 1u;
+    }
+  } else if (valid && lane == 0) {
+    e.progress[ei] = (int16_t)prog;
+    e.reset[ei] = reset;
+    e.term[ei] = terminated;
+  }
+  env_obs(e, l, ei, lane, m, s, t1, off1, valid);
+
   if (e.stats) {
     if (lane == 0) {
 #pragma unroll
@@ -253,62 +340,14 @@ __global__ __launch_bounds__(kBlock) void k_env_step(EnvView e, LibView l, StepC
   }
 }
 
-// ------------------------------------------------------------- env reset --
-// HumanoidPHC.reset(env_ids) for StateInit.Random: sample_time_interval, reference state
-// with the env's previous global offset written into the sim buffers (_set_env_state),
-// counters cleared (_reset_env_tensors), offsets cleared (_reset_ref_state_init), then the
-// env's observation at progress 0 (obs time dt + start).
-__global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, StepConsts c,
-                                                       const uint8_t *__restrict__ mask,
-                                                       const float *__restrict__ phase, unsigned long long seed,
-                                                       unsigned long long counter) {
-  const int64_t env = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kGroup;
-  const int lane = threadIdx.x % kGroup;
-  if (env >= e.n) return;
-  if (!(mask ? mask[env] : e.reset[env])) return;  // uniform per half-wave
-  const bool active = lane < kBodies;
-  const int b = active ? lane : 0;
-
-  const int64_t mid = e.motion_ids[env];
-  const MotionScalars m = load_motion(l, mid);
-  const float u = phase ? phase[env] : uniform01(seed, counter, (unsigned long long)env);
-  const float fps_step = 1.0f / 30.0f;  // motion_lib.py:532 curr_fps
-  const float mt = (float)(int64_t)((u * m.len) / fps_step) * fps_step;
-  const v3 go_old = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
-  const Blend bl = frame_blend(mt, m);
-  const BodyRec s = ref_body(l.frames, bl, b, &go_old);
-  if (active) {
-    store_body(e.rb + (env * kBodies + b) * kRec, s);
-    if (b == 0 && e.root) store_body(e.root + env * kRec, s);
-    if (b >= 1) {
-      const v3 dp = ref_dof_pos(l.local_rot, bl, b);
-      const v3 dv = ref_dof_vel(l.dof_vel, bl, b);
-      float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
-      d[0] = dp.x; d[1] = dv.x; d[2] = dp.y; d[3] = dv.y; d[4] = dp.z; d[5] = dv.z;
-    }
-  }
-  // observation of the reset env: progress 0, start = mt, offsets 0
-  const float t1 = (float)(0 + 1) * c.dt + mt + 0.0f;
-  const Blend bl1 = frame_blend(t1, m);
-  const v3 zero = {0.0f, 0.0f, 0.0f};
-  const BodyRec ref1 = ref_body(l.frames, bl1, b, &zero);
-  const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
-  const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
-  const float hd = calc_heading(root_r);
-  const q4 hinv = quat_from_angle_z(-hd);
-  const q4 hrot = quat_from_angle_z(hd);
-  if (active) write_obs_body(e.obs + env * kObs, b, s, root_p, hinv, hrot, ref1);
-  if (lane == 0) {
-    e.progress[env] = 0;
-    e.reset[env] = 0;
-    e.term[env] = 0;
-    e.goff[3 * env] = 0.0f; e.goff[3 * env + 1] = 0.0f; e.goff[3 * env + 2] = 0.0f;
-    e.start[env] = mt;
-    e.start_off[env] = 0.0f;
-  }
+// --------------------------------------------------------- physics stand-in --
+// Triangular noise with standard deviation `sd` from 16 random bits pairs (cheap integer RNG).
+__device__ __forceinline__ float tri_noise(unsigned long long h, int k, float sd) {
+  const unsigned a = (unsigned)(h >> (32 * (k & 1))) & 0xFFFFu;
+  const unsigned b = (unsigned)(h >> (32 * (k & 1) + 16)) & 0xFFFFu;
+  return ((float)a - (float)b) * (sd * 2.4494897f / 65536.0f);
 }
 
-// --------------------------------------------------------- physics stand-in --
 __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l, StepConsts c, float sigma,
                                                            float force_scale, unsigned long long seed,
                                                            unsigned long long counter) {
@@ -322,30 +361,40 @@ __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l,
   const Blend bl = frame_blend(t, m);
   const v3 go = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
   BodyRec s = ref_body(l.frames, bl, b, &go);
-  const unsigned long long base = (unsigned long long)(env * kBodies + b) * 16ull;
-  s.p.x += sigma * normal01(seed, counter, base + 0);
-  s.p.y += sigma * normal01(seed, counter, base + 1);
-  s.p.z += sigma * normal01(seed, counter, base + 2);
-  q4 r = {s.r.x + sigma * normal01(seed, counter, base + 3), s.r.y + sigma * normal01(seed, counter, base + 4),
-          s.r.z + sigma * normal01(seed, counter, base + 5), s.r.w + sigma * normal01(seed, counter, base + 6)};
+  const unsigned long long base = mix64(seed ^ mix64(counter) ^ ((unsigned long long)(env * kBodies + b) << 8));
+  unsigned long long h = mix64(base + 1);
+  s.p.x += tri_noise(h, 0, sigma);
+  s.p.y += tri_noise(h, 1, sigma);
+  h = mix64(base + 2);
+  s.p.z += tri_noise(h, 0, sigma);
+  q4 r = {s.r.x + tri_noise(h, 1, sigma), s.r.y, s.r.z, s.r.w};
+  h = mix64(base + 3);
+  r.y += tri_noise(h, 0, sigma);
+  r.z += tri_noise(h, 1, sigma);
   s.r = quat_unit(r);
-  s.v.x += 10.0f * sigma * normal01(seed, counter, base + 7);
-  s.v.y += 10.0f * sigma * normal01(seed, counter, base + 8);
-  s.v.z += 10.0f * sigma * normal01(seed, counter, base + 9);
-  s.av.x += 20.0f * sigma * normal01(seed, counter, base + 10);
-  s.av.y += 20.0f * sigma * normal01(seed, counter, base + 11);
-  s.av.z += 20.0f * sigma * normal01(seed, counter, base + 12);
+  h = mix64(base + 4);
+  s.v.x += tri_noise(h, 0, 10.0f * sigma);
+  s.v.y += tri_noise(h, 1, 10.0f * sigma);
+  h = mix64(base + 5);
+  s.v.z += tri_noise(h, 0, 10.0f * sigma);
+  s.av.x += tri_noise(h, 1, 20.0f * sigma);
+  h = mix64(base + 6);
+  s.av.y += tri_noise(h, 0, 20.0f * sigma);
+  s.av.z += tri_noise(h, 1, 20.0f * sigma);
   store_body(e.rb + (env * kBodies + b) * kRec, s);
   if (b >= 1) {
     const v3 dv = ref_dof_vel(l.dof_vel, bl, b);
     float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
-    d[1] = dv.x + 10.0f * sigma * normal01(seed, counter, base + 13);
-    d[3] = dv.y + 10.0f * sigma * normal01(seed, counter, base + 14);
-    d[5] = dv.z + 10.0f * sigma * normal01(seed, counter, base + 15);
+    h = mix64(base + 7);
+    d[1] = dv.x + tri_noise(h, 0, 10.0f * sigma);
+    d[3] = dv.y + tri_noise(h, 1, 10.0f * sigma);
+    h = mix64(base + 8);
+    d[5] = dv.z + tri_noise(h, 0, 10.0f * sigma);
     float *f = const_cast<float *>(e.dof_force) + env * PHC_NUM_DOF + 3 * (b - 1);
-    f[0] = force_scale * normal01(seed ^ 0xF0F0ull, counter, base + 0);
-    f[1] = force_scale * normal01(seed ^ 0xF0F0ull, counter, base + 1);
-    f[2] = force_scale * normal01(seed ^ 0xF0F0ull, counter, base + 2);
+    f[0] = tri_noise(h, 1, force_scale);
+    h = mix64(base + 9);
+    f[1] = tri_noise(h, 0, force_scale);
+    f[2] = tri_noise(h, 1, force_scale);
   }
 }
 
@@ -391,8 +440,9 @@ extern "C" int64_t phc_stats_blocks(int64_t num_envs) { return num_envs <= 0 ? 0
 extern "C" int phc_motion_state(const phc_motion_lib *lib, const int64_t *ids, const float *times,
                                 const float *offset, int64_t n, phc_ref_state *out, void *stream) {
   if (int rc = check_lib(lib)) return rc;
+  PHC_REQUIRE(n >= 0, "motion_state: negative n");
+  if (n == 0) return PHC_OK;
   PHC_REQUIRE(out && out->body && ids && times, "motion_state: null argument");
-  if (n <= 0) return PHC_OK;
   hipLaunchKernelGGL(k_motion_state, dim3(grid_envs(n)), dim3(kBlock), 0, as_stream(stream), lib_view(lib), ids,
                      times, offset, n, out->body, out->dof_pos, out->dof_vel);
   return check_launch("motion_state");
@@ -403,8 +453,15 @@ extern "C" int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *li
   if (int rc = check_env(env)) return rc;
   if (int rc = check_lib(lib)) return rc;
   PHC_REQUIRE(p && p->dt > 0.0f, "env_step: bad params");
-  hipLaunchKernelGGL(k_env_step, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
-                     env_view(env), lib_view(lib), make_consts(p));
+  if (p->auto_reset) {
+    PHC_REQUIRE(lib->local_rot && lib->dof_vel, "env_step: auto_reset needs local_rot and dof_vel");
+    PHC_REQUIRE(env->rng_counter, "env_step: auto_reset needs rng_counter");
+    hipLaunchKernelGGL(k_env_step<true>, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
+                       env_view(env), lib_view(lib), make_consts(p));
+  } else {
+    hipLaunchKernelGGL(k_env_step<false>, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
+                       env_view(env), lib_view(lib), make_consts(p));
+  }
   return check_launch("env_step");
 }
 
@@ -427,6 +484,7 @@ extern "C" int phc_physics_replay(const phc_env_buffers *env, const phc_motion_l
   if (int rc = check_env(env)) return rc;
   if (int rc = check_lib(lib)) return rc;
   PHC_REQUIRE(lib->dof_vel, "physics_replay: motion lib needs dof_vel");
+  PHC_REQUIRE(p, "physics_replay: bad params");
   hipLaunchKernelGGL(k_physics_replay, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
                      env_view(env), lib_view(lib), make_consts(p), pos_sigma, force_scale,
                      (unsigned long long)seed, (unsigned long long)counter);
@@ -435,8 +493,9 @@ extern "C" int phc_physics_replay(const phc_env_buffers *env, const phc_motion_l
 
 extern "C" int phc_actions_to_pd(const float *actions, float *pd, int64_t n, const float *offset,
                                  const float *scale, const uint8_t *frozen, void *stream) {
+  PHC_REQUIRE(n >= 0, "actions_to_pd: negative n");
+  if (n == 0) return PHC_OK;
   PHC_REQUIRE(actions && pd && offset && scale, "actions_to_pd: null argument");
-  if (n <= 0) return PHC_OK;
   const int64_t total = n * PHC_NUM_DOF;
   hipLaunchKernelGGL(k_actions_to_pd, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      as_stream(stream), actions, pd, total, offset, scale, frozen);

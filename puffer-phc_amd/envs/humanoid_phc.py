@@ -161,6 +161,7 @@ class HumanoidPHC:
         self._motion_sample_start_idx = 0
         self._sampled_motion_ids = torch.arange(N, device=dev)
         self._reset_mask = torch.zeros(N, dtype=torch.bool, device=dev)
+        self._rng_counter_buf = torch.zeros(N, dtype=torch.int32, device=dev)
         self._puffer = {}
         self._env_c = None
         self._build_structs()
@@ -176,14 +177,16 @@ class HumanoidPHC:
             self.cfg.num_envs, self._rigid_body_state, self._humanoid_root_states, self._dof_state,
             self.dof_force_tensor, self.progress_buf, self._sampled_motion_ids, self._motion_start_times,
             self._motion_start_times_offset, self._global_offset, self.obs_buf, self.rew_buf, self.reward_raw,
-            self.reset_buf, self._terminate_buf, **self._puffer)
+            self.reset_buf, self._terminate_buf, rng_counter=self._rng_counter_buf, **self._puffer)
         self._build_step_params()
 
     def _build_step_params(self):
-        self._step_params = _native.step_params_struct(
-            self.dt, self.cfg.reward, self.cfg.rew_power_coef, self.cfg.reward.use_power_reward,
-            self.cfg.enable_early_termination, self.flag_im_eval, self._reset_bodies_id,
-            self._termination_distances.detach().cpu().tolist())
+        args = (self.dt, self.cfg.reward, self.cfg.rew_power_coef, self.cfg.reward.use_power_reward,
+                self.cfg.enable_early_termination, self.flag_im_eval, self._reset_bodies_id,
+                self._termination_distances.detach().cpu().tolist())
+        seed = int(self.cfg.seed) * 7919 + 17
+        self._step_params = _native.step_params_struct(*args, auto_reset=False, seed=seed)
+        self._step_params_auto = _native.step_params_struct(*args, auto_reset=True, seed=seed)
 
     def _load_motion(self, motion_train_file):
         """humanoid_phc.py:620-657: train + eval libraries, even initial sampling."""
@@ -237,21 +240,27 @@ class HumanoidPHC:
         _native.reset_envs(self._env_c, self._motion_lib.packed.c, self._step_params, mask=None,
                            seed=self._rng_seed, counter=self._next_counter())
 
-    def step(self, actions):
-        """humanoid_phc.py:105-172 with the physics stand-in."""
+    def step(self, actions, auto_reset=False):
+        """humanoid_phc.py:105-172 with the physics stand-in.  With auto_reset (used by
+        PHCPufferEnv) the envs that come up for reset are re-initialised inside the same
+        fused kernel, as PHCPufferEnv.step's env.reset(reset_indices) does next."""
         if actions.dtype != torch.float32 or not actions.is_contiguous():
             actions = actions.float().contiguous()
         _native.actions_to_pd(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale, self._pd_frozen)
         self.physics.step(self)
+        params = self._step_params_auto if auto_reset else self._step_params
         if self.kernel_events is not None:  # bench: HIP events around the fused kernel
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-            _native.env_step(self._env_c, self._motion_lib.packed.c, self._step_params)
+            _native.env_step(self._env_c, self._motion_lib.packed.c, params)
             ev1.record()
             self.kernel_events.append((ev0, ev1))
         else:
-            _native.env_step(self._env_c, self._motion_lib.packed.c, self._step_params)
-        self.extras["terminate"] = self._terminate_buf.clone()
+            _native.env_step(self._env_c, self._motion_lib.packed.c, params)
+        if auto_reset and "terminals" in self._puffer:
+            self.extras["terminate"] = self._puffer["terminals"]  # this step's outcome, written by the kernel
+        else:
+            self.extras["terminate"] = self._terminate_buf.clone()
         self.extras["reward_raw"] = self.reward_raw
         if self.flag_im_eval:
             t = self.progress_buf * self.dt + self._motion_start_times + self._motion_start_times_offset

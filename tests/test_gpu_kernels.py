@@ -203,6 +203,36 @@ def test_reset_envs_mask_only_touches_masked(golden, golden_lib, N):
     np.testing.assert_array_equal(bufs["start_times"][mask].cpu().numpy(), g["motion_times"][::3])
 
 
+def test_env_step_auto_reset_equals_step_then_reset(golden, golden_lib, N):
+    """The fused in-launch reset must equal env_step followed by phc_reset_envs, bit for bit."""
+    g = golden("env_step")
+    n = len(g["motion_ids"])
+    outs = []
+    for auto in (True, False):
+        bufs, _ = _env_buffers(N, n, g["rb_state"], g["dof_vel"], g["dof_force"], g["motion_ids"],
+                               g["progress"].astype(np.int32) - 1, g["start"], g["start_offset"],
+                               g["global_offset"])
+        bufs["episode_return"].zero_()
+        bufs["episode_length"].zero_()
+        bufs["rng_counter"] = torch.arange(n, dtype=torch.int32, device=DEV) * 3
+        c = N.env_struct(n, **bufs)
+        from types import SimpleNamespace
+
+        p = N.step_params_struct(float(O.DT), SimpleNamespace(**O.REWARD), 0.0005, True, True, False,
+                                 np.arange(24), np.full(24, 0.25), auto_reset=auto, seed=1234)
+        N.env_step(c, golden_lib.c, p)
+        if not auto:
+            N.reset_envs(c, golden_lib.c, p, mask=None, phase=None, seed=1234)
+        torch.cuda.synchronize()
+        outs.append({k: v.clone() for k, v in bufs.items()})
+    a, b = outs
+    assert g["train_reset"].any()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    assert not a["reset"].any()
+    np.testing.assert_array_equal(a["terminals"].cpu().numpy(), g["train_terminate"])
+
+
 def test_fk_vs_reference(golden, N):
     s, m = golden("skeleton"), golden("motion_lib")
     order = m["sample_idxes"]
