@@ -99,12 +99,17 @@ __device__ __forceinline__ void quat_to_tan_norm(q4 q, float out[6]) {
 // torch_utils.py:50-51
 __device__ __forceinline__ float normalize_angle(float x) { return atan2f(sinf(x), cosf(x)); }
 
+// normalize_angle(a) for a in [0, 2pi] (a = 2*acos(w)): atan2(sin a, cos a) is a itself up
+// to libm rounding below pi and a - 2pi above it, so fold the range instead of evaluating
+// three transcendentals.
+__device__ __forceinline__ float fold_angle_0_2pi(float a) { return a > 3.14159265f ? a - 6.28318531f : a; }
+
 // torch_utils.py:86-106 quat_to_angle_axis: NaN lanes masked exactly like torch.where.
 __device__ __forceinline__ float quat_angle_masked(q4 q, float *sin_theta_out) {
   const float sin_theta = sqrtf(1.0f - q.w * q.w);
   *sin_theta_out = sin_theta;
   if (!(fabsf(sin_theta) > 1e-5f)) return 0.0f;
-  return normalize_angle(2.0f * acosf(q.w));
+  return fold_angle_0_2pi(2.0f * acosf(q.w));
 }
 
 __device__ __forceinline__ v3 quat_to_exp_map(q4 q) {
@@ -160,6 +165,31 @@ __device__ __forceinline__ q4 exp_map_to_quat(v3 e) {
 __device__ __forceinline__ float calc_heading(q4 q) {
   const v3 d = my_quat_rotate(q, v3{1.0f, 0.0f, 0.0f});
   return atan2f(d.y, d.x);
+}
+
+// calc_heading_quat / calc_heading_quat_inv (torch_utils.py:384-408) without atan2/sin/cos:
+// with (c, s) = (cos h, sin h) of the heading h = atan2(y, x), the half-angle identities give
+// cos(h/2) = sqrt((1+c)/2), sin(h/2) = s / (2 cos(h/2)) for c >= 0 and sin(h/2) =
+// sign(s) sqrt((1-c)/2), cos(h/2) = s / (2 sin(h/2)) for c < 0 (both well conditioned), then
+// quat_unit as the reference.  Agrees with the transcendental path to a few ulps.
+__device__ __forceinline__ void heading_quats(q4 root_rot, q4 *hrot, q4 *hinv) {
+  const v3 d = my_quat_rotate(root_rot, v3{1.0f, 0.0f, 0.0f});
+  const float r = sqrtf(d.x * d.x + d.y * d.y);
+  float ch = 1.0f, sh = 0.0f;
+  if (r > 0.0f) {
+    ch = d.x / r;
+    sh = d.y / r;
+  }
+  float C, S;
+  if (ch >= 0.0f) {
+    C = sqrtf((1.0f + ch) * 0.5f);
+    S = sh / (2.0f * C);
+  } else {
+    S = copysignf(sqrtf((1.0f - ch) * 0.5f), sh);
+    C = sh / (2.0f * S);
+  }
+  *hrot = quat_unit(q4{0.0f, 0.0f, S, C});
+  *hinv = quat_unit(q4{0.0f, 0.0f, -S, C});
 }
 
 // torch_utils.py:219-228 quat_angle_axis (float64 use at load time): angle in [0, pi].

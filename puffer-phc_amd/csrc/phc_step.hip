@@ -164,9 +164,8 @@ __device__ __forceinline__ void env_obs(const EnvView &e, const LibView &l, int6
   const BodyRec ref1 = ref_body(l.frames, frame_blend(t1, m), b, &off);
   const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
   const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
-  const float hd = calc_heading(root_r);
-  const q4 hinv = quat_from_angle_z(-hd);
-  const q4 hrot = quat_from_angle_z(hd);
+  q4 hinv, hrot;
+  heading_quats(root_r, &hrot, &hinv);
   if (write && active) write_obs_body(e.obs + env * kObs, b, s, root_p, hinv, hrot, ref1);
 }
 

@@ -6,24 +6,31 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
-ENVS=${ENVS:-4096}
+ENVS_LIST=${ENVS_LIST:-4096}
 STEPS=${STEPS:-200}
+BENCH_ARGS=${BENCH_ARGS:-}
 
-timeout -k 10 900 python -m pytest tests -m gpu -q > "$OUT/pytest_gpu.log" 2>&1
-rc=$?
-echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 3; }
-tail -1 "$OUT/smoke.log"
-timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 20 --envs "$ENVS" > "$OUT/bench_$ENVS.log" 2>&1 || { tail -20 "$OUT/bench_$ENVS.log"; exit 4; }
-tail -1 "$OUT/bench_$ENVS.log"
-if [ "${PROFILE:-1}" = "1" ]; then
-  export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_trace_$ENVS" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --steps 50 --warmup 10 --envs "$ENVS" --no-cpu-baseline > "$OUT/prof_trace_$ENVS.log" 2>&1 || { tail -20 "$OUT/prof_trace_$ENVS.log"; exit 5; }
-  for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_env_step" -T -d "$OUT/prof_${C}_$ENVS" -o run --output-format csv -- \
-      python3 "$ROOT/bench.py" --steps 20 --warmup 5 --envs "$ENVS" --no-cpu-baseline > "$OUT/prof_${C}_$ENVS.log" 2>&1 || { tail -20 "$OUT/prof_${C}_$ENVS.log"; exit 6; }
-  done
+if [ "${TESTS:-1}" = "1" ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q > "$OUT/pytest_gpu.log" 2>&1
+  rc=$?
+  echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 3; }
+  tail -1 "$OUT/smoke.log"
 fi
+for ENVS in $ENVS_LIST; do
+  EXTRA=""
+  if [ "$ENVS" != "4096" ]; then EXTRA="--no-cpu-baseline"; fi
+  timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 20 --envs "$ENVS" $EXTRA $BENCH_ARGS > "$OUT/bench_$ENVS.log" 2>&1 || { tail -20 "$OUT/bench_$ENVS.log"; exit 4; }
+  tail -1 "$OUT/bench_$ENVS.log"
+  if [ "${PROFILE:-1}" = "1" ]; then
+    export TMPDIR=/tmp
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_trace_$ENVS" -o run --output-format csv -- \
+      python3 "$ROOT/bench.py" --steps 50 --warmup 10 --envs "$ENVS" --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_trace_$ENVS.log" 2>&1 || { tail -20 "$OUT/prof_trace_$ENVS.log"; exit 5; }
+    for C in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_env_step" -T -d "$OUT/prof_${C}_$ENVS" -o run --output-format csv -- \
+        python3 "$ROOT/bench.py" --steps 20 --warmup 5 --envs "$ENVS" --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_${C}_$ENVS.log" 2>&1 || { tail -20 "$OUT/prof_${C}_$ENVS.log"; exit 6; }
+    done
+  fi
+done
 echo "gpu_check done"
