@@ -1,25 +1,33 @@
-"""Benchmark: whole-job env-steps/s of the PHC imitation env step on MI355X.
+"""Benchmark: whole-job env-steps/s of the PHC imitation rollout + PPO step on MI355X.
 
 Contract: `python bench.py --gpus N --steps K --warmup W` (N>1 under torch.distributed.run,
-one rank per GPU over RCCL).  Rank 0 prints ONE JSON line.
+one rank per GPU over RCCL).  Rank 0 prints ONE JSON line.  Default workload (BASELINE.json
+configs[2] at 4096 envs per GPU; the metric's config):
 
-Workload (BASELINE.json metric: env-steps/s, 24-joint SMPL, 4096 envs per GPU): one step =
-PHCPufferEnv.step on 4096 envs = actions->PD (phc_actions_to_pd) + the physics stand-in
-(phc_physics_replay: replayed reference states + noise, BASELINE configs[1]) + the fused
-obs/reward/reset/bookkeeping kernel (phc_env_step) + re-initialisation of terminated envs
-(phc_reset_envs).  Motions: a synthetic library of 4096 clips, U{60..300} frames at 30 fps,
-built on device by the HIP FK path (AMASS is not available offline).  Actions are a fixed
-random batch (no policy inference in this step).  Envs shard across ranks with no data-path
-collective (weak scaling); the only collectives are the timing barrier and the max-reduce.
+  --mode ppo (default): one step = one full PPO iteration of clean_pufferl exactly as
+      scripts/train.py runs it: evaluate() until 131072 mask-true rows are collected
+      (PHCPolicy inference + PHCPufferEnv.step on 4096 envs + on-device experience store),
+      RunningNorm update over the batch, train() = GAE + 4 epochs x 4 minibatches of 32768
+      (forward, PPO loss, backward, grad clip, Adam).  value = rows collected / wall time,
+      the reference's SPS definition (clean_pufferl/structs.py:354).
+  --mode rollout: one step = policy inference + PHCPufferEnv.step + experience store.
+  --mode env: one step = PHCPufferEnv.step (actions->PD, physics stand-in, fused
+      obs/reward/reset/re-init kernel) with a fixed random action batch.
 
-Roofline: the dominant kernel is phc_env_step (HBM-bound); algorithmic bytes per env-step =
-10,886 (7,122 read + 3,764 written), achieved = bytes x envs / average kernel
-time measured with HIP events around every launch in the timed region.  `traffic` = HBM
-bytes per launch from rocprofv3 PMC counters (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)
-read from profiles/traffic_<envs>.json when present, else null.
+Physics is the replay stand-in (BASELINE configs[1]); motions are a synthetic library of 4096
+clips, U{60..300} frames at 30 fps, built on device by the HIP FK path (AMASS is not
+available offline).  Policy weights are random-init (orthogonal, as the reference).  Envs
+shard across ranks (weak scaling); the PPO update all-reduces gradients and advantage
+statistics over RCCL.
+
+Roofline: the dominant kernel of the env step is phc_env_step (HBM-bound); algorithmic bytes
+per env-step = 10,886 (7,122 read + 3,764 written); achieved = bytes x envs /
+average kernel time measured with HIP events around every launch in the timed region.
+`traffic` = HBM bytes per launch from rocprofv3 PMC counters (2 x FETCH_SIZE + WRITE_SIZE,
+gfx950 correction) read from profiles/traffic_<envs>.json when present, else null.
 
 cpu_baseline: the numpy oracle (oracle/phc_oracle.py) env step on the same 4096-env batch,
-1 thread, bounded to ~10 s, rank 0 at N=1 only.
+1 thread, bounded to ~10 s, rank 0 at N=1 only (the PPO GEMMs have no CPU oracle).
 """
 
 import argparse
@@ -39,47 +47,54 @@ phc_amd_path.register()
 
 BYTES_PER_ENV_STEP = 10886
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+DEFAULTS = {"env": (200, 20), "rollout": (64, 8), "ppo": (3, 1)}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--mode", choices=["env", "rollout", "ppo"], default="ppo")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--batch-size", type=int, default=131072, help="PPO rows per rank per iteration")
+    ap.add_argument("--minibatch-size", type=int, default=32768)
     ap.add_argument("--min-len", type=int, default=60)
     ap.add_argument("--max-len", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic-file", default=None)
-    return ap.parse_args()
+    a = ap.parse_args()
+    k, w = DEFAULTS[a.mode]
+    a.steps = k if a.steps is None else a.steps
+    a.warmup = w if a.warmup is None else a.warmup
+    return a
 
 
-def setup_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+def setup_dist():
+    from puffer_phc_amd import distributed as D
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        D.init_from_env("nccl")
     else:
         torch.cuda.set_device(0)
-    return world, rank, local
+    return D.world_size(), D.rank()
 
 
-def build_env(args, rank, device):
+def build_env(args, rank):
     from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
     from puffer_phc_amd.config import EnvConfig
     from puffer_phc_amd.motion_lib import PackedMotions
     from puffer_phc_amd.synthetic import synthetic_clips
 
+    device = f"cuda:{torch.cuda.current_device()}"
     q, t, counts, fps = synthetic_clips(args.envs, args.min_len, args.max_len, seed=1000 + rank, device=device)
     packed = PackedMotions.from_global_rotations(q, t, counts, fps)
     del q, t
     cfg = EnvConfig(num_envs=args.envs, device_id=torch.cuda.current_device(), seed=rank)
     env = PHCPufferEnv(cfg, motion_data=packed)
     env.reset()
-    return env, packed
+    return env, packed, cfg
 
 
 def cpu_baseline(env, packed, seconds):
@@ -110,41 +125,84 @@ def cpu_baseline(env, packed, seconds):
                       f"1 thread, {dt:.1f}s)"}
 
 
+class Runner:
+    """One benchmark 'step' per mode; returns the env-steps it processed on this rank."""
+
+    def __init__(self, args, env, env_cfg):
+        self.args, self.env = args, env
+        dev = env_cfg.device
+        self.actions = torch.rand((args.envs, 69), device=dev) * 2 - 1
+        if args.mode == "env":
+            return
+        from puffer_phc_amd import clean_pufferl
+        from puffer_phc_amd.config import TrainConfig
+        from puffer_phc_amd.policies import PHCPolicy, Policy
+
+        self.cp = clean_pufferl
+        self.policy = Policy(PHCPolicy(env)).to(dev)
+        self.tcfg = TrainConfig(device_id=torch.cuda.current_device(), batch_size=args.batch_size,
+                                minibatch_size=args.minibatch_size, checkpoint_interval=10 ** 9,
+                                total_timesteps=10 ** 15)
+        self.components, self.info, self.util = clean_pufferl.create("bench", self.tcfg, env_cfg, env, self.policy)
+        self.obs = env.observations
+
+    def step(self):
+        a = self.args
+        if a.mode == "env":
+            self.env.step(self.actions)
+            return a.envs
+        if a.mode == "rollout":
+            exp = self.components.experience
+            if exp.full:
+                exp.ptr = 0
+            o, r, d, t, _, env_id, mask = self.env.recv()
+            with torch.no_grad():
+                actions, logprob, _, value = self.policy(o)
+            exp.store(o, None, value.flatten(), actions, logprob, r, d, t, env_id, mask, n_valid=a.envs)
+            self.env.send(actions)
+            return a.envs
+        g0 = self.info.global_step
+        self.cp.evaluate(self.components, self.info)
+        self.policy.policy.update_obs_rms(self.components.experience.obs)
+        self.cp.train(self.components, self.info, self.util)
+        return self.info.global_step - g0
+
+
 def main():
     args = parse()
-    world, rank, local = setup_dist(args)
+    world, rank = setup_dist()
     device = f"cuda:{torch.cuda.current_device()}"
     torch.manual_seed(1234 + rank)
-    env, packed = build_env(args, rank, device)
-    actions = torch.rand((args.envs, 69), device=device) * 2 - 1
+    env, packed, env_cfg = build_env(args, rank)
+    runner = Runner(args, env, env_cfg)
 
     for _ in range(args.warmup):
-        env.step(actions)
+        runner.step()
     torch.cuda.synchronize()
     env.env.kernel_events = []
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    processed = 0
     for _ in range(args.steps):
-        env.step(actions)
+        processed += runner.step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in env.env.kernel_events]
+    env_steps = len(kern_ms)
     env.env.kernel_events = None
     kern_s = float(np.mean(kern_ms)) * 1e-3
     t = torch.tensor([elapsed, kern_s], dtype=torch.float64, device=device)
+    tot = torch.tensor([float(processed)], dtype=torch.float64, device=device)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    elapsed, kern_s = float(t[0]), float(t[1])
-
-    # sanity: the env must be tracking (not resetting every step)
-    resets = float(env.stats.sum(0)[7].item())
+        torch.distributed.all_reduce(tot)
+    elapsed, kern_s, processed_all = float(t[0]), float(t[1]), float(tot[0])
 
     if rank == 0:
-        total_env_steps = args.envs * world * args.steps
         achieved = BYTES_PER_ENV_STEP * args.envs / kern_s / 1e9
         traffic = None
         tf = args.traffic_file or os.path.join(ROOT, "profiles", f"traffic_{args.envs}.json")
@@ -154,9 +212,17 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(env, packed, args.cpu_seconds)
+        workloads = {
+            "ppo": "clean_pufferl PPO iteration: evaluate %d rows (PHCPolicy fp32 inference + PHCPufferEnv.step) + "
+                   "RMS update + train (GAE, 4 epochs x %d minibatches of %d, Adam)" % (
+                       args.batch_size, args.batch_size // args.minibatch_size, args.minibatch_size),
+            "rollout": "PHCPolicy fp32 inference + PHCPufferEnv.step + on-device experience store",
+            "env": "PHCPufferEnv.step: actions->PD + replay physics + fused obs/reward/reset + reset re-init "
+                   "(fixed random actions, no policy)",
+        }
         out = {
             "metric": "env-steps/sec (whole node), 24-joint SMPL humanoid, 4096 envs per GPU",
-            "value": total_env_steps / elapsed,
+            "value": processed_all / elapsed,
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -166,17 +232,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (device-generated SMPL clips U{%d..%d} frames @30fps; replayed physics)" % (
-                args.min_len, args.max_len),
-            "config": {"workload": "PHCPufferEnv.step: actions->PD + replay physics + fused obs/reward/reset + "
-                                   "reset re-init (no policy)", "envs_per_gpu": args.envs,
+            "data": "synthetic (device-generated SMPL clips U{%d..%d} frames @30fps; replayed physics; "
+                    "random-init policy)" % (args.min_len, args.max_len),
+            "config": {"workload": workloads[args.mode], "mode": args.mode, "envs_per_gpu": args.envs,
                        "global_envs": args.envs * world, "motions_per_gpu": args.envs,
-                       "parallelism": f"dp{world} (env shards)"},
+                       "parallelism": f"dp{world} (env shards, RCCL grad all-reduce)"},
             "roofline": {"bound": "hbm", "kernel": "phc_env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel_us": kern_s * 1e6, "algorithmic_bytes_per_env_step": BYTES_PER_ENV_STEP},
+                         "kernel_us": kern_s * 1e6, "launches_timed": env_steps,
+                         "algorithmic_bytes_per_env_step": BYTES_PER_ENV_STEP},
             "cpu_baseline": cpu,
-            "resets_in_timed_region": resets,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

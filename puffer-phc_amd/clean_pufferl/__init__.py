@@ -1,0 +1,1 @@
+from .core import close, create, evaluate, train  # noqa: F401

@@ -1,0 +1,227 @@
+"""clean_pufferl trainer API (puffer_phc/clean_pufferl/core.py:41-455): create / evaluate /
+train / close, with the rollout buffer, GAE (phc_gae) and RMS statistics (phc_rms_*) on the
+MI355X, and data parallelism over ranks (distributed.py).
+
+Differences from the reference that do not change the math:
+  * actions stay on the device (no .cpu().numpy() round trip per step);
+  * GAE runs on the device over the same env-sorted flat arrays (the reference's Cython
+    pass on the host, core.py:249);
+  * per-parameter grad norms and loss scalars accumulate on the device and are read once
+    per train() call instead of ~46 .item() syncs per minibatch;
+  * with world_size > 1, gradients are averaged across ranks before clipping and the
+    advantage normalisation uses global statistics (see distributed.py).
+"""
+
+from collections import defaultdict
+
+import numpy as np
+import torch
+
+from .. import _native
+from .. import distributed as D
+from .structs import Experience, LossComponents, Profile, StatsData, TrainComponents, TrainInfo, Utilization
+from .utils import count_params, save_checkpoint, seed_everything
+
+
+def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=None):
+    seed_everything(train_cfg.seed + D.rank(), train_cfg.torch_deterministic)
+    profile = Profile()
+    utilization = Utilization()
+    msg = f"Model Size: {count_params(policy)} parameters"
+    vecenv.async_reset(train_cfg.seed)
+    obs_shape = vecenv.single_observation_space.shape
+    atn_shape = vecenv.single_action_space.shape
+    experience = Experience(train_cfg.batch_size, train_cfg.bptt_horizon, train_cfg.minibatch_size, obs_shape,
+                            atn_shape=atn_shape, device=train_cfg.device, use_amp_obs=env_cfg.use_amp_obs,
+                            amp_obs_size=getattr(vecenv.amp_observation_space, "shape", (1960,))[0]
+                            if env_cfg.use_amp_obs else 1960)
+    D.broadcast_params(policy)
+    uncompiled_policy = policy
+    if train_cfg.compile:
+        policy = torch.compile(policy)
+    if optimizer is None:
+        optimizer = torch.optim.Adam(policy.parameters(), lr=train_cfg.learning_rate, eps=1e-5)
+    initial_params = {name: p.detach().clone() for name, p in policy.named_parameters()}
+    components = TrainComponents(vecenv=vecenv, policy=policy, uncompiled_policy=uncompiled_policy,
+                                 experience=experience, optimizer=optimizer)
+    components.flat_grads = D.FlatGrads(uncompiled_policy.parameters())
+    components.gae = _native.GAE()
+    info = TrainInfo(config=train_cfg, exp_id=exp_id, env_name=env_cfg.name, stats=StatsData(), msg=msg,
+                     last_log_time=0, use_amp_obs=env_cfg.use_amp_obs, initial_params=initial_params,
+                     profile=profile, wandb=wandb)
+    return components, info, utilization
+
+
+def evaluate(components, info):
+    """Rollout until the buffer holds batch_size mask-true rows (core.py:120-203)."""
+    train_cfg, profile, experience = info.config, info.profile, components.experience
+    policy = components.policy
+    env_infos = defaultdict(list)
+    with profile.evaluate:
+        while not experience.full:
+            with profile.env:
+                o, r, d, t, env_info, env_id, mask = components.vecenv.recv()
+            with profile.eval_misc:
+                n_valid = int(mask.sum().item())
+                info.global_step += n_valid
+            with profile.eval_forward, torch.no_grad():
+                actions, logprob, _, value = policy(o)
+            with profile.eval_misc:
+                amp_obs = components.vecenv.amp_obs if info.use_amp_obs else None
+                experience.store(o, amp_obs, value.flatten(), actions, logprob, r, d, t, env_id, mask, n_valid)
+                for i in env_info:
+                    for k, v in i.items():
+                        env_infos[k].append(v)
+            with profile.env:
+                components.vecenv.send(actions)
+        for k, v in env_infos.items():
+            info.stats.extend(k, list(np.atleast_1d(v)))
+    experience.ptr = 0
+    experience.step = 0
+    return info.stats, env_infos
+
+
+def compute_advantages(components, info):
+    """Sort to (env, step) order, adversarial reward, GAE, minibatch layout (core.py:212-260)."""
+    cfg, experience = info.config, components.experience
+    idxs = experience.sort_training_data()
+    dones = experience.dones[idxs].contiguous()
+    values = experience.values[idxs].contiguous()
+    rewards = experience.rewards[idxs].contiguous()
+    experience.flatten_batch()
+    adv_rew = torch.zeros((experience.num_minibatches, cfg.minibatch_size), device=cfg.device)
+    discriminate = getattr(components.policy.policy, "discriminate", None) if hasattr(components.policy, "policy") \
+        else None
+    if info.use_amp_obs and discriminate is not None:
+        with torch.no_grad():
+            for mb in range(experience.num_minibatches):
+                logits = discriminate(experience.b_amp_obs[mb]).squeeze()
+                prob = 1 / (1 + torch.exp(-logits))
+                adv_rew[mb] = -torch.log(torch.clamp(1 - prob, min=0.0001))
+    # the adversarial reward is indexed like the reference: flat ravel of [num_mb, mb_size]
+    advantages = components.gae(dones, values, (rewards + adv_rew.reshape(-1)).contiguous(), cfg.gamma,
+                                cfg.gae_lambda)
+    experience.b_advantages = (advantages.reshape(experience.minibatch_rows, experience.num_minibatches,
+                                                  experience.bptt_horizon)
+                               .transpose(0, 1).reshape(experience.num_minibatches, experience.minibatch_size))
+    experience.returns = advantages + values
+    experience.sorted_values = values
+    experience.b_returns = experience.b_advantages + experience.b_values
+    return advantages
+
+
+def train(components, info, utilization=None):
+    """PPO update (core.py:206-440)."""
+    cfg, profile = info.config, info.profile
+    experience = components.experience
+    pol = components.policy.policy if hasattr(components.policy, "policy") else components.policy
+    flat = components.flat_grads
+    acc = torch.zeros(12, dtype=torch.float64, device=cfg.device)  # device-side loss accumulators
+    with profile.train:
+        with profile.train_misc:
+            compute_advantages(components, info)
+            if info.use_amp_obs:
+                amp_obs_demo = components.vecenv.fetch_amp_obs_demo()
+                amp_mb = amp_obs_demo.shape[0]
+        total_minibatches = experience.num_minibatches * cfg.update_epochs
+        obs_dim = components.vecenv.single_observation_space.shape[0]
+        for _epoch in range(cfg.update_epochs):
+            for mb in range(experience.num_minibatches):
+                with profile.train_misc:
+                    obs = experience.b_obs[mb].reshape(-1, obs_dim)
+                    atn = experience.b_actions[mb].reshape(-1, experience.b_actions.shape[-1])
+                    log_probs = experience.b_logprobs[mb].reshape(-1)
+                    val = experience.b_values[mb]
+                    adv = experience.b_advantages[mb]
+                    ret = experience.b_returns[mb]
+                with profile.train_forward:
+                    _, newlogprob, entropy, newvalue = components.policy(obs, action=atn)
+                with profile.train_misc:
+                    logratio = newlogprob - log_probs
+                    ratio = logratio.exp()
+                    with torch.no_grad():
+                        old_approx_kl = (-logratio).mean()
+                        approx_kl = ((ratio - 1) - logratio).mean()
+                        clipfrac = ((ratio - 1.0).abs() > cfg.clip_coef).float().mean()
+                    adv = adv.reshape(-1)
+                    if cfg.norm_adv:
+                        mean, std = D.global_mean_std(adv)
+                        adv = (adv - mean) / (std + 1e-8)
+                    pg_loss1 = -adv * ratio
+                    pg_loss2 = -adv * torch.clamp(ratio, 1 - cfg.clip_coef, 1 + cfg.clip_coef)
+                    pg_loss = torch.max(pg_loss1, pg_loss2).mean()
+                    newvalue = newvalue.view(-1)
+                    if cfg.clip_vloss:
+                        v_unclipped = (newvalue - ret) ** 2
+                        v_clipped = val + torch.clamp(newvalue - val, -cfg.vf_clip_coef, cfg.vf_clip_coef)
+                        v_loss = torch.max(v_unclipped, (v_clipped - ret) ** 2).mean()
+                    else:
+                        v_loss = ((newvalue - ret) ** 2).mean()
+                    entropy_loss = entropy.mean()
+                    loss = pg_loss - cfg.ent_coef * entropy_loss + v_loss * cfg.vf_coef
+                    disc_loss = torch.zeros((), device=cfg.device)
+                    if info.use_amp_obs:
+                        amp_agent = torch.cat([experience.b_amp_obs[mb][:amp_mb],
+                                               experience.b_amp_obs_replay[mb][:amp_mb]])
+                        d_agent = pol.discriminate(amp_agent)
+                        d_demo = pol.discriminate(amp_obs_demo)
+                        bce = torch.nn.BCEWithLogitsLoss()
+                        disc_loss = 0.5 * (bce(d_agent, torch.zeros_like(d_agent)) + bce(d_demo, torch.ones_like(d_demo)))
+                        if cfg.disc_coef > 0:
+                            loss = loss + disc_loss * cfg.disc_coef
+                    mbl = getattr(pol, "mean_bound_loss", None)
+                    if cfg.bound_coef > 0 and mbl is not None:
+                        loss = loss + mbl * cfg.bound_coef
+                    l2 = torch.zeros((), device=cfg.device)
+                    for name, p in components.policy.named_parameters():
+                        if name in info.initial_params:
+                            l2 = l2 + (p - info.initial_params[name]).pow(2).mean()
+                    if cfg.l2_reg_coef > 0:
+                        loss = loss + l2 * cfg.l2_reg_coef
+                with profile.learn:
+                    flat.zero()
+                    loss.backward()
+                    flat.allreduce_mean()
+                    gnorm = flat.norms_sum()
+                    torch.nn.utils.clip_grad_norm_(flat.params, cfg.max_grad_norm)
+                    components.optimizer.step()
+                with profile.train_misc, torch.no_grad():
+                    acc += torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,
+                                        approx_kl, clipfrac, gnorm, l2.detach(), disc_loss.detach(),
+                                        (mbl.detach() if mbl is not None else torch.zeros((), device=cfg.device)),
+                                        torch.zeros((), device=cfg.device),
+                                        torch.zeros((), device=cfg.device)]).double() / total_minibatches
+            if cfg.target_kl is not None and float(approx_kl) > cfg.target_kl:
+                break
+        with profile.train_misc:
+            a = acc.cpu().numpy()
+            losses = LossComponents(policy_loss=a[0], value_loss=a[1], entropy=a[2], old_approx_kl=a[3],
+                                    approx_kl=a[4], clipfrac=a[5], before_clip_grad_norm=a[6],
+                                    l2_init_reg_loss=a[7], disc_loss=a[8], mean_bound_loss=a[9])
+            y_pred = experience.sorted_values
+            y_true = experience.returns
+            var_y = torch.var(y_true, unbiased=False)
+            ev = (1 - torch.var(y_true - y_pred, unbiased=False) / var_y) if float(var_y) != 0 else float("nan")
+            losses.explained_variance = float(ev)
+            info.epoch += 1
+            info.losses = losses
+            done_training = info.global_step >= cfg.total_timesteps
+            if done_training or profile.update(components, info):
+                info.stats.mean_and_log(components, info, losses)
+                info.stats.clear()
+            if D.rank() == 0 and (info.epoch % cfg.checkpoint_interval == 0 or done_training):
+                save_checkpoint(components.uncompiled_policy, components.optimizer, cfg, info.exp_id, info.epoch,
+                                info.global_step)
+                info.msg = f"Checkpoint saved at update {info.epoch}"
+    return losses
+
+
+def close(components, info, utilization=None):
+    components.vecenv.close()
+    if utilization is not None:
+        utilization.stop()
+    if info.wandb is not None:
+        if D.rank() == 0:
+            save_checkpoint(components.uncompiled_policy, components.optimizer, info.config, info.exp_id, info.epoch,
+                            info.global_step)
+        info.wandb.finish()

@@ -196,7 +196,10 @@ __global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, Ste
 //   terminals/truncations/masks and episode return/length (clean_pufferl/env.py:103-140)
 //   and, with AUTO, the env.reset(reset_indices) of the envs that came up for reset.
 template <bool AUTO>
-__global__ __launch_bounds__(kBlock) void k_env_step(EnvView e, LibView l, StepConsts c) {
+#ifndef PHC_ENV_WAVES_PER_SIMD
+#define PHC_ENV_WAVES_PER_SIMD 3
+#endif
+__global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(EnvView e, LibView l, StepConsts c) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
   const int g = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + g;

@@ -1,0 +1,112 @@
+"""Data parallelism over GPUs: one process per GPU, torch.distributed over RCCL (xGMI).
+
+Envs shard across ranks (each rank steps its own envs and motion library: no data-path
+collective in the rollout).  The PPO update needs exactly these collectives:
+  (1) the gradient all-reduce of every minibatch — gradients live in ONE flat fp32 buffer
+      (parameters' .grad are views into it), reduced in `bucket_bytes` slices so RCCL runs a
+      few large ring all-reduces instead of one per parameter;
+  (2) the advantage-normalisation statistics (sum, sum of squares, count) per minibatch;
+  (3) the RunningNorm batch statistics (policies/running_norm.py);
+  (4) scalar loss / SPS reductions for logging;
+  (5) a broadcast of the initial parameters so replicas start identical.
+With world_size 1 every helper is a no-op and the math is the reference's single-GPU math.
+"""
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def is_dist():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def world_size():
+    return dist.get_world_size() if is_dist() else 1
+
+
+def rank():
+    return dist.get_rank() if is_dist() else 0
+
+
+def init_from_env(backend=None):
+    """Initialise from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+        return rank(), world_size()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend, device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return rank(), world_size()
+
+
+class FlatGrads:
+    """Parameters' gradients as views into one flat buffer, all-reduced (averaged) in buckets."""
+
+    def __init__(self, params, bucket_bytes=32 << 20):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            p.grad = self.flat[off:off + k].view_as(p)
+            off += k
+        self.bucket = max(1, bucket_bytes // 4)
+
+    def zero(self):
+        self.flat.zero_()
+
+    def allreduce_mean(self):
+        if not is_dist():
+            return
+        ws = world_size()
+        works = []
+        for s in range(0, self.flat.numel(), self.bucket):
+            works.append(dist.all_reduce(self.flat[s:s + self.bucket], async_op=True))
+        for w in works:
+            w.wait()
+        self.flat.div_(ws)
+
+    def norms_sum(self):
+        """sum over parameters of ||grad_p|| (clean_pufferl/core.py:366-368), on device."""
+        return torch.stack([torch.linalg.vector_norm(p.grad) for p in self.params]).sum()
+
+
+def broadcast_params(module, src=0):
+    if not is_dist():
+        return
+    for t in list(module.parameters()) + list(module.buffers()):
+        dist.broadcast(t.data, src)
+
+
+def global_mean_std(x):
+    """Mean and unbiased std over all ranks' elements of x (torch.std semantics)."""
+    if not is_dist():
+        return x.mean(), x.std()
+    xd = x.double()
+    buf = torch.stack([xd.sum(), (xd * xd).sum(),
+                       torch.tensor(float(x.numel()), dtype=torch.float64, device=x.device)])
+    dist.all_reduce(buf)
+    n = buf[2]
+    mean = buf[0] / n
+    var = (buf[1] - n * mean * mean) / (n - 1)
+    return mean.float(), var.clamp_min(0).sqrt().float()
+
+
+def allreduce_sum_(t):
+    if is_dist():
+        dist.all_reduce(t)
+    return t
+
+
+def allreduce_max_(t):
+    if is_dist():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t

@@ -1,0 +1,45 @@
+"""PHCPolicy (puffer_phc/policies/phc_policy.py:10-61): 6-layer SiLU actor and critic with a
+LayerNorm head, fixed-sigma Normal.  State-dict keys match the reference
+(tests/golden/state_dict_keys.tsv)."""
+
+from typing import Sequence
+
+import torch
+from torch import nn
+
+from .discriminator_policy import DiscriminatorPolicy
+from .pufferl_policy import layer_init
+
+
+def mlp(layer_sizes, activation):
+    layers = []
+    for a, b in zip(layer_sizes[:-2], layer_sizes[1:-1]):
+        layers.append(layer_init(nn.Linear(a, b)))
+        layers.append(activation())
+    layers.append(layer_init(nn.Linear(layer_sizes[-2], layer_sizes[-1])))
+    return layers
+
+
+class PHCPolicy(DiscriminatorPolicy):
+    def __init__(self, env, hidden_size: int = 512, layer_sizes: Sequence[int] = (2048, 1536, 1024, 1024, 512)):
+        super().__init__(env, hidden_size)
+        self.actor_mlp = nn.Sequential(*mlp([self.input_size] + list(layer_sizes) + [hidden_size], nn.SiLU),
+                                       nn.LayerNorm(hidden_size), nn.SiLU())
+        self.critic_mlp = nn.Sequential(*mlp([self.input_size] + list(layer_sizes) + [hidden_size], nn.SiLU),
+                                        nn.LayerNorm(hidden_size), nn.SiLU(),
+                                        layer_init(nn.Linear(hidden_size, 1), std=0.01))
+
+    def encode_observations(self, obs):
+        self.obs_pointer = self.obs_norm(obs)
+        return self.actor_mlp(self.obs_pointer), None
+
+    def decode_actions(self, hidden, lookup=None):
+        mu = self.mu(hidden)
+        std = torch.exp(self.sigma).expand_as(mu)
+        if self._deterministic_action is True:
+            std = torch.clamp(std, max=1e-6)
+        probs = torch.distributions.Normal(mu, std, validate_args=False)  # no host-syncing checks
+        if self.training:
+            self.mean_bound_loss = self.bound_loss(mu)
+        value = self.critic_mlp(self.obs_pointer)
+        return probs, value

@@ -1,0 +1,89 @@
+"""Data-parallel collectives (distributed.py, RunningNorm) on CPU with gloo, world_size 2.
+
+Each check compares the 2-rank result with the single-process computation over the union of
+both ranks' data (what one GPU would have computed on the whole global batch)."""
+
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import phc_oracle as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _data(rank, n=64, f=12):
+    g = torch.Generator().manual_seed(100 + rank)
+    return torch.randn(n, f, generator=g) * (1 + rank) + rank, torch.randn(n, 1, generator=g)
+
+
+def _worker(rank, world, port, root):
+    import sys
+
+    sys.path.insert(0, root)
+    import phc_amd_path
+
+    phc_amd_path.register()
+    from puffer_phc_amd import distributed as D
+    from puffer_phc_amd.policies.running_norm import RunningNorm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # (5) parameter broadcast: rank 1 starts from a different init
+        torch.manual_seed(rank)
+        net = torch.nn.Sequential(torch.nn.Linear(12, 16), torch.nn.SiLU(), torch.nn.Linear(16, 1))
+        D.broadcast_params(net)
+        torch.manual_seed(0)
+        ref_net = torch.nn.Sequential(torch.nn.Linear(12, 16), torch.nn.SiLU(), torch.nn.Linear(16, 1))
+        for a, b in zip(net.parameters(), ref_net.parameters()):
+            assert torch.equal(a, b)
+        # (1) flat-bucket gradient all-reduce == gradient of the mean loss over both ranks
+        fg = D.FlatGrads(net.parameters(), bucket_bytes=256)  # force several buckets
+        x, y = _data(rank)
+        fg.zero()
+        ((net(x) - y) ** 2).mean().backward()
+        fg.allreduce_mean()
+        xs = torch.cat([_data(r)[0] for r in range(world)])
+        ys = torch.cat([_data(r)[1] for r in range(world)])
+        ref_net.zero_grad()
+        ((ref_net(xs) - ys) ** 2).mean().backward()
+        for p, q in zip(net.parameters(), ref_net.parameters()):
+            torch.testing.assert_close(p.grad, q.grad, atol=1e-6, rtol=1e-5)
+        # (2) global advantage statistics
+        adv = x[:, 0].contiguous()
+        m, s = D.global_mean_std(adv)
+        allv = xs[:, 0]
+        torch.testing.assert_close(m, allv.mean(), atol=1e-6, rtol=1e-6)
+        torch.testing.assert_close(s, allv.std(), atol=1e-6, rtol=1e-6)
+        # (3) RunningNorm stats over the global batch
+        rn = RunningNorm(12)
+        rn.update(x)
+        rn.update(x * 2)
+        mean, var, cnt = np.zeros((1, 12), np.float32), np.ones((1, 12), np.float32), np.ones(1, np.float32)
+        mean, var, cnt = O.rms_update(mean, var, cnt, xs.numpy())
+        mean, var, cnt = O.rms_update(mean, var, cnt, (xs * 2).numpy())
+        np.testing.assert_allclose(rn.running_mean.numpy(), mean, atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(rn.running_var.numpy(), var, atol=1e-5, rtol=1e-5)
+        assert float(rn.count) == float(cnt[0])
+        # (4) scalar reductions
+        t = torch.tensor([float(rank + 1)])
+        D.allreduce_max_(t)
+        assert float(t) == world
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collectives_world2():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mp.spawn(_worker, args=(2, _free_port(), root), nprocs=2, join=True)

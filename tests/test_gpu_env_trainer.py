@@ -1,0 +1,144 @@
+"""End-to-end HIP path: motion-library build, multi-step env parity with the oracle (including
+in-launch resets), and the on-device PPO trainer (needs an MI355X)."""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import phc_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _oracle_lib(packed):
+    fr = packed.frames.cpu().numpy()
+    return O.MotionLib(fr[..., 0:3], fr[..., 3:7], packed.local_rot.cpu().numpy(), fr[..., 7:10], fr[..., 10:13],
+                       packed.dof_vel.cpu().numpy(), packed.num_frames.cpu().numpy(),
+                       (1.0 / packed.motion_dt.double()).cpu().numpy())
+
+
+@pytest.fixture(scope="module")
+def small_env():
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    q, t, c, fps = synthetic_clips(64, 20, 90, seed=5, device=DEV)
+    packed = PackedMotions.from_global_rotations(q, t, c, fps)
+    env = PHCPufferEnv(EnvConfig(num_envs=64, seed=3), motion_data=packed)
+    env.reset()
+    return env, packed, (q.cpu().numpy(), t.cpu().numpy(), c.cpu().numpy())
+
+
+def test_fk_library_vs_oracle(small_env):
+    from puffer_phc_amd.skeleton import SkeletonTree
+
+    env, packed, (q, t, c) = small_env
+    sk = SkeletonTree.smpl()
+    starts = np.concatenate([[0], np.cumsum(c)[:-1]])
+    fr = packed.frames.cpu().numpy()
+    for m in (0, 17, 63):
+        sl = slice(starts[m], starts[m] + c[m])
+        out = O.fk_motion(sk.parent_indices.numpy(), sk.local_translation.numpy(), q[sl], t[sl], fps=30)
+        np.testing.assert_allclose(fr[sl, :, 0:3], out["gts"], atol=2e-5, rtol=1e-5)
+        np.testing.assert_allclose(fr[sl, :, 7:10], out["gvs"], atol=2e-5, rtol=1e-5)
+        np.testing.assert_allclose(fr[sl, :, 10:13], out["gavs"], atol=2e-5, rtol=1e-5)
+        np.testing.assert_allclose(packed.local_rot[sl].cpu().numpy(), out["lrs"], atol=1e-6)
+        np.testing.assert_allclose(packed.dof_vel[sl].cpu().numpy(), out["dvs"], atol=2e-5, rtol=1e-5)
+
+
+def test_multi_step_parity_with_resets(small_env):
+    """20 steps of PHCPufferEnv.step at the kernel level: every env's reward/obs/flags match the
+    oracle; envs that reset are re-initialised at a 1/30-snapped time with the old offset."""
+    from puffer_phc_amd import _native as N
+
+    env, packed, _ = small_env
+    e = env.env
+    lib = _oracle_lib(packed)
+    ids = e._sampled_motion_ids.cpu().numpy()
+    seen_reset = 0
+    for step in range(20):
+        e.physics.step(e)  # replay physics writes rigid bodies / dof state
+        pre = dict(progress=e.progress_buf.cpu().numpy().astype(np.int32), start=e._motion_start_times.cpu().numpy(),
+                   off=e._motion_start_times_offset.cpu().numpy(), goff=e._global_offset.cpu().numpy(),
+                   rb=e._rigid_body_state.cpu().numpy(), dv=e._dof_vel.cpu().numpy(),
+                   df=e.dof_force_tensor.cpu().numpy())
+        N.env_step(e._env_c, e._motion_lib.packed.c, e._step_params_auto)
+        torch.cuda.synchronize()
+        ref = O.env_step(lib, ids, (pre["progress"] + 1).astype(np.int16), pre["start"], pre["off"], pre["goff"],
+                         pre["rb"], pre["dv"], pre["df"])
+        rew = env.rewards.cpu().numpy()
+        np.testing.assert_allclose(rew, ref["rew"], atol=1e-5, rtol=1e-5)
+        term = env.terminals.cpu().numpy()
+        trunc = env.truncations.cpu().numpy()
+        ties = np.any(np.abs(ref["reset_dist"] - 0.25) < 1e-6, -1)
+        np.testing.assert_array_equal(term[~ties], ref["terminate"][~ties])
+        np.testing.assert_array_equal((term | trunc)[~ties], ref["reset"][~ties])
+        obs = env.observations.cpu().numpy()
+        reset = term | trunc
+        keep = ~reset
+        np.testing.assert_allclose(obs[keep], ref["obs"][keep], atol=1e-5, rtol=1e-5)
+        if reset.any():
+            seen_reset += int(reset.sum())
+            st = e._motion_start_times.cpu().numpy()[reset]
+            lens = lib.motion_lengths[ids[reset]]
+            assert np.all(st >= 0) and np.all(st <= lens + 1e-6)
+            np.testing.assert_allclose(st * 30, np.round(st * 30), atol=1e-3)
+            # re-initialised state = reference at the new start with the OLD global offset
+            ms = O.motion_state(lib, ids[reset], st, pre["goff"][reset])
+            rb = e._rigid_body_state.cpu().numpy()[reset]
+            np.testing.assert_array_equal(rb[..., 0:3], ms["rg_pos"])
+            np.testing.assert_allclose(rb[..., 3:7], ms["rb_rot"], atol=1e-6)
+            # obs after reset: progress 0, offsets 0, reference at dt + start
+            bp, br, bv, bav = ms["rg_pos"], ms["rb_rot"], ms["body_vel"], ms["body_ang_vel"]
+            ms1 = O.motion_state(lib, ids[reset], (np.float32(1) * O.DT + st + np.float32(0)).astype(np.float32),
+                                 np.zeros((reset.sum(), 3), np.float32))
+            exp = np.concatenate([O.humanoid_obs(bp, br, bv, bav),
+                                  O.imitation_obs_v6(bp[:, 0], br[:, 0], bp, br, bv, bav, ms1["rg_pos"], ms1["rb_rot"],
+                                                     ms1["body_vel"], ms1["body_ang_vel"])], -1)
+            np.testing.assert_allclose(obs[reset], exp, atol=1e-5, rtol=1e-5)
+            assert (e.progress_buf[torch.from_numpy(reset).to(DEV)] == 0).all()
+    assert seen_reset > 0  # short clips (20..90 frames) must reach pass_time within 20 steps
+
+
+def test_vecenv_protocol_and_logging(small_env):
+    env, _, _ = small_env
+    env.async_reset(0)
+    for _ in range(env.cfg.log_interval):
+        o, r, d, t, info, ids, mask = env.recv()
+        env.send(torch.zeros((64, 69), device=DEV))
+    _, _, _, _, info, _, _ = env.recv()
+    assert info and "rew_body_pos" in info[0] and 0.0 < info[0]["rew_body_pos"] <= 1.0
+    assert o.shape == (64, 934) and mask.dtype == torch.bool
+
+
+def test_ppo_iteration_trains(small_env):
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.config import TrainConfig
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+
+    env, _, _ = small_env
+    torch.manual_seed(0)
+    policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+    cfg = TrainConfig(batch_size=64 * 16, minibatch_size=256, bptt_horizon=8, checkpoint_interval=10 ** 9)
+    comps, info, util = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+    before = {k: v.detach().clone() for k, v in policy.named_parameters()}
+    clean_pufferl.evaluate(comps, info)
+    exp = comps.experience
+    assert info.global_step >= cfg.batch_size
+    policy.policy.update_obs_rms(exp.obs)
+    # GAE parity on the trainer's own sorted arrays
+    adv = clean_pufferl.core.compute_advantages(comps, info)
+    idx = torch.sort(exp.env_ids, stable=True).indices
+    ref = O.compute_gae(exp.dones[idx].cpu().numpy(), exp.values[idx].cpu().numpy(),
+                        exp.rewards[idx].cpu().numpy(), cfg.gamma, cfg.gae_lambda)
+    np.testing.assert_allclose(adv.cpu().numpy(), ref, atol=1e-5, rtol=1e-5)
+    env_sorted = exp.env_ids[idx].cpu().numpy()
+    assert np.all(np.diff(env_sorted) >= 0)
+    losses = clean_pufferl.train(comps, info, util)
+    assert np.isfinite([losses.policy_loss, losses.value_loss, losses.approx_kl]).all()
+    changed = sum(not torch.equal(before[k], v) for k, v in policy.named_parameters() if v.requires_grad)
+    assert changed > 0
+    assert float(policy.policy.obs_norm.count) == 2.0
