@@ -104,7 +104,7 @@ def cpu_baseline(env, packed, seconds):
     fr = packed.frames.cpu().numpy()
     lib = O.MotionLib(fr[..., 0:3], fr[..., 3:7], packed.local_rot.cpu().numpy(), fr[..., 7:10], fr[..., 10:13],
                       packed.dof_vel.cpu().numpy(), packed.num_frames.cpu().numpy(),
-                      (1.0 / packed.motion_dt.double()).cpu().numpy())
+                      packed.fps.cpu().numpy())
     e = env.env
     args = (e._sampled_motion_ids.cpu().numpy(), (e.progress_buf.cpu().numpy() + 1).astype(np.int16),
             e._motion_start_times.cpu().numpy(), e._motion_start_times_offset.cpu().numpy(),

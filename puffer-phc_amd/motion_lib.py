@@ -62,6 +62,7 @@ class PackedMotions:
         self.local_rot = local_rot
         self.dof_vel = dof_vel
         self.num_frames = num_frames
+        self.fps = fps
         fps64 = fps.double()
         self.motion_dt = (1.0 / fps64).float()
         self.motion_len = (1.0 / fps64 * (num_frames - 1).double()).float()
@@ -266,7 +267,7 @@ class MotionLibBase:
         self._curr_motion_ids = sample_idxes if sample_idxes is not None else torch.arange(M, device=dev)
         self._motion_lengths = packed.motion_len
         self._motion_dt = packed.motion_dt
-        self._motion_fps = (1.0 / packed.motion_dt.double()).float()
+        self._motion_fps = packed.fps
         self._motion_num_frames = packed.num_frames
         self.length_starts = packed.length_starts
         self._motion_aa = torch.zeros((packed.frames.shape[0], 72), device=dev)

@@ -15,7 +15,7 @@ def _oracle_lib(packed):
     fr = packed.frames.cpu().numpy()
     return O.MotionLib(fr[..., 0:3], fr[..., 3:7], packed.local_rot.cpu().numpy(), fr[..., 7:10], fr[..., 10:13],
                        packed.dof_vel.cpu().numpy(), packed.num_frames.cpu().numpy(),
-                       (1.0 / packed.motion_dt.double()).cpu().numpy())
+                       packed.fps.cpu().numpy())
 
 
 @pytest.fixture(scope="module")

@@ -1,13 +1,14 @@
 #!/bin/bash
 # One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats + HBM counters.
 # Every GPU step runs under its own timeout; anything other than a test failure stops the pass.
+#   TESTS=0|1  PROFILE=0|1  ENVS_LIST="4096 32768"  MODES="ppo env"  BENCH_ARGS="..."
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 ENVS_LIST=${ENVS_LIST:-4096}
-STEPS=${STEPS:-200}
+MODES=${MODES:-ppo env}
 BENCH_ARGS=${BENCH_ARGS:-}
 
 if [ "${TESTS:-1}" = "1" ]; then
@@ -18,19 +19,25 @@ if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 3; }
   tail -1 "$OUT/smoke.log"
 fi
-for ENVS in $ENVS_LIST; do
-  EXTRA=""
-  if [ "$ENVS" != "4096" ]; then EXTRA="--no-cpu-baseline"; fi
-  timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 20 --envs "$ENVS" $EXTRA $BENCH_ARGS > "$OUT/bench_$ENVS.log" 2>&1 || { tail -20 "$OUT/bench_$ENVS.log"; exit 4; }
-  tail -1 "$OUT/bench_$ENVS.log"
-  if [ "${PROFILE:-1}" = "1" ]; then
-    export TMPDIR=/tmp
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_trace_$ENVS" -o run --output-format csv -- \
-      python3 "$ROOT/bench.py" --steps 50 --warmup 10 --envs "$ENVS" --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_trace_$ENVS.log" 2>&1 || { tail -20 "$OUT/prof_trace_$ENVS.log"; exit 5; }
-    for C in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_env_step" -T -d "$OUT/prof_${C}_$ENVS" -o run --output-format csv -- \
-        python3 "$ROOT/bench.py" --steps 20 --warmup 5 --envs "$ENVS" --no-cpu-baseline $BENCH_ARGS > "$OUT/prof_${C}_$ENVS.log" 2>&1 || { tail -20 "$OUT/prof_${C}_$ENVS.log"; exit 6; }
-    done
-  fi
+for MODE in $MODES; do
+  for ENVS in $ENVS_LIST; do
+    EXTRA=""
+    if [ "$ENVS" != "4096" ] || [ "$MODE" != "ppo" ]; then EXTRA="--no-cpu-baseline"; fi
+    LOG="$OUT/bench_${MODE}_$ENVS.log"
+    timeout -k 10 900 python bench.py --mode "$MODE" --envs "$ENVS" $EXTRA $BENCH_ARGS > "$LOG" 2>&1 || { tail -20 "$LOG"; exit 4; }
+    tail -1 "$LOG"
+    if [ "${PROFILE:-1}" = "1" ]; then
+      export TMPDIR=/tmp
+      P="$OUT/prof_trace_${MODE}_$ENVS"
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -T -d "$P" -o run --output-format csv -- \
+        python3 "$ROOT/bench.py" --mode "$MODE" --envs "$ENVS" --no-cpu-baseline $BENCH_ARGS > "$P.log" 2>&1 || { tail -20 "$P.log"; exit 5; }
+      if [ "$MODE" = "env" ]; then
+        for C in FETCH_SIZE WRITE_SIZE; do
+          timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_env_step" -T -d "$OUT/prof_${C}_$ENVS" -o run --output-format csv -- \
+            python3 "$ROOT/bench.py" --mode env --steps 20 --warmup 5 --envs "$ENVS" --no-cpu-baseline > "$OUT/prof_${C}_$ENVS.log" 2>&1 || { tail -20 "$OUT/prof_${C}_$ENVS.log"; exit 6; }
+        done
+      fi
+    fi
+  done
 done
 echo "gpu_check done"
