@@ -76,7 +76,7 @@ class FlatGrads:
 
     def norms_sum(self):
         """sum over parameters of ||grad_p|| (clean_pufferl/core.py:366-368), on device."""
-        return torch.stack([torch.linalg.vector_norm(p.grad) for p in self.params]).sum()
+        return torch.stack(torch._foreach_norm([p.grad for p in self.params])).sum()
 
 
 def broadcast_params(module, src=0):
