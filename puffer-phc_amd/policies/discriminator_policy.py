@@ -3,7 +3,7 @@
 import torch
 from torch import nn
 
-from .pufferl_policy import layer_init
+from .pufferl_policy import Linear, layer_init
 from .running_norm import RunningNorm
 
 
@@ -17,7 +17,7 @@ class DiscriminatorPolicy(nn.Module):
         self.soft_bound = 0.9 * float(env.single_action_space.high[0])
         self.obs_norm = RunningNorm(self.input_size)
         self.actor_mlp = None
-        self.mu = nn.Sequential(layer_init(nn.Linear(hidden_size, self.action_size), std=0.01))
+        self.mu = nn.Sequential(layer_init(Linear(hidden_size, self.action_size), std=0.01))
         self.sigma = nn.Parameter(torch.zeros(self.action_size, dtype=torch.float32), requires_grad=False)
         nn.init.constant_(self.sigma, -2.9)
         self.critic_mlp = None
@@ -26,9 +26,9 @@ class DiscriminatorPolicy(nn.Module):
         if self.use_amp_obs:
             amp_obs_size = env.amp_observation_space.shape[0]
             self.amp_obs_norm = RunningNorm(amp_obs_size)
-            self._disc_mlp = nn.Sequential(layer_init(nn.Linear(amp_obs_size, 1024)), nn.ReLU(),
-                                           layer_init(nn.Linear(1024, hidden_size)), nn.ReLU())
-            self._disc_logits = layer_init(nn.Linear(hidden_size, 1))
+            self._disc_mlp = nn.Sequential(layer_init(Linear(amp_obs_size, 1024)), nn.ReLU(),
+                                           layer_init(Linear(1024, hidden_size)), nn.ReLU())
+            self._disc_logits = layer_init(Linear(hidden_size, 1))
         self.obs_pointer = None
         self.mean_bound_loss = None
 

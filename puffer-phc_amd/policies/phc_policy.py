@@ -8,15 +8,15 @@ import torch
 from torch import nn
 
 from .discriminator_policy import DiscriminatorPolicy
-from .pufferl_policy import layer_init
+from .pufferl_policy import Linear, layer_init
 
 
 def mlp(layer_sizes, activation):
     layers = []
     for a, b in zip(layer_sizes[:-2], layer_sizes[1:-1]):
-        layers.append(layer_init(nn.Linear(a, b)))
+        layers.append(layer_init(Linear(a, b)))
         layers.append(activation())
-    layers.append(layer_init(nn.Linear(layer_sizes[-2], layer_sizes[-1])))
+    layers.append(layer_init(Linear(layer_sizes[-2], layer_sizes[-1])))
     return layers
 
 
@@ -27,7 +27,7 @@ class PHCPolicy(DiscriminatorPolicy):
                                        nn.LayerNorm(hidden_size), nn.SiLU())
         self.critic_mlp = nn.Sequential(*mlp([self.input_size] + list(layer_sizes) + [hidden_size], nn.SiLU),
                                         nn.LayerNorm(hidden_size), nn.SiLU(),
-                                        layer_init(nn.Linear(hidden_size, 1), std=0.01))
+                                        layer_init(Linear(hidden_size, 1), std=0.01))
 
     def encode_observations(self, obs):
         self.obs_pointer = self.obs_norm(obs)

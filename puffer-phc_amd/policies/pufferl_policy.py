@@ -11,6 +11,15 @@ import torch
 from torch import nn
 
 
+class Linear(nn.Linear):
+    """nn.Linear whose GEMM runs without the fused-bias epilogue: on gfx950 hipBLASLt serves the
+    'high' float32 precision (xf32 emulation, 2x fp32 MFMA rate) only for plain GEMMs, so the
+    bias is added by one elementwise pass.  Same parameters / state-dict keys as nn.Linear."""
+
+    def forward(self, x):
+        return torch.matmul(x, self.weight.t()) + self.bias
+
+
 def layer_init(layer, std=np.sqrt(2), bias_const=0.0):
     """pufferlib.pytorch.layer_init: orthogonal weights, constant bias."""
     torch.nn.init.orthogonal_(layer.weight, std)
