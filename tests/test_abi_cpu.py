@@ -1,0 +1,76 @@
+"""The C-ABI library loads on a machine without a GPU and exports every symbol phc.h declares
+(no compute calls)."""
+
+import os
+import re
+
+from puffer_phc_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "phc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(phc_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.load_library()
+    names = _declared()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_native._EXPORTS), "binding and header disagree"
+
+
+def test_host_only_queries():
+    lib = _native.lib()
+    assert lib.phc_version() == 1
+    assert lib.phc_stats_blocks(4096) == 512 and lib.phc_stats_blocks(0) == 0
+    assert lib.phc_gae_workspace_bytes(131072) > 0
+    assert lib.phc_rms_workspace_bytes(131072, 934) == 256 * 934 * 2 * 8
+    assert lib.phc_fk_workspace_bytes(1000) >= 1000 * 24 * 3 * 12
+
+
+def test_struct_layouts_match_header_sizes():
+    import ctypes
+
+    # 22 pointers/ints in phc_env_buffers, 9 fields in phc_motion_lib
+    assert ctypes.sizeof(_native.EnvBuffersC) == 8 * 22
+    assert ctypes.sizeof(_native.MotionLibC) == 8 * 9
+    # 10 floats + 4 int32 + 24 floats + int32 + pad + uint64
+    assert ctypes.sizeof(_native.StepParamsC) == 4 * (10 + 4 + 24 + 1) + 4 + 8
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    import pytest
+
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _native.load_library(str(tmp_path / "nope.so"))
+
+
+def test_struct_offsets_match_c_compiler(tmp_path):
+    """Compile a probe against include/phc.h with gcc and compare every field offset with the
+    ctypes mirror."""
+    import ctypes
+    import subprocess
+
+    structs = {"phc_env_buffers": _native.EnvBuffersC, "phc_motion_lib": _native.MotionLibC,
+               "phc_step_params": _native.StepParamsC, "phc_ref_state": _native.RefStateC}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "phc.h"', "int main(void){"]
+    for s, cls in structs.items():
+        lines.append(f'printf("{s} size %zu\\n", sizeof({s}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{s} {f} %zu\\n", offsetof({s}, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for s, cls in structs.items():
+        assert got[(s, "size")] == ctypes.sizeof(cls), s
+        for f, _ in cls._fields_:
+            assert got[(s, f)] == getattr(cls, f).offset, (s, f)
