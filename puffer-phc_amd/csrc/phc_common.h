@@ -139,36 +139,39 @@ __device__ __forceinline__ float group_bcast(float v) { return __shfl(v, 0, kGro
 // ------------------------------------------------------------ observation --
 // One body's slices of the 934-float observation (common.py:23-103 self obs with
 // local_root_obs/root_height_obs/upright; common.py:107-176 imitation obs v6, time_steps 1).
-__device__ __forceinline__ void write_obs_body(float *__restrict__ o, int b, const BodyRec &s, v3 root_p, q4 hinv,
-                                               q4 hrot, const BodyRec &ref) {
+// The heading rotations use the exact specialisations of phc_quat.h (rot_heading,
+// qmul_heading_*, tan_norm_fast): same float32 values as the generic formulas (only the sign
+// of some exact zeros can differ; checked over 40 steps x 2048 envs with tools/ab_compare.py).
+__device__ __forceinline__ void write_obs_body(float *__restrict__ o, int b, const BodyRec &s, v3 root_p,
+                                               const Heading &hinv, const Heading &hrot, const BodyRec &ref) {
   float t6[6];
   if (b == 0) {
     o[0] = root_p.z;
   } else {
-    const v3 lp = my_quat_rotate(hinv, vsub(s.p, root_p));
+    const v3 lp = rot_heading(hinv, vsub(s.p, root_p));
     float *d = o + 1 + 3 * (b - 1);
     d[0] = lp.x; d[1] = lp.y; d[2] = lp.z;
   }
-  quat_to_tan_norm(quat_mul(hinv, s.r), t6);
+  tan_norm_fast(qmul_heading_left(hinv, s.r), t6);
 #pragma unroll
   for (int k = 0; k < 6; ++k) o[70 + 6 * b + k] = t6[k];
-  v3 x = my_quat_rotate(hinv, s.v);
+  v3 x = rot_heading(hinv, s.v);
   o[214 + 3 * b] = x.x; o[215 + 3 * b] = x.y; o[216 + 3 * b] = x.z;
-  x = my_quat_rotate(hinv, s.av);
+  x = rot_heading(hinv, s.av);
   o[286 + 3 * b] = x.x; o[287 + 3 * b] = x.y; o[288 + 3 * b] = x.z;
   // task obs
-  x = my_quat_rotate(hinv, vsub(ref.p, s.p));
+  x = rot_heading(hinv, vsub(ref.p, s.p));
   o[358 + 3 * b] = x.x; o[359 + 3 * b] = x.y; o[360 + 3 * b] = x.z;
-  quat_to_tan_norm(quat_mul(quat_mul(hinv, quat_mul(ref.r, quat_conj(s.r))), hrot), t6);
+  tan_norm_fast(qmul_heading_right(qmul_heading_left(hinv, quat_mul(ref.r, quat_conj(s.r))), hrot), t6);
 #pragma unroll
   for (int k = 0; k < 6; ++k) o[430 + 6 * b + k] = t6[k];
-  x = my_quat_rotate(hinv, vsub(ref.v, s.v));
+  x = rot_heading(hinv, vsub(ref.v, s.v));
   o[574 + 3 * b] = x.x; o[575 + 3 * b] = x.y; o[576 + 3 * b] = x.z;
-  x = my_quat_rotate(hinv, vsub(ref.av, s.av));
+  x = rot_heading(hinv, vsub(ref.av, s.av));
   o[646 + 3 * b] = x.x; o[647 + 3 * b] = x.y; o[648 + 3 * b] = x.z;
-  x = my_quat_rotate(hinv, vsub(ref.p, root_p));
+  x = rot_heading(hinv, vsub(ref.p, root_p));
   o[718 + 3 * b] = x.x; o[719 + 3 * b] = x.y; o[720 + 3 * b] = x.z;
-  quat_to_tan_norm(quat_mul(hinv, ref.r), t6);
+  tan_norm_fast(qmul_heading_left(hinv, ref.r), t6);
 #pragma unroll
   for (int k = 0; k < 6; ++k) o[790 + 6 * b + k] = t6[k];
 }

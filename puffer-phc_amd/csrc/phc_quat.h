@@ -96,6 +96,58 @@ __device__ __forceinline__ void quat_to_tan_norm(q4 q, float out[6]) {
   out[3] = n.x; out[4] = n.y; out[5] = n.z;
 }
 
+// ---- exact specialisations -------------------------------------------------------------
+// The reference evaluates its generic formulas on operands with structural zeros (unit axes,
+// heading quaternions (0,0,z,w)).  Every product with such a zero is +-0 and every sum with it
+// is exact, so dropping those terms (keeping the association of the surviving ones) gives the
+// same float32 result bit for bit (up to the sign of an exact zero) at a third of the VALU cost.
+
+// quat_to_tan_norm(q) = [my_quat_rotate(q, x-axis), my_quat_rotate(q, z-axis)]
+__device__ __forceinline__ void tan_norm_fast(q4 q, float out[6]) {
+  const float s = 2.0f * (q.w * q.w) - 1.0f;
+  out[0] = s + (q.x * q.x) * 2.0f;
+  out[1] = (q.z * q.w) * 2.0f + (q.y * q.x) * 2.0f;
+  out[2] = (-q.y * q.w) * 2.0f + (q.z * q.x) * 2.0f;
+  out[3] = (q.y * q.w) * 2.0f + (q.x * q.z) * 2.0f;
+  out[4] = (-q.x * q.w) * 2.0f + (q.y * q.z) * 2.0f;
+  out[5] = s + (q.z * q.z) * 2.0f;
+}
+
+// Heading quaternion h = (0, 0, z, w) with its my_quat_rotate coefficient precomputed.
+struct Heading {
+  float z, w, s;  // s = 2 w^2 - 1
+};
+
+__device__ __forceinline__ Heading make_heading(float z, float w) { return {z, w, 2.0f * (w * w) - 1.0f}; }
+
+// my_quat_rotate(h, v) for h = (0,0,z,w): a + b + c with cross = (-(z vy), z vx, 0), dot = z vz
+__device__ __forceinline__ v3 rot_heading(const Heading &h, v3 v) {
+  return {v.x * h.s + ((-(h.z * v.y)) * h.w) * 2.0f,
+          v.y * h.s + ((h.z * v.x) * h.w) * 2.0f,
+          v.z * h.s + (h.z * (h.z * v.z)) * 2.0f};
+}
+
+// quat_mul(h, b) for h = (0,0,z,w) (8-multiply form with a.x = a.y = 0)
+__device__ __forceinline__ q4 qmul_heading_left(const Heading &h, q4 b) {
+  const float ww = h.z * (b.x + b.y);
+  const float yy = h.w * (b.w + b.z);
+  const float zz = h.w * (b.w - b.z);
+  const float xx = ww + yy + zz;
+  const float qq = 0.5f * (xx + h.z * (b.x - b.y));
+  return {qq - xx + h.w * (b.x + b.w), qq - yy + h.w * (b.y + b.z), qq - zz + h.z * (b.w - b.x),
+          qq - ww + h.z * (b.y - b.z)};
+}
+
+// quat_mul(a, h) for h = (0,0,z,w) (8-multiply form with b.x = b.y = 0)
+__device__ __forceinline__ q4 qmul_heading_right(q4 a, const Heading &h) {
+  const float yy = (a.w - a.y) * (h.w + h.z);
+  const float zz = (a.w + a.y) * (h.w - h.z);
+  const float xx = yy + zz;
+  const float qq = 0.5f * xx;
+  return {qq - xx + (a.x + a.w) * h.w, qq - yy + (a.w - a.x) * h.z, qq - zz + (a.z + a.y) * h.w,
+          qq + (a.z - a.y) * (-h.z)};
+}
+
 // torch_utils.py:50-51
 __device__ __forceinline__ float normalize_angle(float x) { return atan2f(sinf(x), cosf(x)); }
 
@@ -172,8 +224,10 @@ __device__ __forceinline__ float calc_heading(q4 q) {
 // cos(h/2) = sqrt((1+c)/2), sin(h/2) = s / (2 cos(h/2)) for c >= 0 and sin(h/2) =
 // sign(s) sqrt((1-c)/2), cos(h/2) = s / (2 sin(h/2)) for c < 0 (both well conditioned), then
 // quat_unit as the reference.  Agrees with the transcendental path to a few ulps.
-__device__ __forceinline__ void heading_quats(q4 root_rot, q4 *hrot, q4 *hinv) {
-  const v3 d = my_quat_rotate(root_rot, v3{1.0f, 0.0f, 0.0f});
+__device__ __forceinline__ void heading_quats(q4 root_rot, Heading *hrot, Heading *hinv) {
+  float tn[6];
+  tan_norm_fast(root_rot, tn);  // tn[0..2] = my_quat_rotate(root_rot, x-axis)
+  const v3 d = {tn[0], tn[1], tn[2]};
   const float r = sqrtf(d.x * d.x + d.y * d.y);
   float ch = 1.0f, sh = 0.0f;
   if (r > 0.0f) {
@@ -188,8 +242,12 @@ __device__ __forceinline__ void heading_quats(q4 root_rot, q4 *hrot, q4 *hinv) {
     S = copysignf(sqrtf((1.0f - ch) * 0.5f), sh);
     C = sh / (2.0f * S);
   }
-  *hrot = quat_unit(q4{0.0f, 0.0f, S, C});
-  *hinv = quat_unit(q4{0.0f, 0.0f, -S, C});
+  // quat_unit of (0,0,+-S,C): the norm sqrt(S^2 + C^2) is shared and -S/n == -(S/n) exactly
+  float n = sqrtf(S * S + C * C);
+  n = n < 1e-9f ? 1e-9f : n;
+  const float z = S / n, w = C / n;
+  *hrot = make_heading(z, w);
+  *hinv = make_heading(-z, w);
 }
 
 // torch_utils.py:219-228 quat_angle_axis (float64 use at load time): angle in [0, pi].

@@ -164,7 +164,7 @@ __device__ __forceinline__ void env_obs(const EnvView &e, const LibView &l, int6
   const BodyRec ref1 = ref_body(l.frames, frame_blend(t1, m), b, &off);
   const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
   const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
-  q4 hinv, hrot;
+  Heading hinv, hrot;
   heading_quats(root_r, &hrot, &hinv);
   if (write && active) write_obs_body(e.obs + env * kObs, b, s, root_p, hinv, hrot, ref1);
 }
@@ -227,7 +227,12 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
   e_pos = e_pos + dp.y * dp.y;
   e_pos = (e_pos + dp.z * dp.z) / 3.0f;
   float sin_t;
+#ifdef PHC_EXP_NO_REWARD_TRIG  // timing ablation only
+  const float ang = ref0.r.w - s.r.w;
+  sin_t = 0.0f;
+#else
   const float ang = quat_angle_masked(quat_mul(ref0.r, quat_conj(s.r)), &sin_t);
+#endif
   float e_rot = ang * ang;
   const v3 dv = vsub(ref0.v, s.v);
   float e_vel = dv.x * dv.x;
@@ -325,7 +330,14 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
     e.reset[ei] = reset;
     e.term[ei] = terminated;
   }
+#ifdef PHC_EXP_NO_OBS  // timing ablation only: gather the t+dt rows, skip the observation math
+  {
+    const BodyRec r1 = ref_body(l.frames, frame_blend(t1, m), b, &off1);
+    if (valid && active) e.obs[ei * kObs + b] = r1.p.x + r1.r.w + s.v.x;
+  }
+#else
   env_obs(e, l, ei, lane, m, s, t1, off1, valid);
+#endif
 
   if (e.stats) {
     if (lane == 0) {
