@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--minibatch-size", type=int, default=32768)
     ap.add_argument("--min-len", type=int, default=60)
     ap.add_argument("--max-len", type=int, default=300)
+    ap.add_argument("--precision", default="xf32", choices=["xf32", "fp16", "bf16"],
+                    help="policy GEMM arithmetic (TrainConfig.precision)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic-file", default=None)
@@ -142,9 +144,22 @@ class Runner:
         self.policy = Policy(PHCPolicy(env)).to(dev)
         self.tcfg = TrainConfig(device_id=torch.cuda.current_device(), batch_size=args.batch_size,
                                 minibatch_size=args.minibatch_size, checkpoint_interval=10 ** 9,
-                                total_timesteps=10 ** 15)
+                                total_timesteps=10 ** 15, precision=args.precision)
         self.components, self.info, self.util = clean_pufferl.create("bench", self.tcfg, env_cfg, env, self.policy)
         self.obs = env.observations
+
+    def phase_ms(self, steps):
+        """Host wall time of evaluate / train per timed step (clean_pufferl Profile; ppo mode)."""
+        if self.args.mode != "ppo":
+            return None
+        p = self.info.profile
+        return {k: (getattr(p, k).elapsed - self._p0[k]) / steps * 1e3 for k in self._p0}
+
+    def mark(self):
+        if self.args.mode == "ppo":
+            p = self.info.profile
+            self._p0 = {k: getattr(p, k).elapsed for k in ("evaluate", "env", "eval_forward", "train",
+                                                             "train_forward", "learn", "train_misc")}
 
     def step(self):
         a = self.args
@@ -156,7 +171,7 @@ class Runner:
             if exp.full:
                 exp.ptr = 0
             o, r, d, t, _, env_id, mask = self.env.recv()
-            with torch.no_grad():
+            with torch.no_grad(), self.cp.core.autocast(self.tcfg):
                 actions, logprob, _, value = self.policy(o)
             exp.store(o, None, value.flatten(), actions, logprob, r, d, t, env_id, mask, n_valid=a.envs)
             self.env.send(actions)
@@ -183,6 +198,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    runner.mark()
     t0 = time.perf_counter()
     processed = 0
     for _ in range(args.steps):
@@ -213,10 +229,10 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(env, packed, args.cpu_seconds)
         workloads = {
-            "ppo": "clean_pufferl PPO iteration: evaluate %d rows (PHCPolicy fp32 inference + PHCPufferEnv.step) + "
+            "ppo": "clean_pufferl PPO iteration: evaluate %d rows (PHCPolicy %s inference + PHCPufferEnv.step) + "
                    "RMS update + train (GAE, 4 epochs x %d minibatches of %d, Adam)" % (
-                       args.batch_size, args.batch_size // args.minibatch_size, args.minibatch_size),
-            "rollout": "PHCPolicy fp32 inference + PHCPufferEnv.step + on-device experience store",
+                       args.batch_size, args.precision, args.batch_size // args.minibatch_size, args.minibatch_size),
+            "rollout": "PHCPolicy %s inference + PHCPufferEnv.step + on-device experience store" % args.precision,
             "env": "PHCPufferEnv.step: actions->PD + replay physics + fused obs/reward/reset + reset re-init "
                    "(fixed random actions, no policy)",
         }
@@ -231,12 +247,18 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": {"xf32": "fp32", "fp16": "fp16", "bf16": "bf16"}[args.precision] if args.mode != "env"
+            else "fp32",
             "data": "synthetic (device-generated SMPL clips U{%d..%d} frames @30fps; replayed physics; "
                     "random-init policy)" % (args.min_len, args.max_len),
             "config": {"workload": workloads[args.mode], "mode": args.mode, "envs_per_gpu": args.envs,
                        "global_envs": args.envs * world, "motions_per_gpu": args.envs,
-                       "parallelism": f"dp{world} (env shards, RCCL grad all-reduce)"},
+                       "parallelism": f"dp{world} (env shards, RCCL grad all-reduce)",
+                       "policy_gemm": {"xf32": "fp32 storage, hipBLASLt xf32 (torch 'high', as the reference)",
+                                       "fp16": "autocast fp16 MFMA + dynamic loss scaling",
+                                       "bf16": "autocast bf16 MFMA"}[args.precision] if args.mode != "env"
+                       else None,
+                       "phase_ms_per_step": runner.phase_ms(args.steps)},
             "roofline": {"bound": "hbm", "kernel": "phc_env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_us": kern_s * 1e6, "launches_timed": env_steps,

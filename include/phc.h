@@ -129,6 +129,29 @@ int phc_reset_envs(const phc_env_buffers *env, const phc_motion_lib *lib, const 
                    const uint8_t *env_mask, const float *phase, uint64_t seed, uint64_t counter,
                    void *stream);
 
+/* AMP observation history of HumanoidPHC (humanoid_phc.py:600-611): amp_obs[N, S, 196] with
+ * frame 0 = current (_curr_amp_obs_buf) and frames 1..S-1 = history; amp_obs_demo same shape. */
+typedef struct phc_amp_buffers {
+  float *amp_obs;      /* [N, num_steps, PHC_AMP_OBS_STEP] */
+  float *amp_obs_demo; /* [N, num_steps, PHC_AMP_OBS_STEP] */
+  int32_t num_steps;   /* cfg.num_amp_obs_steps (10) */
+} phc_amp_buffers;
+
+enum {
+  PHC_AMP_STEP = 0, /* every env: progress == 0 -> init, else shift history + current frame */
+  PHC_AMP_INIT = 1, /* envs with progress == 0 only: init; other envs untouched */
+};
+
+/* R16: AMP observations (envs/common.py:180-267 build_amp_observations_smpl with local root obs,
+ * root height, dof subset, upright).  PHC_AMP_STEP = _update_hist_amp_obs +
+ * _compute_amp_observations of HumanoidPHC.step (humanoid_phc.py:154-157, 1123-1160, 1339-1348);
+ * init (envs that were just reset, progress == 0) = _init_amp_obs (:789-836): frame 0 from the
+ * sim state, frame k from the motion library at motion_start_time - k*dt (no offset), and
+ * amp_obs_demo[env] = amp_obs[env].  Run after phc_env_step (STEP) and after phc_reset_envs
+ * (INIT).  Reads rigid_body_state, dof_state, progress, motion_ids, motion_start_times. */
+int phc_amp_obs(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_amp_buffers *amp, float dt,
+                int32_t mode, void *stream);
+
 /* R13: clip(a,-1,1), pd = offset + scale*a, frozen dofs = 0
  * (clean_pufferl/env.py:91-93, humanoid_phc.py:106-128, 1216-1226). */
 int phc_actions_to_pd(const float *actions, float *pd_target, int64_t n, const float *offset,

@@ -568,6 +568,48 @@ def amp_obs(root_pos, root_rot, root_vel, root_ang_vel, dof_pos, dof_vel, key_bo
     return np.concatenate([root_pos[:, 2:3], root_rot_obs, lv, lav, dof_obs, dof_vel[:, sub], kb], -1)
 
 
+KEY_BODY_IDS = np.array([BODY_NAMES.index(n) for n in KEY_BODIES])
+
+
+def amp_obs_from_sim(rb_state, dof_pos, dof_vel):
+    """_compute_amp_observations (humanoid_phc.py:1123-1160) from the sim buffers."""
+    rb = f32(rb_state)
+    return amp_obs(rb[:, 0, 0:3], rb[:, 0, 3:7], rb[:, 0, 7:10], rb[:, 0, 10:13], f32(dof_pos), f32(dof_vel),
+                   rb[:, KEY_BODY_IDS, 0:3])
+
+
+def amp_obs_from_motion(lib, motion_ids, motion_times):
+    """_get_amp_obs (humanoid_phc.py:819-836): reference state without offset."""
+    ms = motion_state(lib, motion_ids, motion_times)
+    return amp_obs(ms["root_pos"], ms["root_rot"], ms["root_vel"], ms["root_ang_vel"], ms["dof_pos"],
+                   ms["dof_vel"], ms["rg_pos"][:, KEY_BODY_IDS])
+
+
+def amp_update(amp, demo, lib, rb_state, dof_pos, dof_vel, progress, motion_ids, start, dt, init_only):
+    """AMP history update in place on amp / demo [N, S, 196].
+
+    init_only=False: HumanoidPHC.step's _update_hist_amp_obs + _compute_amp_observations
+    (humanoid_phc.py:154-157, 1339-1348) for every env, followed by the reset of the envs that
+    were just re-initialised (progress == 0) — whose _init_amp_obs (:789-836) overwrites all
+    frames: frame 0 from the sim state, frame k from the motion library at start - k*dt, and
+    copies the window into amp_obs_demo.  init_only=True: only the reset part (reset(env_ids))."""
+    n, steps = amp.shape[0], amp.shape[1]
+    init = np.asarray(progress) == 0
+    if not init_only:
+        amp[:, 1:] = amp[:, :-1].copy()
+        amp[:, 0] = amp_obs_from_sim(rb_state, dof_pos, dof_vel)
+    ids = np.nonzero(init)[0]
+    if len(ids):
+        amp[ids, 0] = amp_obs_from_sim(rb_state[ids], dof_pos[ids], dof_vel[ids])
+        ks = np.arange(1, steps)
+        times = f32(start)[ids][:, None] + (-F32(dt)) * ks.astype(np.float32)[None, :]
+        mids = np.repeat(np.asarray(motion_ids)[ids], steps - 1)
+        hist = amp_obs_from_motion(lib, mids, times.reshape(-1))
+        amp[ids, 1:] = hist.reshape(len(ids), steps - 1, -1)
+        demo[ids] = amp[ids]
+    return amp, demo
+
+
 # --------------------------------------------------------------- R17 RMS ----
 def rms_update(mean, var, count, x):
     """RunningNorm.update, puffer_phc/policies/running_norm.py:22-34 (float64 batch stats)."""

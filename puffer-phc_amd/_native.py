@@ -20,6 +20,8 @@ NUM_BODIES = 24
 NUM_DOF = 69
 BODY_STRIDE = 13
 OBS_DIM = 934
+AMP_OBS_STEP = 196
+AMP_STEP, AMP_INIT = 0, 1
 STATS_SLOTS = 16
 
 c_i64 = ctypes.c_int64
@@ -55,6 +57,10 @@ class StepParamsC(ctypes.Structure):
                 ("auto_reset", ctypes.c_int32), ("seed", ctypes.c_uint64)]
 
 
+class AmpBuffersC(ctypes.Structure):
+    _fields_ = [("amp_obs", c_vp), ("amp_obs_demo", c_vp), ("num_steps", ctypes.c_int32)]
+
+
 _EXPORTS = {
     "phc_version": (ctypes.c_int, []),
     "phc_last_error": (ctypes.c_char_p, []),
@@ -66,6 +72,8 @@ _EXPORTS = {
     "phc_reset_envs": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                        ctypes.POINTER(StepParamsC), c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint64,
                                        c_vp]),
+    "phc_amp_obs": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
+                                    ctypes.POINTER(AmpBuffersC), ctypes.c_float, ctypes.c_int32, c_vp]),
     "phc_actions_to_pd": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "phc_physics_replay": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                            ctypes.POINTER(StepParamsC), ctypes.c_float, ctypes.c_float,
@@ -243,6 +251,22 @@ def reset_envs(env_c, mlib, params, mask=None, phase=None, seed=0, counter=0, nu
                                 _ptr(phase, torch.float32, (n,), "phase", nullable=True),
                                 ctypes.c_uint64(seed), ctypes.c_uint64(counter), _stream()),
            "phc_reset_envs")
+
+
+def amp_struct(amp_obs, amp_obs_demo):
+    """phc_amp_buffers over [N, S, 196] float32 tensors (demo nullable)."""
+    if amp_obs is None or amp_obs.dim() != 3 or amp_obs.shape[2] != AMP_OBS_STEP:
+        raise ValueError("amp_obs: expected a [N, num_steps, 196] tensor")
+    shape = tuple(amp_obs.shape)
+    return AmpBuffersC(_ptr(amp_obs, torch.float32, shape, "amp_obs"),
+                       _ptr(amp_obs_demo, torch.float32, shape, "amp_obs_demo", nullable=True), shape[1])
+
+
+def amp_obs(env_c, mlib, amp_c, dt, mode=AMP_STEP):
+    """R16: AMP history step (mode AMP_STEP) or re-initialisation of just-reset envs (AMP_INIT)."""
+    _check(lib().phc_amp_obs(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(amp_c), float(dt), int(mode),
+                             _stream()),
+           "phc_amp_obs")
 
 
 def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):

@@ -12,6 +12,7 @@ Differences from the reference that do not change the math:
     advantage normalisation uses global statistics (see distributed.py).
 """
 
+import contextlib
 from collections import defaultdict
 
 import numpy as np
@@ -50,6 +51,17 @@ def _l2_init_reg(named_params, initial_params, need_grad):
 
 _NUMEL_CACHE = {}
 
+_AUTOCAST = {"fp16": torch.float16, "bf16": torch.bfloat16}
+
+
+def autocast(cfg):
+    """Policy-GEMM precision context for TrainConfig.precision (see config.py)."""
+    if cfg.precision == "xf32":
+        return contextlib.nullcontext()
+    if cfg.precision not in _AUTOCAST:
+        raise ValueError(f"unknown precision {cfg.precision!r} (xf32 | fp16 | bf16)")
+    return torch.autocast("cuda", dtype=_AUTOCAST[cfg.precision])
+
 
 def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=None):
     seed_everything(train_cfg.seed + D.rank(), train_cfg.torch_deterministic)
@@ -72,6 +84,10 @@ def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=Non
     initial_params = {name: p.detach().clone() for name, p in policy.named_parameters()}
     components = TrainComponents(vecenv=vecenv, policy=policy, uncompiled_policy=uncompiled_policy,
                                  experience=experience, optimizer=optimizer)
+    autocast(train_cfg)  # validates the precision name
+    if train_cfg.precision == "fp16":
+        # fp16 keeps TF32's mantissa but not its exponent range: dynamic loss scaling for the grads
+        components.scaler = torch.amp.GradScaler("cuda")
     components.flat_grads = D.FlatGrads(uncompiled_policy.parameters())
     components.gae = _native.GAE()
     info = TrainInfo(config=train_cfg, exp_id=exp_id, env_name=env_cfg.name, stats=StatsData(), msg=msg,
@@ -92,7 +108,7 @@ def evaluate(components, info):
             with profile.eval_misc:
                 n_valid = int(mask.sum().item())
                 info.global_step += n_valid
-            with profile.eval_forward, torch.no_grad():
+            with profile.eval_forward, torch.no_grad(), autocast(train_cfg):
                 actions, logprob, _, value = policy(o)
             with profile.eval_misc:
                 amp_obs = components.vecenv.amp_obs if info.use_amp_obs else None
@@ -121,7 +137,7 @@ def compute_advantages(components, info):
     discriminate = getattr(components.policy.policy, "discriminate", None) if hasattr(components.policy, "policy") \
         else None
     if info.use_amp_obs and discriminate is not None:
-        with torch.no_grad():
+        with torch.no_grad(), autocast(cfg):
             for mb in range(experience.num_minibatches):
                 logits = discriminate(experience.b_amp_obs[mb]).squeeze()
                 prob = 1 / (1 + torch.exp(-logits))
@@ -162,7 +178,7 @@ def train(components, info, utilization=None):
                     val = experience.b_values[mb]
                     adv = experience.b_advantages[mb]
                     ret = experience.b_returns[mb]
-                with profile.train_forward:
+                with profile.train_forward, autocast(cfg):
                     _, newlogprob, entropy, newvalue = components.policy(obs, action=atn)
                 with profile.train_misc:
                     logratio = newlogprob - log_probs
@@ -191,8 +207,9 @@ def train(components, info, utilization=None):
                     if info.use_amp_obs:
                         amp_agent = torch.cat([experience.b_amp_obs[mb][:amp_mb],
                                                experience.b_amp_obs_replay[mb][:amp_mb]])
-                        d_agent = pol.discriminate(amp_agent)
-                        d_demo = pol.discriminate(amp_obs_demo)
+                        with autocast(cfg):
+                            d_agent = pol.discriminate(amp_agent).float()
+                            d_demo = pol.discriminate(amp_obs_demo).float()
                         bce = torch.nn.BCEWithLogitsLoss()
                         disc_loss = 0.5 * (bce(d_agent, torch.zeros_like(d_agent)) + bce(d_demo, torch.ones_like(d_demo)))
                         if cfg.disc_coef > 0:
@@ -206,11 +223,21 @@ def train(components, info, utilization=None):
                         loss = loss + l2 * cfg.l2_reg_coef
                 with profile.learn:
                     flat.zero()
-                    loss.backward()
-                    flat.allreduce_mean()
-                    gnorm = flat.norms_sum()
-                    torch.nn.utils.clip_grad_norm_(flat.params, cfg.max_grad_norm)
-                    components.optimizer.step()
+                    scaler = components.scaler
+                    if scaler is None:
+                        loss.backward()
+                        flat.allreduce_mean()
+                        gnorm = flat.norms_sum()
+                        torch.nn.utils.clip_grad_norm_(flat.params, cfg.max_grad_norm)
+                        components.optimizer.step()
+                    else:
+                        scaler.scale(loss).backward()
+                        flat.allreduce_mean()
+                        scaler.unscale_(components.optimizer)
+                        gnorm = flat.norms_sum()
+                        torch.nn.utils.clip_grad_norm_(flat.params, cfg.max_grad_norm)
+                        scaler.step(components.optimizer)  # skipped when a grad is inf/nan
+                        scaler.update()
                 with profile.train_misc, torch.no_grad():
                     acc += torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,
                                         approx_kl, clipfrac, gnorm, l2.detach(), disc_loss.detach(),

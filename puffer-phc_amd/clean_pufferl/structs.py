@@ -258,6 +258,7 @@ class TrainComponents:
     uncompiled_policy: Any
     experience: Experience
     optimizer: torch.optim.Optimizer
+    scaler: Any = None
 
 
 @dataclass

@@ -173,3 +173,8 @@ class TrainConfig(DeviceConfig):
     disc_coef: float = 5.0
     bound_coef: float = 10.0
     l2_reg_coef: float = 0.0
+    # policy GEMM arithmetic: "xf32" = float32 storage with hipBLASLt's xf32 emulation (what
+    # torch "high" precision gives on gfx950, at least TF32-accurate as the reference);
+    # "fp16" = autocast fp16 MFMA (TF32's 10-bit mantissa) with dynamic loss scaling;
+    # "bf16" = autocast bf16 MFMA (BASELINE config C5).
+    precision: str = "xf32"

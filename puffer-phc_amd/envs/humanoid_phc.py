@@ -162,6 +162,15 @@ class HumanoidPHC:
         self._sampled_motion_ids = torch.arange(N, device=dev)
         self._reset_mask = torch.zeros(N, dtype=torch.bool, device=dev)
         self._rng_counter_buf = torch.zeros(N, dtype=torch.int32, device=dev)
+        # AMP history (humanoid_phc.py:600-611): frame 0 = current, 1.. = history
+        self._amp_c = None
+        if self.cfg.use_amp_obs:
+            assert self._num_amp_obs_per_step == _native.AMP_OBS_STEP
+            self._amp_obs_buf = torch.zeros((N, self.cfg.num_amp_obs_steps, self._num_amp_obs_per_step), device=dev)
+            self._curr_amp_obs_buf = self._amp_obs_buf[:, 0]
+            self._hist_amp_obs_buf = self._amp_obs_buf[:, 1:]
+            self._amp_obs_demo_buf = torch.zeros_like(self._amp_obs_buf)
+            self._amp_c = _native.amp_struct(self._amp_obs_buf, self._amp_obs_demo_buf)
         self._puffer = {}
         self._env_c = None
         self._build_structs()
@@ -232,13 +241,20 @@ class HumanoidPHC:
             self._reset_mask[env_ids] = True
             _native.reset_envs(self._env_c, self._motion_lib.packed.c, self._step_params, mask=self._reset_mask,
                                seed=self._rng_seed, counter=self._next_counter())
+        self._init_amp_obs()
         return self.obs_buf
+
+    def _init_amp_obs(self):
+        """_init_amp_obs (humanoid_phc.py:789-836) of every env that was just reset (progress 0)."""
+        if self._amp_c is not None:
+            _native.amp_obs(self._env_c, self._motion_lib.packed.c, self._amp_c, self.dt, _native.AMP_INIT)
 
     def reset_done(self):
         """Reset every env whose reset_buf is set (PHCPufferEnv's nonzero(reset_buf) + reset,
         clean_pufferl/env.py:114-116, without leaving the device)."""
         _native.reset_envs(self._env_c, self._motion_lib.packed.c, self._step_params, mask=None,
                            seed=self._rng_seed, counter=self._next_counter())
+        self._init_amp_obs()
 
     def step(self, actions, auto_reset=False):
         """humanoid_phc.py:105-172 with the physics stand-in.  With auto_reset (used by
@@ -262,6 +278,11 @@ class HumanoidPHC:
         else:
             self.extras["terminate"] = self._terminate_buf.clone()
         self.extras["reward_raw"] = self.reward_raw
+        if self._amp_c is not None:
+            # _update_hist_amp_obs + _compute_amp_observations (humanoid_phc.py:154-157); envs that
+            # auto-reset in this step (progress 0) get _init_amp_obs instead, as reset() would
+            _native.amp_obs(self._env_c, self._motion_lib.packed.c, self._amp_c, self.dt, _native.AMP_STEP)
+            self.extras["amp_obs"] = self.amp_obs
         if self.flag_im_eval:
             t = self.progress_buf * self.dt + self._motion_start_times + self._motion_start_times_offset
             res = self._motion_lib.get_motion_state(self._sampled_motion_ids, t, self._global_offset)
@@ -356,7 +377,7 @@ class HumanoidPHC:
 
     @property
     def amp_obs(self):
-        return None
+        return self._amp_obs_buf.view(-1, self.num_amp_obs) if self._amp_c is not None else None
 
     def fetch_amp_obs_demo(self):
-        return None
+        return self._amp_obs_demo_buf.view(-1, self.num_amp_obs) if self._amp_c is not None else None

@@ -34,12 +34,12 @@ class PHCPolicy(DiscriminatorPolicy):
         return self.actor_mlp(self.obs_pointer), None
 
     def decode_actions(self, hidden, lookup=None):
-        mu = self.mu(hidden)
+        mu = self.mu(hidden).float()  # fp32 head under autocast
         std = torch.exp(self.sigma).expand_as(mu)
         if self._deterministic_action is True:
             std = torch.clamp(std, max=1e-6)
         probs = torch.distributions.Normal(mu, std, validate_args=False)  # no host-syncing checks
         if self.training:
             self.mean_bound_loss = self.bound_loss(mu)
-        value = self.critic_mlp(self.obs_pointer)
+        value = self.critic_mlp(self.obs_pointer).float()
         return probs, value

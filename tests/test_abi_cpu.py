@@ -57,7 +57,8 @@ def test_struct_offsets_match_c_compiler(tmp_path):
     import subprocess
 
     structs = {"phc_env_buffers": _native.EnvBuffersC, "phc_motion_lib": _native.MotionLibC,
-               "phc_step_params": _native.StepParamsC, "phc_ref_state": _native.RefStateC}
+               "phc_step_params": _native.StepParamsC, "phc_ref_state": _native.RefStateC,
+               "phc_amp_buffers": _native.AmpBuffersC}
     lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "phc.h"', "int main(void){"]
     for s, cls in structs.items():
         lines.append(f'printf("{s} size %zu\\n", sizeof({s}));')
@@ -74,3 +75,25 @@ def test_struct_offsets_match_c_compiler(tmp_path):
         assert got[(s, "size")] == ctypes.sizeof(cls), s
         for f, _ in cls._fields_:
             assert got[(s, f)] == getattr(cls, f).offset, (s, f)
+
+
+def test_amp_constant_tables_match_body_sets():
+    """phc_amp.hip's per-body tables (dof-subset rank, key-body slot) agree with body_sets
+    (puffer_phc/body_sets.py:39-45) — checked on the HIP source, no GPU needed."""
+    from puffer_phc_amd.body_sets import BODY_NAMES, DOF_NAMES, KEY_BODIES
+
+    src = open(os.path.join(ROOT, "puffer-phc_amd", "csrc", "phc_amp.hip")).read()
+
+    def table(name):
+        m = re.search(name + r"\[kBodies\] = \{([^}]*)\}", src)
+        return [int(x) for x in m.group(1).split(",")]
+
+    slots = table("kKeySlot")
+    assert [slots.index(k) for k in range(len(KEY_BODIES))] == [BODY_NAMES.index(b) for b in KEY_BODIES]
+    assert sum(s >= 0 for s in slots) == len(KEY_BODIES)
+    removed = ("L_Hand", "R_Hand", "L_Toe", "R_Toe")
+    expect, r = [-1], 0
+    for n in DOF_NAMES:
+        expect.append(-1 if n in removed else r)
+        r += n not in removed
+    assert table("kDofRank") == expect

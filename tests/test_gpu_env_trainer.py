@@ -142,3 +142,29 @@ def test_ppo_iteration_trains(small_env):
     changed = sum(not torch.equal(before[k], v) for k, v in policy.named_parameters() if v.requires_grad)
     assert changed > 0
     assert float(policy.policy.obs_norm.count) == 2.0
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_ppo_iteration_reduced_precision(small_env, precision):
+    """TrainConfig.precision fp16 (dynamic loss scaling) / bf16 (autocast): one full PPO
+    iteration stays finite, updates the weights and keeps fp32 master parameters."""
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.config import TrainConfig
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+
+    env, _, _ = small_env
+    torch.manual_seed(0)
+    policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+    cfg = TrainConfig(batch_size=64 * 16, minibatch_size=256, bptt_horizon=8, checkpoint_interval=10 ** 9,
+                      precision=precision)
+    comps, info, util = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+    assert (comps.scaler is not None) == (precision == "fp16")
+    before = {k: v.detach().clone() for k, v in policy.named_parameters()}
+    clean_pufferl.evaluate(comps, info)
+    assert comps.experience.values.dtype == torch.float32
+    policy.policy.update_obs_rms(comps.experience.obs)
+    losses = clean_pufferl.train(comps, info, util)
+    assert np.isfinite([losses.policy_loss, losses.value_loss, losses.approx_kl]).all()
+    assert all(v.dtype == torch.float32 for v in policy.parameters())
+    changed = sum(not torch.equal(before[k], v) for k, v in policy.named_parameters() if v.requires_grad)
+    assert changed > 0
