@@ -185,6 +185,10 @@ class Runner:
 
 def main():
     args = parse()
+    if os.environ.get("PHC_WATCHDOG_S"):  # debugging aid: dump every thread's stack periodically
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["PHC_WATCHDOG_S"]), repeat=True)
     world, rank = setup_dist()
     device = f"cuda:{torch.cuda.current_device()}"
     torch.manual_seed(1234 + rank)

@@ -188,6 +188,27 @@ int phc_rms_update(const float *x, int64_t rows, int64_t cols, float *mean, floa
 int phc_rms_normalize(const float *x, float *y, int64_t rows, int64_t cols, const float *mean,
                       const float *var, float eps, float clip, void *stream);
 
+/* R19/R21: fused epilogues of the twin actor/critic SiLU trunks (policies/phc_policy.py:10-61:
+ * nn.Linear bias + nn.SiLU forward, their backward and the bias gradient).  A twin tensor holds
+ * `groups` trunks of `cols` columns for `rows` rows, laid out SPLIT [rows, groups*cols] or
+ * GROUPED [groups, rows, cols]; elements are dtype (f32 | f16 | bf16), arithmetic fp32, bias
+ * and bias_grad fp32 [groups*cols].  cols % 4 == 0. */
+enum { PHC_DT_F32 = 0, PHC_DT_F16 = 1, PHC_DT_BF16 = 2 };
+enum { PHC_LAYOUT_SPLIT = 0, PHC_LAYOUT_GROUPED = 1 };
+enum { PHC_ACT_NONE = 0, PHC_ACT_SILU = 1 };
+
+/* pre = y + bias (same layout as y; may be y itself, nullable), out = act(pre) in out_layout
+ * (nullable). */
+int phc_bias_act_fwd(const void *y, int32_t y_layout, const float *bias, void *pre, void *out, int32_t out_layout,
+                     int64_t rows, int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *stream);
+
+/* grad_pre = grad_out * act'(pre) (nullable; may be grad_out itself when the layouts agree) and
+ * bias_grad = column sums of grad_pre in fp32 (nullable; needs phc_act_bwd_workspace_bytes). */
+size_t phc_act_bwd_workspace_bytes(int64_t rows, int32_t groups, int32_t cols);
+int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, int32_t pre_layout, void *grad_pre,
+                int32_t grad_pre_layout, float *bias_grad, int64_t rows, int32_t groups, int32_t cols, int32_t act,
+                int32_t dtype, void *workspace, void *stream);
+
 /* Library version and last error (thread-local). */
 int phc_version(void);
 const char *phc_last_error(void);

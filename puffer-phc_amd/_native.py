@@ -75,6 +75,11 @@ _EXPORTS = {
     "phc_amp_obs": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                     ctypes.POINTER(AmpBuffersC), ctypes.c_float, ctypes.c_int32, c_vp]),
     "phc_actions_to_pd": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "phc_bias_act_fwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, c_vp, c_vp, ctypes.c_int32, c_i64, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp]),
+    "phc_act_bwd_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
+    "phc_act_bwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, ctypes.c_int32, c_vp, ctypes.c_int32, c_vp, c_i64,
+                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp, c_vp]),
     "phc_physics_replay": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                            ctypes.POINTER(StepParamsC), ctypes.c_float, ctypes.c_float,
                                            ctypes.c_uint64, ctypes.c_uint64, c_vp]),
@@ -267,6 +272,58 @@ def amp_obs(env_c, mlib, amp_c, dt, mode=AMP_STEP):
     _check(lib().phc_amp_obs(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(amp_c), float(dt), int(mode),
                              _stream()),
            "phc_amp_obs")
+
+
+# ------------------------------------------------------- twin MLP epilogues --
+DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+SPLIT, GROUPED = 0, 1
+ACT_NONE, ACT_SILU = 0, 1
+
+
+def _twin(t, dtype, layout, rows, groups, cols, name, nullable=False):
+    shape = (rows, groups * cols) if layout == SPLIT else (groups, rows, cols)
+    return _ptr(t, dtype, shape, name, nullable=nullable)
+
+
+def bias_act_fwd(y, y_layout, bias, pre, out, out_layout, rows, groups, cols, act):
+    """pre = y + bias, out = act(pre) over a twin tensor (phc_bias_act_fwd)."""
+    dt = y.dtype
+    if dt not in DTYPE_CODE:
+        raise ValueError(f"bias_act_fwd: unsupported dtype {dt}")
+    _check(lib().phc_bias_act_fwd(_twin(y, dt, y_layout, rows, groups, cols, "y"), y_layout,
+                                  _ptr(bias, torch.float32, (groups * cols,), "bias", nullable=True),
+                                  _twin(pre, dt, y_layout, rows, groups, cols, "pre", nullable=True),
+                                  _twin(out, dt, out_layout, rows, groups, cols, "out", nullable=True), out_layout,
+                                  rows, groups, cols, act, DTYPE_CODE[dt], _stream()),
+           "phc_bias_act_fwd")
+
+
+_WS = {}
+
+
+def _workspace(nbytes, device):
+    key = (device.index if device.index is not None else torch.cuda.current_device(), torch.cuda.current_stream())
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def act_bwd(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, bias_grad, rows, groups, cols, act):
+    """grad_pre = grad_out * act'(pre), bias_grad = column sums (phc_act_bwd)."""
+    dt = grad_out.dtype
+    if dt not in DTYPE_CODE:
+        raise ValueError(f"act_bwd: unsupported dtype {dt}")
+    ws = None
+    if bias_grad is not None:
+        ws = _workspace(lib().phc_act_bwd_workspace_bytes(rows, groups, cols), grad_out.device).data_ptr()
+    _check(lib().phc_act_bwd(_twin(grad_out, dt, go_layout, rows, groups, cols, "grad_out"), go_layout,
+                             _twin(pre, dt, pre_layout, rows, groups, cols, "pre", nullable=act == ACT_NONE),
+                             pre_layout, _twin(grad_pre, dt, gp_layout, rows, groups, cols, "grad_pre", nullable=True),
+                             gp_layout, _ptr(bias_grad, torch.float32, (groups * cols,), "bias_grad", nullable=True),
+                             rows, groups, cols, act, DTYPE_CODE[dt], ws, _stream()),
+           "phc_act_bwd")
 
 
 def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):

@@ -1,0 +1,242 @@
+// phc_mlp.hip — fused epilogues of the PHCPolicy actor/critic trunks (R19/R21).
+//
+// The two 6-layer SiLU trunks (policies/phc_policy.py:10-61) run side by side as "twin"
+// layers: the GEMMs are plain library GEMMs (one [M,934]x[934,2x2048] GEMM for the shared
+// input, then batched GEMMs over the 2 trunks), and everything between GEMMs is one of the two
+// kernels below, so each activation tensor makes one HBM round trip per direction:
+//   forward : pre = y + bias (kept for backward), out = silu(pre)
+//   backward: g = dout * silu'(pre), bias_grad = sum over rows of g (per-block partial column
+//             sums in fp32, then one reduce; deterministic, no atomics)
+// A twin tensor holds G groups (trunks) of N columns for M rows, either SPLIT [M, G*N] (the
+// output of the shared first GEMM) or GROUPED [G, M, N] (batched-GEMM operands); the kernels
+// convert between the two on the fly.  Element types: f32 (xf32 GEMMs), f16, bf16 (GEMMs in
+// reduced precision); arithmetic is fp32.
+#include "phc_common.h"
+
+namespace phc {
+
+constexpr int kColsPerBlock = 256;  // 64 lanes x 4 consecutive columns
+constexpr int kRowsPerBlock = 64;   // 4 waves x 16 rows
+
+template <typename T> struct Pack4 {
+  T v[4];
+};
+
+template <typename T> __device__ __forceinline__ void ld4(const T *p, float o[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 v = *reinterpret_cast<const float4 *>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  } else {
+    const uint2 raw = *reinterpret_cast<const uint2 *>(p);
+    Pack4<T> v;
+    __builtin_memcpy(&v, &raw, sizeof(raw));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (float)v.v[k];
+  }
+}
+
+template <typename T> __device__ __forceinline__ void st4(T *p, const float o[4]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4 *>(p) = float4{o[0], o[1], o[2], o[3]};
+  } else {
+    Pack4<T> v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v.v[k] = (T)o[k];
+    uint2 raw;
+    __builtin_memcpy(&raw, &v, sizeof(raw));
+    *reinterpret_cast<uint2 *>(p) = raw;
+  }
+}
+
+struct TwinShape {
+  int64_t m;
+  int g, n;
+};
+
+// offset of logical element (row, column c = group * n + j) in a twin tensor
+__device__ __forceinline__ int64_t twin_off(const TwinShape &s, int layout, int64_t row, int c) {
+  if (layout == PHC_LAYOUT_SPLIT) return row * (int64_t)(s.g * s.n) + c;
+  const int grp = c / s.n;
+  return ((int64_t)grp * s.m + row) * s.n + (c - grp * s.n);
+}
+
+__device__ __forceinline__ float silu(float a) { return a / (1.0f + expf(-a)); }
+__device__ __forceinline__ float silu_grad(float dz, float a) {
+  const float sg = 1.0f / (1.0f + expf(-a));
+  return dz * sg * (1.0f + a * (1.0f - sg));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_bias_act_fwd(const T *y, int y_layout, const float *__restrict__ bias, T *pre,
+                                                      T *out, int out_layout, TwinShape s, int act) {
+  const int c = blockIdx.x * kColsPerBlock + (threadIdx.x & 63) * 4;
+  if (c >= s.g * s.n) return;
+  float b[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (bias) {
+    const float4 bv = *reinterpret_cast<const float4 *>(bias + c);
+    b[0] = bv.x; b[1] = bv.y; b[2] = bv.z; b[3] = bv.w;
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * kRowsPerBlock + (threadIdx.x >> 6);
+  for (int i = 0; i < kRowsPerBlock / 4; ++i) {
+    const int64_t row = r0 + 4 * i;
+    if (row >= s.m) break;
+    float v[4];
+    const int64_t oy = twin_off(s, y_layout, row, c);
+    ld4(y + oy, v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = v[k] + b[k];
+    if (pre) st4(pre + oy, v);
+    if (act == PHC_ACT_SILU) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = silu(v[k]);
+    }
+    if (out) st4(out + twin_off(s, out_layout, row, c), v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_act_bwd(const T *dz, int dz_layout, const T *pre, int pre_layout,
+                                                 T *g, int g_layout, float *__restrict__ partial, TwinShape s,
+                                                 int act) {
+  __shared__ float red[4][kColsPerBlock];
+  const int lane4 = (threadIdx.x & 63) * 4;
+  const int w = threadIdx.x >> 6;
+  const int c = blockIdx.x * kColsPerBlock + lane4;
+  const bool col_ok = c < s.g * s.n;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (col_ok) {
+    const int64_t r0 = (int64_t)blockIdx.y * kRowsPerBlock + w;
+    for (int i = 0; i < kRowsPerBlock / 4; ++i) {
+      const int64_t row = r0 + 4 * i;
+      if (row >= s.m) break;
+      float d[4];
+      ld4(dz + twin_off(s, dz_layout, row, c), d);
+      if (act == PHC_ACT_SILU) {
+        float a[4];
+        ld4(pre + twin_off(s, pre_layout, row, c), a);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = silu_grad(d[k], a[k]);
+      }
+      if (g) st4(g + twin_off(s, g_layout, row, c), d);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += d[k];
+    }
+  }
+  if (!partial) return;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[w][lane4 + k] = acc[k];
+  __syncthreads();
+  if (w == 0 && col_ok) {
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = ((red[0][lane4 + k] + red[1][lane4 + k]) + red[2][lane4 + k]) + red[3][lane4 + k];
+    *reinterpret_cast<float4 *>(partial + (int64_t)blockIdx.y * (s.g * s.n) + c) = float4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+__global__ __launch_bounds__(256) void k_colsum(const float *__restrict__ partial, int rows, int cols,
+                                                float *__restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float acc = 0.0f;
+  for (int r = 0; r < rows; ++r) acc += partial[(int64_t)r * cols + c];
+  out[c] = acc;
+}
+
+static int check_twin(const void *p, int layout, int dtype, const char *what) {
+  PHC_REQUIRE(p, "%s: null tensor", what);
+  PHC_REQUIRE(layout == PHC_LAYOUT_SPLIT || layout == PHC_LAYOUT_GROUPED, "%s: bad layout", what);
+  const uintptr_t align = dtype == PHC_DT_F32 ? 16 : 8;
+  PHC_REQUIRE((reinterpret_cast<uintptr_t>(p) & (align - 1)) == 0, "%s: misaligned", what);
+  return PHC_OK;
+}
+
+static dim3 twin_grid(const TwinShape &s) {
+  return dim3((unsigned)((s.g * s.n + kColsPerBlock - 1) / kColsPerBlock),
+              (unsigned)((s.m + kRowsPerBlock - 1) / kRowsPerBlock));
+}
+
+template <typename T>
+static void launch_fwd(const void *y, int yl, const float *bias, void *pre, void *out, int ol, TwinShape s, int act,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_bias_act_fwd<T>, twin_grid(s), dim3(256), 0, st, (const T *)y, yl, bias, (T *)pre, (T *)out,
+                     ol, s, act);
+}
+
+template <typename T>
+static void launch_bwd(const void *dz, int dl, const void *pre, int pl, void *g, int gl, float *partial, TwinShape s,
+                       int act, hipStream_t st) {
+  hipLaunchKernelGGL(k_act_bwd<T>, twin_grid(s), dim3(256), 0, st, (const T *)dz, dl, (const T *)pre, pl, (T *)g, gl,
+                     partial, s, act);
+}
+
+}  // namespace phc
+
+using namespace phc;
+
+extern "C" int phc_bias_act_fwd(const void *y, int32_t y_layout, const float *bias, void *pre, void *out,
+                                int32_t out_layout, int64_t rows, int32_t groups, int32_t cols, int32_t act,
+                                int32_t dtype, void *stream) {
+  PHC_REQUIRE(rows >= 0 && groups >= 1 && cols > 0 && cols % 4 == 0, "bias_act_fwd: bad shape");
+  PHC_REQUIRE(act == PHC_ACT_NONE || act == PHC_ACT_SILU, "bias_act_fwd: bad act");
+  PHC_REQUIRE(dtype == PHC_DT_F32 || dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "bias_act_fwd: bad dtype");
+  if (rows == 0) return PHC_OK;
+  if (int rc = check_twin(y, y_layout, dtype, "bias_act_fwd y")) return rc;
+  PHC_REQUIRE(pre || out, "bias_act_fwd: nothing to write");
+  if (out)
+    if (int rc = check_twin(out, out_layout, dtype, "bias_act_fwd out")) return rc;
+  if (pre)
+    if (int rc = check_twin(pre, y_layout, dtype, "bias_act_fwd pre")) return rc;
+  PHC_REQUIRE(!bias || (reinterpret_cast<uintptr_t>(bias) & 15) == 0, "bias_act_fwd: misaligned bias");
+  PHC_REQUIRE(!(out && out == y && out_layout != y_layout), "bias_act_fwd: in-place output needs the input layout");
+  const TwinShape s{rows, groups, cols};
+  hipStream_t st = as_stream(stream);
+  if (dtype == PHC_DT_F32) launch_fwd<float>(y, y_layout, bias, pre, out, out_layout, s, act, st);
+  else if (dtype == PHC_DT_F16) launch_fwd<_Float16>(y, y_layout, bias, pre, out, out_layout, s, act, st);
+  else launch_fwd<__bf16>(y, y_layout, bias, pre, out, out_layout, s, act, st);
+  return check_launch("bias_act_fwd");
+}
+
+extern "C" size_t phc_act_bwd_workspace_bytes(int64_t rows, int32_t groups, int32_t cols) {
+  if (rows <= 0 || groups <= 0 || cols <= 0) return 0;
+  return (size_t)((rows + kRowsPerBlock - 1) / kRowsPerBlock) * (size_t)groups * (size_t)cols * sizeof(float);
+}
+
+extern "C" int phc_act_bwd(const void *grad_out, int32_t go_layout, const void *pre, int32_t pre_layout,
+                           void *grad_pre, int32_t gp_layout, float *bias_grad, int64_t rows, int32_t groups,
+                           int32_t cols, int32_t act, int32_t dtype, void *workspace, void *stream) {
+  PHC_REQUIRE(rows >= 0 && groups >= 1 && cols > 0 && cols % 4 == 0, "act_bwd: bad shape");
+  PHC_REQUIRE(act == PHC_ACT_NONE || act == PHC_ACT_SILU, "act_bwd: bad act");
+  PHC_REQUIRE(dtype == PHC_DT_F32 || dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "act_bwd: bad dtype");
+  const TwinShape s{rows, groups, cols};
+  hipStream_t st = as_stream(stream);
+  if (rows == 0) {
+    if (bias_grad) (void)hipMemsetAsync(bias_grad, 0, sizeof(float) * groups * cols, st);
+    return check_launch("act_bwd");
+  }
+  if (int rc = check_twin(grad_out, go_layout, dtype, "act_bwd grad_out")) return rc;
+  if (act == PHC_ACT_SILU)
+    if (int rc = check_twin(pre, pre_layout, dtype, "act_bwd pre")) return rc;
+  if (grad_pre)
+    if (int rc = check_twin(grad_pre, gp_layout, dtype, "act_bwd grad_pre")) return rc;
+  PHC_REQUIRE(!(grad_pre && grad_pre == grad_out && gp_layout != go_layout),
+              "act_bwd: in-place grad needs the grad_out layout");
+  PHC_REQUIRE(grad_pre || bias_grad, "act_bwd: nothing to write");
+  float *partial = nullptr;
+  const dim3 grid = twin_grid(s);
+  if (bias_grad) {
+    PHC_REQUIRE(workspace, "act_bwd: bias_grad needs a workspace");
+    PHC_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "act_bwd: misaligned workspace");
+    partial = static_cast<float *>(workspace);
+  }
+  if (dtype == PHC_DT_F32) launch_bwd<float>(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, partial, s, act, st);
+  else if (dtype == PHC_DT_F16)
+    launch_bwd<_Float16>(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, partial, s, act, st);
+  else launch_bwd<__bf16>(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, partial, s, act, st);
+  if (bias_grad) {
+    const int c = groups * cols;
+    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((c + 255) / 256)), dim3(256), 0, st, partial, (int)grid.y, c,
+                       bias_grad);
+  }
+  return check_launch("act_bwd");
+}

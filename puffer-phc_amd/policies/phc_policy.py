@@ -9,6 +9,7 @@ from torch import nn
 
 from .discriminator_policy import DiscriminatorPolicy
 from .pufferl_policy import Linear, layer_init
+from .twin_mlp import TwinWeights, twin_trunks
 
 
 def mlp(layer_sizes, activation):
@@ -28,9 +29,21 @@ class PHCPolicy(DiscriminatorPolicy):
         self.critic_mlp = nn.Sequential(*mlp([self.input_size] + list(layer_sizes) + [hidden_size], nn.SiLU),
                                         nn.LayerNorm(hidden_size), nn.SiLU(),
                                         layer_init(Linear(hidden_size, 1), std=0.01))
+        # both trunks' Linear layers, run as twin GEMMs + fused HIP epilogues on the device
+        lin = [i for i, m in enumerate(self.actor_mlp) if isinstance(m, nn.Linear)]
+        self._twin = TwinWeights([self.actor_mlp[i] for i in lin], [self.critic_mlp[i] for i in lin])
+        self._head = len(lin) * 2 - 1  # index of the actor LayerNorm in the Sequential
+        self.fused = True
+        self._critic_trunk = None
 
     def encode_observations(self, obs):
         self.obs_pointer = self.obs_norm(obs)
+        if self.fused and obs.is_cuda:
+            y = twin_trunks(self.obs_pointer, self._twin)  # [2, M, hidden]: actor, critic
+            h = self._head
+            self._critic_trunk = y[1]
+            return self.actor_mlp[h + 1](self.actor_mlp[h](y[0])), None
+        self._critic_trunk = None
         return self.actor_mlp(self.obs_pointer), None
 
     def decode_actions(self, hidden, lookup=None):
@@ -41,5 +54,10 @@ class PHCPolicy(DiscriminatorPolicy):
         probs = torch.distributions.Normal(mu, std, validate_args=False)  # no host-syncing checks
         if self.training:
             self.mean_bound_loss = self.bound_loss(mu)
-        value = self.critic_mlp(self.obs_pointer).float()
+        if self._critic_trunk is not None:
+            h, c = self._head, self.critic_mlp
+            value = c[h + 2](c[h + 1](c[h](self._critic_trunk))).float()
+            self._critic_trunk = None
+        else:
+            value = self.critic_mlp(self.obs_pointer).float()
         return probs, value

@@ -1,0 +1,148 @@
+"""Twin actor/critic trunks of PHCPolicy on MI355X (R19/R21).
+
+PHCPolicy (puffer_phc/policies/phc_policy.py:10-61) runs two 6-layer SiLU MLPs of identical
+shape over the same normalised observation.  Here they run side by side: the shared input
+goes through ONE GEMM against the stacked first-layer weights ([2*2048, 934]), layers 2-6 are
+batched GEMMs over the two trunks ([2, M, K] x [2, K, N]), and every bias-add / SiLU /
+SiLU-backward / bias-gradient between the GEMMs is one fused HIP kernel (phc_bias_act_fwd,
+phc_act_bwd).  Parameters stay the reference's nn.Linear modules (same state-dict keys); the
+stacked weights are a cache in the GEMM dtype, rebuilt when a parameter's version changes
+(i.e. after each optimizer step).
+
+GEMM arithmetic follows the autocast context: fp32 storage with torch's "high" matmul
+precision (hipBLASLt xf32) outside autocast, fp16 / bf16 operands (fp32 accumulate, fp32
+weight gradients) inside.  The reference's unfused path (nn.Sequential of Linear/SiLU) is what
+the tests compare against.
+"""
+
+import torch
+
+from .. import _native as N
+
+
+def _compute_dtype():
+    if torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return torch.float32
+
+
+def _mm(a, b, out_fp32):
+    if out_fp32 and a.dtype != torch.float32:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    return torch.mm(a, b)
+
+
+def _bmm(a, b, out_fp32):
+    if out_fp32 and a.dtype != torch.float32:
+        return torch.bmm(a, b, out_dtype=torch.float32)
+    return torch.bmm(a, b)
+
+
+class TwinWeights:
+    """Stacked [actor; critic] weights in the GEMM dtype + fp32 biases, keyed on parameter
+    versions (in-place optimizer updates and load_state_dict bump them)."""
+
+    def __init__(self, actor_linears, critic_linears):
+        assert len(actor_linears) == len(critic_linears)
+        self.pairs = list(zip(actor_linears, critic_linears))
+        self._key = None
+        self.w, self.b = [], []
+
+    def params(self):
+        out = []
+        for a, c in self.pairs:
+            out += [a.weight, a.bias, c.weight, c.bias]
+        return out
+
+    def get(self, dtype):
+        ps = self.params()
+        key = (dtype,) + tuple((p._version, p.data_ptr()) for p in ps)
+        if key != self._key:
+            with torch.no_grad():
+                w, b = [], []
+                for i, (a, c) in enumerate(self.pairs):
+                    if i == 0:
+                        w.append(torch.cat([a.weight, c.weight]).to(dtype).contiguous())
+                    else:
+                        w.append(torch.stack([a.weight, c.weight]).to(dtype).contiguous())
+                    b.append(torch.cat([a.bias, c.bias]).float().contiguous())
+            self.w, self.b, self._key = w, b, key
+        return self.w, self.b
+
+
+class TwinTrunkFn(torch.autograd.Function):
+    """y[2, M, H] = the two trunks' last Linear outputs (before LayerNorm)."""
+
+    @staticmethod
+    def forward(ctx, x, weights, need_grad, *params):
+        dt = _compute_dtype()
+        with torch.autocast("cuda", enabled=False):
+            W, B = weights.get(dt)
+            M = x.shape[0]
+            xc = x.to(dt).contiguous()
+            n1 = W[0].shape[0] // 2
+            y = torch.mm(xc, W[0].t())  # [M, 2*n1], SPLIT
+            z = torch.empty((2, M, n1), dtype=dt, device=x.device)
+            N.bias_act_fwd(y, N.SPLIT, B[0], y if need_grad else None, z, N.GROUPED, M, 2, n1, N.ACT_SILU)
+            pres, zs = [y], [z]
+            L = len(W)
+            for l in range(1, L):
+                n = W[l].shape[1]
+                y = torch.bmm(zs[-1], W[l].transpose(1, 2))  # [2, M, n]
+                if l < L - 1:
+                    z = torch.empty_like(y)
+                    N.bias_act_fwd(y, N.GROUPED, B[l], y if need_grad else None, z, N.GROUPED, M, 2, n, N.ACT_SILU)
+                    pres.append(y)
+                    zs.append(z)
+                else:
+                    N.bias_act_fwd(y, N.GROUPED, B[l], None, y, N.GROUPED, M, 2, n, N.ACT_NONE)
+        if need_grad:
+            ctx.save_for_backward(xc, *W, *pres, *zs)
+            ctx.L = L
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        L = ctx.L
+        saved = ctx.saved_tensors
+        xc, W, pres, zs = saved[0], saved[1:1 + L], saved[1 + L:1 + 2 * L - 1], saved[2 * L:3 * L - 1]
+        dt = xc.dtype
+        M = xc.shape[0]
+        grads = [None] * (2 * L)  # (dW, db) per layer, stacked over the two trunks
+        with torch.autocast("cuda", enabled=False):
+            g = gy.to(dt).contiguous()
+            n = g.shape[2]
+            db = torch.empty(2 * n, dtype=torch.float32, device=g.device)
+            N.act_bwd(g, N.GROUPED, None, N.GROUPED, None, N.GROUPED, db, M, 2, n, N.ACT_NONE)
+            for l in range(L - 1, 0, -1):
+                dW = _bmm(g.transpose(1, 2), zs[l - 1], True)  # [2, n_out, n_in]
+                grads[2 * l], grads[2 * l + 1] = dW, db
+                dz = torch.bmm(g, W[l])  # [2, M, n_in]
+                n = dz.shape[2]
+                db = torch.empty(2 * n, dtype=torch.float32, device=g.device)
+                if l > 1:
+                    N.act_bwd(dz, N.GROUPED, pres[l - 1], N.GROUPED, dz, N.GROUPED, db, M, 2, n, N.ACT_SILU)
+                    g = dz
+                else:
+                    g1 = pres[0]  # SPLIT [M, 2n]: the layer-1 pre-activation buffer is reused for its grad
+                    N.act_bwd(dz, N.GROUPED, pres[0], N.SPLIT, g1, N.SPLIT, db, M, 2, n, N.ACT_SILU)
+                    grads[0] = _mm(g1.t(), xc, True)  # [2n, K]
+                    grads[1] = db
+        out = []
+        for l in range(L):
+            dW, db = grads[2 * l], grads[2 * l + 1]
+            n = db.shape[0] // 2
+            if l == 0:
+                dWa, dWc = dW[:n], dW[n:]
+            else:
+                dWa, dWc = dW[0], dW[1]
+            out += [dWa.float(), db[:n], dWc.float(), db[n:]]
+        return (None, None, None, *out)
+
+
+def twin_trunks(x, weights):
+    """Both trunks' pre-LayerNorm outputs, [2, M, H] (index 0 = actor, 1 = critic)."""
+    if not x.is_cuda:
+        raise RuntimeError("twin_trunks runs on the HIP path only (no CPU fallback)")
+    need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in weights.params())
+    return TwinTrunkFn.apply(x, weights, need_grad, *weights.params())
