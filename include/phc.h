@@ -202,12 +202,14 @@ enum { PHC_ACT_NONE = 0, PHC_ACT_SILU = 1 };
 int phc_bias_act_fwd(const void *y, int32_t y_layout, const float *bias, void *pre, void *out, int32_t out_layout,
                      int64_t rows, int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *stream);
 
-/* grad_pre = grad_out * act'(pre) (nullable; may be grad_out itself when the layouts agree) and
- * bias_grad = column sums of grad_pre in fp32 (nullable; needs phc_act_bwd_workspace_bytes). */
+/* grad_pre = grad_out * act'(pre + pre_bias) (nullable; may be grad_out or pre itself when the
+ * layouts agree; pre_bias fp32 [groups*cols] nullable, so the forward may keep the raw GEMM output
+ * instead of writing pre) and bias_grad = column sums of grad_pre in fp32 (nullable; needs
+ * phc_act_bwd_workspace_bytes of workspace). */
 size_t phc_act_bwd_workspace_bytes(int64_t rows, int32_t groups, int32_t cols);
-int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, int32_t pre_layout, void *grad_pre,
-                int32_t grad_pre_layout, float *bias_grad, int64_t rows, int32_t groups, int32_t cols, int32_t act,
-                int32_t dtype, void *workspace, void *stream);
+int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, int32_t pre_layout,
+                const float *pre_bias, void *grad_pre, int32_t grad_pre_layout, float *bias_grad, int64_t rows,
+                int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *workspace, void *stream);
 
 /* Library version and last error (thread-local). */
 int phc_version(void);

@@ -78,8 +78,9 @@ _EXPORTS = {
     "phc_bias_act_fwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, c_vp, c_vp, ctypes.c_int32, c_i64, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp]),
     "phc_act_bwd_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
-    "phc_act_bwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, ctypes.c_int32, c_vp, ctypes.c_int32, c_vp, c_i64,
-                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp, c_vp]),
+    "phc_act_bwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, ctypes.c_int32, c_vp, c_vp, ctypes.c_int32, c_vp,
+                                    c_i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp,
+                                    c_vp]),
     "phc_physics_replay": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                            ctypes.POINTER(StepParamsC), ctypes.c_float, ctypes.c_float,
                                            ctypes.c_uint64, ctypes.c_uint64, c_vp]),
@@ -310,8 +311,9 @@ def _workspace(nbytes, device):
     return buf
 
 
-def act_bwd(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, bias_grad, rows, groups, cols, act):
-    """grad_pre = grad_out * act'(pre), bias_grad = column sums (phc_act_bwd)."""
+def act_bwd(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, bias_grad, rows, groups, cols, act,
+            pre_bias=None):
+    """grad_pre = grad_out * act'(pre + pre_bias), bias_grad = column sums (phc_act_bwd)."""
     dt = grad_out.dtype
     if dt not in DTYPE_CODE:
         raise ValueError(f"act_bwd: unsupported dtype {dt}")
@@ -320,7 +322,8 @@ def act_bwd(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, bias_grad
         ws = _workspace(lib().phc_act_bwd_workspace_bytes(rows, groups, cols), grad_out.device).data_ptr()
     _check(lib().phc_act_bwd(_twin(grad_out, dt, go_layout, rows, groups, cols, "grad_out"), go_layout,
                              _twin(pre, dt, pre_layout, rows, groups, cols, "pre", nullable=act == ACT_NONE),
-                             pre_layout, _twin(grad_pre, dt, gp_layout, rows, groups, cols, "grad_pre", nullable=True),
+                             pre_layout, _ptr(pre_bias, torch.float32, (groups * cols,), "pre_bias", nullable=True),
+                             _twin(grad_pre, dt, gp_layout, rows, groups, cols, "grad_pre", nullable=True),
                              gp_layout, _ptr(bias_grad, torch.float32, (groups * cols,), "bias_grad", nullable=True),
                              rows, groups, cols, act, DTYPE_CODE[dt], ws, _stream()),
            "phc_act_bwd")

@@ -96,14 +96,19 @@ __global__ __launch_bounds__(256) void k_bias_act_fwd(const T *y, int y_layout, 
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_act_bwd(const T *dz, int dz_layout, const T *pre, int pre_layout,
-                                                 T *g, int g_layout, float *__restrict__ partial, TwinShape s,
-                                                 int act) {
+                                                 const float *__restrict__ pre_bias, T *g, int g_layout,
+                                                 float *__restrict__ partial, TwinShape s, int act) {
   __shared__ float red[4][kColsPerBlock];
   const int lane4 = (threadIdx.x & 63) * 4;
   const int w = threadIdx.x >> 6;
   const int c = blockIdx.x * kColsPerBlock + lane4;
   const bool col_ok = c < s.g * s.n;
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float pb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (col_ok && pre_bias) {
+    const float4 bv = *reinterpret_cast<const float4 *>(pre_bias + c);
+    pb[0] = bv.x; pb[1] = bv.y; pb[2] = bv.z; pb[3] = bv.w;
+  }
   if (col_ok) {
     const int64_t r0 = (int64_t)blockIdx.y * kRowsPerBlock + w;
     for (int i = 0; i < kRowsPerBlock / 4; ++i) {
@@ -115,7 +120,7 @@ __global__ __launch_bounds__(256) void k_act_bwd(const T *dz, int dz_layout, con
         float a[4];
         ld4(pre + twin_off(s, pre_layout, row, c), a);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = silu_grad(d[k], a[k]);
+        for (int k = 0; k < 4; ++k) d[k] = silu_grad(d[k], a[k] + pb[k]);
       }
       if (g) st4(g + twin_off(s, g_layout, row, c), d);
 #pragma unroll
@@ -134,13 +139,31 @@ __global__ __launch_bounds__(256) void k_act_bwd(const T *dz, int dz_layout, con
   }
 }
 
+// column sums of the [rows, cols] partials: 16 lanes x float4 = 64 columns per block, 16 row
+// slices reduced through LDS
 __global__ __launch_bounds__(256) void k_colsum(const float *__restrict__ partial, int rows, int cols,
                                                 float *__restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float acc = 0.0f;
-  for (int r = 0; r < rows; ++r) acc += partial[(int64_t)r * cols + c];
-  out[c] = acc;
+  __shared__ float4 red[16][16];
+  const int cl = threadIdx.x & 15, rs = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + cl * 4;
+  float4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (c < cols) {
+#pragma unroll 4
+    for (int r = rs; r < rows; r += 16) {
+      const float4 v = *reinterpret_cast<const float4 *>(partial + (int64_t)r * cols + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[rs][cl] = acc;
+  __syncthreads();
+  if (rs == 0 && c < cols) {
+    float4 t = red[0][cl];
+    for (int k = 1; k < 16; ++k) {
+      const float4 v = red[k][cl];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    *reinterpret_cast<float4 *>(out + c) = t;
+  }
 }
 
 static int check_twin(const void *p, int layout, int dtype, const char *what) {
@@ -164,10 +187,10 @@ static void launch_fwd(const void *y, int yl, const float *bias, void *pre, void
 }
 
 template <typename T>
-static void launch_bwd(const void *dz, int dl, const void *pre, int pl, void *g, int gl, float *partial, TwinShape s,
-                       int act, hipStream_t st) {
-  hipLaunchKernelGGL(k_act_bwd<T>, twin_grid(s), dim3(256), 0, st, (const T *)dz, dl, (const T *)pre, pl, (T *)g, gl,
-                     partial, s, act);
+static void launch_bwd(const void *dz, int dl, const void *pre, int pl, const float *pb, void *g, int gl,
+                       float *partial, TwinShape s, int act, hipStream_t st) {
+  hipLaunchKernelGGL(k_act_bwd<T>, twin_grid(s), dim3(256), 0, st, (const T *)dz, dl, (const T *)pre, pl, pb, (T *)g,
+                     gl, partial, s, act);
 }
 
 }  // namespace phc
@@ -203,8 +226,8 @@ extern "C" size_t phc_act_bwd_workspace_bytes(int64_t rows, int32_t groups, int3
 }
 
 extern "C" int phc_act_bwd(const void *grad_out, int32_t go_layout, const void *pre, int32_t pre_layout,
-                           void *grad_pre, int32_t gp_layout, float *bias_grad, int64_t rows, int32_t groups,
-                           int32_t cols, int32_t act, int32_t dtype, void *workspace, void *stream) {
+                           const float *pre_bias, void *grad_pre, int32_t gp_layout, float *bias_grad, int64_t rows,
+                           int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *workspace, void *stream) {
   PHC_REQUIRE(rows >= 0 && groups >= 1 && cols > 0 && cols % 4 == 0, "act_bwd: bad shape");
   PHC_REQUIRE(act == PHC_ACT_NONE || act == PHC_ACT_SILU, "act_bwd: bad act");
   PHC_REQUIRE(dtype == PHC_DT_F32 || dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "act_bwd: bad dtype");
@@ -222,6 +245,7 @@ extern "C" int phc_act_bwd(const void *grad_out, int32_t go_layout, const void *
   PHC_REQUIRE(!(grad_pre && grad_pre == grad_out && gp_layout != go_layout),
               "act_bwd: in-place grad needs the grad_out layout");
   PHC_REQUIRE(grad_pre || bias_grad, "act_bwd: nothing to write");
+  PHC_REQUIRE(!pre_bias || (reinterpret_cast<uintptr_t>(pre_bias) & 15) == 0, "act_bwd: misaligned pre_bias");
   float *partial = nullptr;
   const dim3 grid = twin_grid(s);
   if (bias_grad) {
@@ -229,13 +253,14 @@ extern "C" int phc_act_bwd(const void *grad_out, int32_t go_layout, const void *
     PHC_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "act_bwd: misaligned workspace");
     partial = static_cast<float *>(workspace);
   }
-  if (dtype == PHC_DT_F32) launch_bwd<float>(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, partial, s, act, st);
+  if (dtype == PHC_DT_F32)
+    launch_bwd<float>(grad_out, go_layout, pre, pre_layout, pre_bias, grad_pre, gp_layout, partial, s, act, st);
   else if (dtype == PHC_DT_F16)
-    launch_bwd<_Float16>(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, partial, s, act, st);
-  else launch_bwd<__bf16>(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, partial, s, act, st);
+    launch_bwd<_Float16>(grad_out, go_layout, pre, pre_layout, pre_bias, grad_pre, gp_layout, partial, s, act, st);
+  else launch_bwd<__bf16>(grad_out, go_layout, pre, pre_layout, pre_bias, grad_pre, gp_layout, partial, s, act, st);
   if (bias_grad) {
     const int c = groups * cols;
-    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((c + 255) / 256)), dim3(256), 0, st, partial, (int)grid.y, c,
+    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((c + 63) / 64)), dim3(256), 0, st, partial, (int)grid.y, c,
                        bias_grad);
   }
   return check_launch("act_bwd");

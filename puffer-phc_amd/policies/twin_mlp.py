@@ -83,7 +83,8 @@ class TwinTrunkFn(torch.autograd.Function):
             n1 = W[0].shape[0] // 2
             y = torch.mm(xc, W[0].t())  # [M, 2*n1], SPLIT
             z = torch.empty((2, M, n1), dtype=dt, device=x.device)
-            N.bias_act_fwd(y, N.SPLIT, B[0], y if need_grad else None, z, N.GROUPED, M, 2, n1, N.ACT_SILU)
+            # the raw GEMM output y is kept for backward (pre-activation = y + b recomputed there)
+            N.bias_act_fwd(y, N.SPLIT, B[0], None, z, N.GROUPED, M, 2, n1, N.ACT_SILU)
             pres, zs = [y], [z]
             L = len(W)
             for l in range(1, L):
@@ -91,13 +92,13 @@ class TwinTrunkFn(torch.autograd.Function):
                 y = torch.bmm(zs[-1], W[l].transpose(1, 2))  # [2, M, n]
                 if l < L - 1:
                     z = torch.empty_like(y)
-                    N.bias_act_fwd(y, N.GROUPED, B[l], y if need_grad else None, z, N.GROUPED, M, 2, n, N.ACT_SILU)
+                    N.bias_act_fwd(y, N.GROUPED, B[l], None, z, N.GROUPED, M, 2, n, N.ACT_SILU)
                     pres.append(y)
                     zs.append(z)
                 else:
                     N.bias_act_fwd(y, N.GROUPED, B[l], None, y, N.GROUPED, M, 2, n, N.ACT_NONE)
         if need_grad:
-            ctx.save_for_backward(xc, *W, *pres, *zs)
+            ctx.save_for_backward(xc, *W, *B, *pres, *zs)
             ctx.L = L
         return y
 
@@ -105,7 +106,8 @@ class TwinTrunkFn(torch.autograd.Function):
     def backward(ctx, gy):
         L = ctx.L
         saved = ctx.saved_tensors
-        xc, W, pres, zs = saved[0], saved[1:1 + L], saved[1 + L:1 + 2 * L - 1], saved[2 * L:3 * L - 1]
+        xc, W, B = saved[0], saved[1:1 + L], saved[1 + L:1 + 2 * L]
+        pres, zs = saved[1 + 2 * L:3 * L], saved[3 * L:4 * L - 1]
         dt = xc.dtype
         M = xc.shape[0]
         grads = [None] * (2 * L)  # (dW, db) per layer, stacked over the two trunks
@@ -121,11 +123,12 @@ class TwinTrunkFn(torch.autograd.Function):
                 n = dz.shape[2]
                 db = torch.empty(2 * n, dtype=torch.float32, device=g.device)
                 if l > 1:
-                    N.act_bwd(dz, N.GROUPED, pres[l - 1], N.GROUPED, dz, N.GROUPED, db, M, 2, n, N.ACT_SILU)
+                    N.act_bwd(dz, N.GROUPED, pres[l - 1], N.GROUPED, dz, N.GROUPED, db, M, 2, n, N.ACT_SILU,
+                              pre_bias=B[l - 1])
                     g = dz
                 else:
-                    g1 = pres[0]  # SPLIT [M, 2n]: the layer-1 pre-activation buffer is reused for its grad
-                    N.act_bwd(dz, N.GROUPED, pres[0], N.SPLIT, g1, N.SPLIT, db, M, 2, n, N.ACT_SILU)
+                    g1 = pres[0]  # SPLIT [M, 2n]: the layer-1 GEMM output buffer is reused for its grad
+                    N.act_bwd(dz, N.GROUPED, pres[0], N.SPLIT, g1, N.SPLIT, db, M, 2, n, N.ACT_SILU, pre_bias=B[0])
                     grads[0] = _mm(g1.t(), xc, True)  # [2n, K]
                     grads[1] = db
         out = []
