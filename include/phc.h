@@ -211,6 +211,24 @@ int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, 
                 const float *pre_bias, void *grad_pre, int32_t grad_pre_layout, float *bias_grad, int64_t rows,
                 int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *workspace, void *stream);
 
+/* R18: Experience.store (clean_pufferl/structs.py:113-131) on the device.  Each field copies
+ * row r of src [n, row_elems] to row (*cursor + rank(r)) of dst [capacity, row_elems] for the
+ * rows whose mask byte is set (mask NULL = all rows), in row order, while rows remain;
+ * counts[0] = mask-true rows (n_valid), counts[1] = rows taken, *cursor += taken.  cursor and
+ * counts are device int64 so a captured hipGraph can replay the call. */
+#define PHC_MAX_ROW_FIELDS 12
+enum { PHC_ROW_COPY32 = 0, PHC_ROW_COPY64 = 1, PHC_ROW_U8_TO_F32 = 2 };
+typedef struct phc_row_field {
+  const void *src;
+  void *dst;
+  int64_t row_elems; /* elements per row (4-byte, 8-byte or 1-byte source elements by kind) */
+  int32_t kind;
+  int32_t reserved;
+} phc_row_field;
+size_t phc_compact_workspace_bytes(int64_t n);
+int phc_compact_rows(const phc_row_field *fields, int32_t num_fields, const uint8_t *mask, int64_t n,
+                     int64_t *cursor, int64_t capacity, int64_t *counts, void *workspace, void *stream);
+
 /* Library version and last error (thread-local). */
 int phc_version(void);
 const char *phc_last_error(void);

@@ -10,6 +10,7 @@ any op raises.
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 _LIB_PATH = os.environ.get(
@@ -57,6 +58,15 @@ class StepParamsC(ctypes.Structure):
                 ("auto_reset", ctypes.c_int32), ("seed", ctypes.c_uint64)]
 
 
+class RowFieldC(ctypes.Structure):
+    _fields_ = [("src", c_vp), ("dst", c_vp), ("row_elems", c_i64), ("kind", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+MAX_ROW_FIELDS = 12
+ROW_COPY32, ROW_COPY64, ROW_U8_TO_F32 = 0, 1, 2
+
+
 class AmpBuffersC(ctypes.Structure):
     _fields_ = [("amp_obs", c_vp), ("amp_obs_demo", c_vp), ("num_steps", ctypes.c_int32)]
 
@@ -75,6 +85,9 @@ _EXPORTS = {
     "phc_amp_obs": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                     ctypes.POINTER(AmpBuffersC), ctypes.c_float, ctypes.c_int32, c_vp]),
     "phc_actions_to_pd": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "phc_compact_workspace_bytes": (ctypes.c_size_t, [c_i64]),
+    "phc_compact_rows": (ctypes.c_int, [ctypes.POINTER(RowFieldC), ctypes.c_int32, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                         c_vp, c_vp]),
     "phc_bias_act_fwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, c_vp, c_vp, ctypes.c_int32, c_i64, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp]),
     "phc_act_bwd_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
@@ -327,6 +340,51 @@ def act_bwd(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, bias_grad
                              gp_layout, _ptr(bias_grad, torch.float32, (groups * cols,), "bias_grad", nullable=True),
                              rows, groups, cols, act, DTYPE_CODE[dt], ws, _stream()),
            "phc_act_bwd")
+
+
+# ------------------------------------------------------- experience store --
+class RowCompactor:
+    """Experience.store on the device (phc_compact_rows): a fixed list of (src [n, ...],
+    dst [capacity, ...]) tensor pairs, a device cursor and {n_valid, taken} counts.  The C
+    argument array is built once, so repeated calls (or a captured graph) reuse it."""
+
+    def __init__(self, pairs, n, capacity, device):
+        if not 1 <= len(pairs) <= MAX_ROW_FIELDS:
+            raise ValueError(f"RowCompactor: 1..{MAX_ROW_FIELDS} fields")
+        self.n, self.capacity = n, capacity
+        self.cursor = torch.zeros(1, dtype=torch.int64, device=device)
+        self.counts = torch.zeros(2, dtype=torch.int64, device=device)
+        self.workspace = torch.empty(lib().phc_compact_workspace_bytes(n), dtype=torch.uint8, device=device)
+        self._keep = []
+        arr = (RowFieldC * len(pairs))()
+        for k, (src, dst) in enumerate(pairs):
+            if src.shape[0] != n or dst.shape[0] != capacity or src.shape[1:] != dst.shape[1:]:
+                raise ValueError(f"RowCompactor field {k}: src {tuple(src.shape)} vs dst {tuple(dst.shape)}")
+            elems = int(np.prod(src.shape[1:])) if src.dim() > 1 else 1
+            if src.dtype in (torch.bool, torch.uint8) and dst.dtype == torch.float32:
+                kind = ROW_U8_TO_F32
+                src = _as_u8(src)
+            elif src.dtype == dst.dtype and src.element_size() == 4:
+                kind = ROW_COPY32
+            elif src.dtype == dst.dtype and src.element_size() == 8:
+                kind = ROW_COPY64
+            else:
+                raise ValueError(f"RowCompactor field {k}: unsupported {src.dtype} -> {dst.dtype}")
+            _ptr(src, src.dtype, None, f"src{k}")
+            _ptr(dst, dst.dtype, None, f"dst{k}")
+            arr[k] = RowFieldC(src.data_ptr(), dst.data_ptr(), elems, kind, 0)
+            self._keep += [src, dst]
+        self._arr, self._nf = arr, len(pairs)
+
+    def __call__(self, mask=None):
+        _check(lib().phc_compact_rows(self._arr, self._nf,
+                                      _ptr(_as_u8(mask), torch.uint8, (self.n,), "mask", nullable=True), self.n,
+                                      self.cursor.data_ptr(), self.capacity, self.counts.data_ptr(),
+                                      self.workspace.data_ptr(), _stream()),
+               "phc_compact_rows")
+
+    def reset(self, ptr=0):
+        self.cursor.fill_(ptr)
 
 
 def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):

@@ -96,9 +96,99 @@ def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=Non
     return components, info, utilization
 
 
+class RolloutStep:
+    """Device part of one rollout step — policy inference on the env's observation buffer,
+    staging of actions / logprob / value, and Experience.store of the mask-true rows
+    (phc_compact_rows with a device cursor) — captured once as a hipGraph and replayed every
+    step.  The env step (5 HIP launches) stays eager so its kernels keep their own timing.
+    Inputs are the env's persistent buffers, so the graph is valid for the vecenv's lifetime;
+    the twin-trunk weight cache is refreshed in place before every replay."""
+
+    def __init__(self, components, info):
+        env, exp = components.vecenv, components.experience
+        self.env, self.exp, self.policy, self.cfg = env, exp, components.policy, info.config
+        n = env.num_agents
+        dev = env.observations.device
+        self.value = torch.zeros(n, device=dev)
+        self.actions = torch.zeros((n, *env.single_action_space.shape), device=dev)
+        self.logprob = torch.zeros(n, device=dev)
+        pairs = [(env.observations, exp.obs), (self.value, exp.values), (self.actions, exp.actions),
+                 (self.logprob, exp.logprobs), (env.rewards, exp.rewards), (env.terminals, exp.dones),
+                 (env.truncations, exp.truncateds), (env.env_ids, exp.env_ids)]
+        if info.use_amp_obs:
+            pairs.append((env.amp_obs, exp.amp_obs))
+        self.store = _native.RowCompactor(pairs, n, exp.batch_size, dev)
+        self.graph = None
+        self.eager_steps = 0
+        pol = self.policy.policy if hasattr(self.policy, "policy") else self.policy
+        self.twin = getattr(pol, "_twin", None)
+
+    def _body(self):
+        with torch.no_grad(), autocast(self.cfg):
+            actions, logprob, _, value = self.policy(self.env.observations)
+        self.value.copy_(value.flatten())
+        self.actions.copy_(actions)
+        self.logprob.copy_(logprob)
+        self.store(self.env.masks)
+
+    def run(self, use_graph=True):
+        if self.twin is not None:
+            self.twin.get(_compute_dtype(self.cfg))  # in-place refresh after optimizer steps
+        if self.graph is not None:
+            self.graph.replay()
+        elif not use_graph or self.eager_steps == 0:
+            self._body()  # first step eager: lazy library / allocator initialisation
+            self.eager_steps += 1
+        else:
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body()
+            self.graph = g
+            g.replay()
+
+
+def _compute_dtype(cfg):
+    return _AUTOCAST.get(cfg.precision, torch.float32)
+
+
+def _evaluate_graph(components, info):
+    train_cfg, profile, experience = info.config, info.profile, components.experience
+    rs = getattr(components, "rollout", None)
+    if rs is None or rs.exp is not experience or rs.env is not components.vecenv:
+        rs = components.rollout = RolloutStep(components, info)
+    env_infos = defaultdict(list)
+    vecenv = components.vecenv
+    with profile.evaluate:
+        rs.store.reset(experience.ptr)
+        while not experience.full:
+            with profile.env:
+                _, _, _, _, env_info, _, _ = vecenv.recv()
+            for i in env_info:
+                for k, v in i.items():
+                    env_infos[k].append(v)
+            with profile.eval_forward:
+                rs.run(train_cfg.rollout_graph)
+            with profile.env:
+                vecenv.send(rs.actions)
+            with profile.eval_misc:
+                n_valid, taken = rs.store.counts.tolist()  # the reference's mask.sum().item()
+                info.global_step += n_valid
+                experience.ptr += taken
+                experience.step += 1
+        for k, v in env_infos.items():
+            info.stats.extend(k, list(np.atleast_1d(v)))
+    experience.ptr = 0
+    experience.step = 0
+    return info.stats, env_infos
+
+
 def evaluate(components, info):
     """Rollout until the buffer holds batch_size mask-true rows (core.py:120-203)."""
     train_cfg, profile, experience = info.config, info.profile, components.experience
+    if train_cfg.rollout_graph and experience.lstm_h is None and \
+            getattr(components.vecenv, "observations", None) is not None and components.vecenv.observations.is_cuda:
+        return _evaluate_graph(components, info)
     policy = components.policy
     env_infos = defaultdict(list)
     with profile.evaluate:

@@ -178,3 +178,6 @@ class TrainConfig(DeviceConfig):
     # "fp16" = autocast fp16 MFMA (TF32's 10-bit mantissa) with dynamic loss scaling;
     # "bf16" = autocast bf16 MFMA (BASELINE config C5).
     precision: str = "xf32"
+    # replay policy inference + experience store of each rollout step from a captured hipGraph
+    # (the env step itself stays eager); False = the reference's eager loop
+    rollout_graph: bool = True

@@ -375,7 +375,12 @@ __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l,
   const Blend bl = frame_blend(t, m);
   const v3 go = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
   BodyRec s = ref_body(l.frames, bl, b, &go);
-  const unsigned long long base = mix64(seed ^ mix64(counter) ^ ((unsigned long long)(env * kBodies + b) << 8));
+  // noise keyed by (seed, counter, env, body) and, when the env has RNG counters, by the env's
+  // episode (rng_counter) and step (progress): no per-step host value, so a captured graph replays
+  // fresh noise every step
+  unsigned long long key = seed ^ mix64(counter);
+  if (e.rng) key ^= mix64(((unsigned long long)e.rng[env] << 20) ^ (unsigned long long)(unsigned)prog ^ 0x5bd1e995ull);
+  const unsigned long long base = mix64(key ^ ((unsigned long long)(env * kBodies + b) << 8));
   unsigned long long h = mix64(base + 1);
   s.p.x += tri_noise(h, 0, sigma);
   s.p.y += tri_noise(h, 1, sigma);

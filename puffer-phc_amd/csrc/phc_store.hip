@@ -1,0 +1,118 @@
+// phc_store.hip — Experience.store on the device (R18, clean_pufferl/structs.py:113-131).
+//
+// The reference appends the mask-true rows of one rollout step to the flat training buffer
+// (`idx = nonzero(mask)`, CPU copies, a host-side ptr).  Here one scan block ranks the mask,
+// clamps to the remaining capacity and advances a DEVICE cursor; a copy kernel moves every
+// field of every taken row.  No host value enters the launch, so the whole rollout step can be
+// replayed from a hipGraph; the host reads back {n_valid, taken} once per step.
+#include "phc_common.h"
+
+namespace phc {
+
+constexpr int kScanThreads = 1024;
+
+struct RowFields {
+  phc_row_field f[PHC_MAX_ROW_FIELDS];
+  int n;
+};
+
+// workspace: [0] = start row (int64), then rank[n] (int32)
+__global__ __launch_bounds__(kScanThreads) void k_rank_mask(const uint8_t *__restrict__ mask, int64_t n,
+                                                            int64_t *__restrict__ cursor, int64_t capacity,
+                                                            int64_t *__restrict__ counts, int64_t *__restrict__ ws) {
+  __shared__ int64_t warp_tot[kScanThreads / 64];
+  __shared__ int64_t carry;
+  int32_t *rank = reinterpret_cast<int32_t *>(ws + 1);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += kScanThreads) {
+    const int64_t i = base + t;
+    const int v = (i < n && (!mask || mask[i])) ? 1 : 0;
+    // inclusive wave scan
+    int s = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(s, o, 64);
+      if (lane >= o) s += u;
+    }
+    if (lane == 63) warp_tot[wv] = s;
+    __syncthreads();
+    int64_t off = carry;
+    for (int w = 0; w < wv; ++w) off += warp_tot[w];
+    if (i < n) rank[i] = (int32_t)(off + s - v);
+    __syncthreads();
+    if (t == kScanThreads - 1) carry = off + s;
+    __syncthreads();
+  }
+  if (t == 0) {
+    const int64_t total = carry;
+    const int64_t start = *cursor;
+    int64_t room = capacity - start;
+    room = room < 0 ? 0 : room;
+    const int64_t take = total < room ? total : room;
+    counts[0] = total;
+    counts[1] = take;
+    ws[0] = start;
+    *cursor = start + take;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy_rows(RowFields fs, const uint8_t *__restrict__ mask, int64_t n,
+                                                   const int64_t *__restrict__ counts,
+                                                   const int64_t *__restrict__ ws) {
+  const int64_t row = blockIdx.x;
+  if (row >= n || (mask && !mask[row])) return;
+  const int32_t *rank = reinterpret_cast<const int32_t *>(ws + 1);
+  const int64_t r = rank[row];
+  if (r >= counts[1]) return;
+  const int64_t dst_row = ws[0] + r;
+  for (int k = 0; k < fs.n; ++k) {
+    const phc_row_field &f = fs.f[k];
+    const int64_t e = f.row_elems;
+    if (f.kind == PHC_ROW_COPY32) {
+      const uint32_t *s = static_cast<const uint32_t *>(f.src) + row * e;
+      uint32_t *d = static_cast<uint32_t *>(f.dst) + dst_row * e;
+      for (int64_t j = threadIdx.x; j < e; j += 256) d[j] = s[j];
+    } else if (f.kind == PHC_ROW_COPY64) {
+      const uint64_t *s = static_cast<const uint64_t *>(f.src) + row * e;
+      uint64_t *d = static_cast<uint64_t *>(f.dst) + dst_row * e;
+      for (int64_t j = threadIdx.x; j < e; j += 256) d[j] = s[j];
+    } else {  // PHC_ROW_U8_TO_F32: bool flags stored as float (structs.py:124-125)
+      const uint8_t *s = static_cast<const uint8_t *>(f.src) + row * e;
+      float *d = static_cast<float *>(f.dst) + dst_row * e;
+      for (int64_t j = threadIdx.x; j < e; j += 256) d[j] = s[j] ? 1.0f : 0.0f;
+    }
+  }
+}
+
+}  // namespace phc
+
+using namespace phc;
+
+extern "C" size_t phc_compact_workspace_bytes(int64_t n) {
+  return n <= 0 ? 16 : (size_t)(8 + 4 * n + 15) / 16 * 16;
+}
+
+extern "C" int phc_compact_rows(const phc_row_field *fields, int32_t num_fields, const uint8_t *mask, int64_t n,
+                                int64_t *cursor, int64_t capacity, int64_t *counts, void *workspace, void *stream) {
+  PHC_REQUIRE(fields && num_fields >= 1 && num_fields <= PHC_MAX_ROW_FIELDS, "compact_rows: 1..%d fields",
+              PHC_MAX_ROW_FIELDS);
+  PHC_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "compact_rows: bad n");
+  PHC_REQUIRE(cursor && counts && workspace, "compact_rows: null cursor/counts/workspace");
+  PHC_REQUIRE(capacity >= 0, "compact_rows: bad capacity");
+  RowFields fs;
+  fs.n = num_fields;
+  for (int k = 0; k < num_fields; ++k) {
+    const phc_row_field &f = fields[k];
+    PHC_REQUIRE(f.src && f.dst && f.row_elems > 0, "compact_rows: field %d null or empty", k);
+    PHC_REQUIRE(f.kind == PHC_ROW_COPY32 || f.kind == PHC_ROW_COPY64 || f.kind == PHC_ROW_U8_TO_F32,
+                "compact_rows: field %d bad kind", k);
+    fs.f[k] = f;
+  }
+  hipStream_t st = as_stream(stream);
+  int64_t *ws = static_cast<int64_t *>(workspace);
+  hipLaunchKernelGGL(k_rank_mask, dim3(1), dim3(kScanThreads), 0, st, mask, n, cursor, capacity, counts, ws);
+  if (n > 0) hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)n), dim3(256), 0, st, fs, mask, n, counts, ws);
+  return check_launch("compact_rows");
+}

@@ -30,7 +30,10 @@ def layer_init(layer, std=np.sqrt(2), bias_const=0.0):
 def sample_logits(probs, action=None):
     batch = probs.loc.shape[0]
     if action is None:
-        action = probs.sample().view(batch, -1)
+        # same law as probs.sample(); written as loc + scale * N(0,1) because torch.normal(mean,
+        # std) host-checks std on ROCm and so cannot run inside a captured rollout graph
+        with torch.no_grad():
+            action = (probs.loc + probs.scale * torch.randn_like(probs.loc)).view(batch, -1)
     logprob = probs.log_prob(action.view(batch, -1)).sum(1)
     entropy = probs.entropy().view(batch, -1).sum(1)
     return action, logprob, entropy

@@ -32,9 +32,21 @@ def _mm(a, b, out_fp32):
     return torch.mm(a, b)
 
 
-def _bmm(a, b, out_fp32):
-    if out_fp32 and a.dtype != torch.float32:
-        return torch.bmm(a, b, out_dtype=torch.float32)
+def _bmm(a, b, out_fp32=False):
+    """Batched GEMM over the two trunks.  bf16 runs as one GEMM per trunk: hipBLASLt's batched
+    bf16 solution for [2, 32768, 2048] x [2, 2048, 1536] (ROCm 7.0 torch wheel) faults the GPU
+    (illegal address; tools/bf16_probe.py), the per-trunk 2-D GEMMs do not."""
+    out_dt = torch.float32 if (out_fp32 and a.dtype != torch.float32) else None
+    if a.dtype == torch.bfloat16:
+        out = torch.empty((a.shape[0], a.shape[1], b.shape[2]), dtype=out_dt or a.dtype, device=a.device)
+        for g in range(a.shape[0]):
+            if out_dt is None:
+                torch.mm(a[g], b[g], out=out[g])
+            else:
+                out[g] = torch.mm(a[g], b[g], out_dtype=out_dt)
+        return out
+    if out_dt is not None:
+        return torch.bmm(a, b, out_dtype=out_dt)
     return torch.bmm(a, b)
 
 
@@ -55,18 +67,36 @@ class TwinWeights:
         return out
 
     def get(self, dtype):
+        """Stacked weights for `dtype`; refreshed IN PLACE when a parameter changed, so a captured
+        rollout graph that reads these buffers sees every optimizer update."""
         ps = self.params()
         key = (dtype,) + tuple((p._version, p.data_ptr()) for p in ps)
-        if key != self._key:
-            with torch.no_grad():
-                w, b = [], []
-                for i, (a, c) in enumerate(self.pairs):
+        if key == self._key:
+            return self.w, self.b
+        with torch.no_grad():
+            same = bool(self.w) and self.w[0].dtype == dtype
+            for i, (a, c) in enumerate(self.pairs):
+                if same:
                     if i == 0:
-                        w.append(torch.cat([a.weight, c.weight]).to(dtype).contiguous())
+                        n = a.weight.shape[0]
+                        self.w[0][:n].copy_(a.weight)
+                        self.w[0][n:].copy_(c.weight)
                     else:
-                        w.append(torch.stack([a.weight, c.weight]).to(dtype).contiguous())
-                    b.append(torch.cat([a.bias, c.bias]).float().contiguous())
-            self.w, self.b, self._key = w, b, key
+                        self.w[i][0].copy_(a.weight)
+                        self.w[i][1].copy_(c.weight)
+                    self.b[i][:a.bias.shape[0]].copy_(a.bias)
+                    self.b[i][a.bias.shape[0]:].copy_(c.bias)
+                else:
+                    if i == 0:
+                        w = torch.cat([a.weight, c.weight]).to(dtype).contiguous()
+                    else:
+                        w = torch.stack([a.weight, c.weight]).to(dtype).contiguous()
+                    b = torch.cat([a.bias, c.bias]).float().contiguous()
+                    if i == 0:
+                        self.w, self.b = [], []
+                    self.w.append(w)
+                    self.b.append(b)
+        self._key = key
         return self.w, self.b
 
 
@@ -89,7 +119,7 @@ class TwinTrunkFn(torch.autograd.Function):
             L = len(W)
             for l in range(1, L):
                 n = W[l].shape[1]
-                y = torch.bmm(zs[-1], W[l].transpose(1, 2))  # [2, M, n]
+                y = _bmm(zs[-1], W[l].transpose(1, 2))  # [2, M, n]
                 if l < L - 1:
                     z = torch.empty_like(y)
                     N.bias_act_fwd(y, N.GROUPED, B[l], None, z, N.GROUPED, M, 2, n, N.ACT_SILU)
@@ -119,7 +149,7 @@ class TwinTrunkFn(torch.autograd.Function):
             for l in range(L - 1, 0, -1):
                 dW = _bmm(g.transpose(1, 2), zs[l - 1], True)  # [2, n_out, n_in]
                 grads[2 * l], grads[2 * l + 1] = dW, db
-                dz = torch.bmm(g, W[l])  # [2, M, n_in]
+                dz = _bmm(g, W[l])  # [2, M, n_in]
                 n = dz.shape[2]
                 db = torch.empty(2 * n, dtype=torch.float32, device=g.device)
                 if l > 1:

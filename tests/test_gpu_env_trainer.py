@@ -168,3 +168,43 @@ def test_ppo_iteration_reduced_precision(small_env, precision):
     assert all(v.dtype == torch.float32 for v in policy.parameters())
     changed = sum(not torch.equal(before[k], v) for k, v in policy.named_parameters() if v.requires_grad)
     assert changed > 0
+
+
+@pytest.mark.parametrize("use_amp", [False, True])
+def test_graph_rollout_matches_eager_loop(use_amp):
+    """evaluate() with the captured rollout graph + device experience store fills the buffer
+    exactly like the reference's eager loop (same obs / rewards / dones / env ids / values and
+    the same global step count), including partial stores of masked (truncated) rows."""
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig, TrainConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    runs = []
+    for graph in (False, True):
+        q, t, c, fps = synthetic_clips(64, 12, 40, seed=21, device=DEV)  # short clips: many truncations
+        packed = PackedMotions.from_global_rotations(q, t, c, fps)
+        env = PHCPufferEnv(EnvConfig(num_envs=64, seed=8, use_amp_obs=use_amp), motion_data=packed)
+        torch.manual_seed(0)
+        policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+        cfg = TrainConfig(batch_size=64 * 24, minibatch_size=64 * 8, bptt_horizon=8, checkpoint_interval=10 ** 9,
+                          rollout_graph=graph)
+        comps, info, _ = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+        clean_pufferl.evaluate(comps, info)
+        steps1 = info.global_step
+        clean_pufferl.evaluate(comps, info)  # second call: graph replays only
+        e = comps.experience
+        runs.append(dict(step=(steps1, info.global_step), obs=e.obs.clone(), rew=e.rewards.clone(),
+                         done=e.dones.clone(), trunc=e.truncateds.clone(), ids=e.env_ids.clone(),
+                         val=e.values.clone(), amp=e.amp_obs.clone() if use_amp else None,
+                         logp=e.logprobs.clone()))
+    a, b = runs
+    assert a["step"] == b["step"] and a["step"][1] >= 64 * 24 * 2
+    for k in ("obs", "rew", "done", "trunc", "ids"):
+        assert torch.equal(a[k], b[k]), k
+    torch.testing.assert_close(a["val"], b["val"], atol=1e-5, rtol=1e-5)
+    if use_amp:
+        assert torch.equal(a["amp"], b["amp"])
+    assert torch.isfinite(b["logp"]).all()
