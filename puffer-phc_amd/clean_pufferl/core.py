@@ -80,7 +80,9 @@ def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=Non
     if train_cfg.compile:
         policy = torch.compile(policy)
     if optimizer is None:
-        optimizer = torch.optim.Adam(policy.parameters(), lr=train_cfg.learning_rate, eps=1e-5)
+        # one fused kernel for the whole parameter set on the device (same Adam update)
+        fused = next(policy.parameters()).is_cuda
+        optimizer = torch.optim.Adam(policy.parameters(), lr=train_cfg.learning_rate, eps=1e-5, fused=fused)
     initial_params = {name: p.detach().clone() for name, p in policy.named_parameters()}
     components = TrainComponents(vecenv=vecenv, policy=policy, uncompiled_policy=uncompiled_policy,
                                  experience=experience, optimizer=optimizer)
@@ -317,15 +319,13 @@ def train(components, info, utilization=None):
                     if scaler is None:
                         loss.backward()
                         flat.allreduce_mean()
-                        gnorm = flat.norms_sum()
-                        torch.nn.utils.clip_grad_norm_(flat.params, cfg.max_grad_norm)
+                        gnorm = flat.clip_(cfg.max_grad_norm)  # clip_grad_norm_ (core.py:366-370)
                         components.optimizer.step()
                     else:
                         scaler.scale(loss).backward()
                         flat.allreduce_mean()
                         scaler.unscale_(components.optimizer)
-                        gnorm = flat.norms_sum()
-                        torch.nn.utils.clip_grad_norm_(flat.params, cfg.max_grad_norm)
+                        gnorm = flat.clip_(cfg.max_grad_norm)
                         scaler.step(components.optimizer)  # skipped when a grad is inf/nan
                         scaler.update()
                 with profile.train_misc, torch.no_grad():

@@ -78,6 +78,15 @@ class FlatGrads:
         """sum over parameters of ||grad_p|| (clean_pufferl/core.py:366-368), on device."""
         return torch.stack(torch._foreach_norm([p.grad for p in self.params])).sum()
 
+    def clip_(self, max_norm):
+        """torch.nn.utils.clip_grad_norm_ over the flat buffer (one multi-tensor norm, one scale
+        kernel).  Returns the sum of per-parameter norms the reference logs."""
+        norms = torch.stack(torch._foreach_norm([p.grad for p in self.params]))
+        total = torch.linalg.vector_norm(norms)
+        coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+        self.flat.mul_(coef)
+        return norms.sum()
+
 
 def broadcast_params(module, src=0):
     if not is_dist():

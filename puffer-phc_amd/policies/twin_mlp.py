@@ -26,12 +26,6 @@ def _compute_dtype():
     return torch.float32
 
 
-def _mm(a, b, out_fp32):
-    if out_fp32 and a.dtype != torch.float32:
-        return torch.mm(a, b, out_dtype=torch.float32)
-    return torch.mm(a, b)
-
-
 def _bmm(a, b, out_fp32=False):
     """Batched GEMM over the two trunks.  bf16 runs as one GEMM per trunk: hipBLASLt's batched
     bf16 solution for [2, 32768, 2048] x [2, 2048, 1536] (ROCm 7.0 torch wheel) faults the GPU
@@ -48,6 +42,29 @@ def _bmm(a, b, out_fp32=False):
     if out_dt is not None:
         return torch.bmm(a, b, out_dtype=out_dt)
     return torch.bmm(a, b)
+
+
+def _split_k(m, n, k, groups):
+    """Row chunks for a weight-gradient GEMM (a [n, m] x [m, k] reduction over m rows): the output
+    has only ceil(n/256) * ceil(k/256) * groups tiles, too few for 256 CUs, so the rows are cut
+    into S chunks run as one batched GEMM (S * tiles >= ~256 workgroups, >= 1024 rows per chunk)
+    and the fp32 partials summed (measured: tools/gemm_shapes.py)."""
+    tiles = max(1, -(-n // 256) * -(-k // 256) * groups)
+    s = 1
+    while s * 2 * tiles <= 256 and s < 32 and m % (s * 2) == 0 and m // (s * 2) >= 1024:
+        s *= 2
+    return s
+
+
+def _weight_grad(g, z):
+    """dW[b] = g[b]^T z[b] in fp32 for g [B, M, n], z [B, M, k] (split-K over M)."""
+    B, M, n = g.shape
+    k = z.shape[2]
+    S = 1 if g.dtype == torch.bfloat16 else _split_k(M, n, k, B)
+    if S == 1:
+        return _bmm(g.transpose(1, 2), z, True)
+    part = _bmm(g.reshape(B * S, M // S, n).transpose(1, 2), z.reshape(B * S, M // S, k), True)
+    return part.view(B, S, n, k).sum(1)
 
 
 class TwinWeights:
@@ -147,7 +164,7 @@ class TwinTrunkFn(torch.autograd.Function):
             db = torch.empty(2 * n, dtype=torch.float32, device=g.device)
             N.act_bwd(g, N.GROUPED, None, N.GROUPED, None, N.GROUPED, db, M, 2, n, N.ACT_NONE)
             for l in range(L - 1, 0, -1):
-                dW = _bmm(g.transpose(1, 2), zs[l - 1], True)  # [2, n_out, n_in]
+                dW = _weight_grad(g, zs[l - 1])  # [2, n_out, n_in] fp32
                 grads[2 * l], grads[2 * l + 1] = dW, db
                 dz = _bmm(g, W[l])  # [2, M, n_in]
                 n = dz.shape[2]
@@ -159,7 +176,7 @@ class TwinTrunkFn(torch.autograd.Function):
                 else:
                     g1 = pres[0]  # SPLIT [M, 2n]: the layer-1 GEMM output buffer is reused for its grad
                     N.act_bwd(dz, N.GROUPED, pres[0], N.SPLIT, g1, N.SPLIT, db, M, 2, n, N.ACT_SILU, pre_bias=B[0])
-                    grads[0] = _mm(g1.t(), xc, True)  # [2n, K]
+                    grads[0] = _weight_grad(g1[None], xc[None])[0]  # [2n, K]
                     grads[1] = db
         out = []
         for l in range(L):
