@@ -77,7 +77,8 @@ def setup_dist():
     from puffer_phc_amd import distributed as D
 
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        D.init_from_env("nccl")
+        # RCCL over xGMI; PHC_DIST_BACKEND=gloo rehearses several ranks on one GPU
+        D.init_from_env(os.environ.get("PHC_DIST_BACKEND", "nccl"))
     else:
         torch.cuda.set_device(0)
     return D.world_size(), D.rank()

@@ -41,6 +41,8 @@ def init_from_env(backend=None):
         torch.cuda.set_device(local)
         dist.init_process_group(backend, device_id=torch.device("cuda", local))
     else:
+        if torch.cuda.device_count() > 0:  # gloo over device tensors (rank rehearsal on one GPU)
+            torch.cuda.set_device(local % torch.cuda.device_count())
         dist.init_process_group(backend)
     return rank(), world_size()
 
