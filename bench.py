@@ -22,7 +22,8 @@ statistics over RCCL.
 
 Roofline: the dominant kernel of the env step is phc_env_step (HBM-bound); algorithmic bytes
 per env-step = 10,886 (7,122 read + 3,764 written); achieved = bytes x envs /
-average kernel time measured with HIP events around every launch in the timed region.
+average kernel time from HIP start/stop events recorded by each launch's own dispatch
+(hipExtLaunchKernel, phc_env_step_timed) for every launch in the timed region.
 `traffic` = HBM bytes per launch from rocprofv3 PMC counters (2 x FETCH_SIZE + WRITE_SIZE,
 gfx950 correction) read from profiles/traffic_<envs>.json when present, else null.
 
@@ -199,7 +200,9 @@ def main():
     for _ in range(args.warmup):
         runner.step()
     torch.cuda.synchronize()
-    env.env.kernel_events = []
+    from puffer_phc_amd._native import KernelTimer
+
+    timer = env.env.kernel_timer = KernelTimer(capacity=max(4096, 64 * args.steps))
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -212,10 +215,9 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in env.env.kernel_events]
-    env_steps = len(kern_ms)
-    env.env.kernel_events = None
-    kern_s = float(np.mean(kern_ms)) * 1e-3
+    env_steps = timer.count  # phc_env_step launches in the timed region, each timed by its dispatch events
+    kern_s = timer.total_ms() / max(env_steps, 1) * 1e-3
+    env.env.kernel_timer = None
     t = torch.tensor([elapsed, kern_s], dtype=torch.float64, device=device)
     tot = torch.tensor([float(processed)], dtype=torch.float64, device=device)
     if world > 1:

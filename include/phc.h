@@ -120,6 +120,18 @@ int phc_motion_state(const phc_motion_lib *lib, const int64_t *motion_ids, const
 int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
                  void *stream);
 
+/* Kernel timer for measurement: phc_env_step_timed records start/stop events from the kernel
+ * dispatch itself (hipExtLaunchKernel), one pair per launch, up to `capacity` launches;
+ * phc_timer_total_ms waits for them and returns the summed kernel time (negative on error). */
+typedef struct phc_kernel_timer phc_kernel_timer;
+phc_kernel_timer *phc_timer_create(int32_t capacity);
+void phc_timer_destroy(phc_kernel_timer *timer);
+void phc_timer_reset(phc_kernel_timer *timer);
+int32_t phc_timer_count(const phc_kernel_timer *timer);
+double phc_timer_total_ms(phc_kernel_timer *timer);
+int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                       phc_kernel_timer *timer, void *stream);
+
 /* R15: HumanoidPHC.reset(env_ids) with StateInit.Random (humanoid_phc.py:90-103, 663-778,
  * 843-929 + motion_lib.py:526-535) for every env whose flag in `env_mask` is set (env_mask
  * nullable = use env->reset).  `phase` [N] holds the uniform draws (nullable = counter-based

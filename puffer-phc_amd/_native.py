@@ -79,6 +79,13 @@ _EXPORTS = {
                                          ctypes.POINTER(RefStateC), c_vp]),
     "phc_env_step": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                      ctypes.POINTER(StepParamsC), c_vp]),
+    "phc_timer_create": (c_vp, [ctypes.c_int32]),
+    "phc_timer_destroy": (None, [c_vp]),
+    "phc_timer_reset": (None, [c_vp]),
+    "phc_timer_count": (ctypes.c_int32, [c_vp]),
+    "phc_timer_total_ms": (ctypes.c_double, [c_vp]),
+    "phc_env_step_timed": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
+                                           ctypes.POINTER(StepParamsC), c_vp, c_vp]),
     "phc_reset_envs": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                        ctypes.POINTER(StepParamsC), c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint64,
                                        c_vp]),
@@ -258,9 +265,41 @@ def motion_state(mlib, motion_ids, motion_times, offset=None, want_dof=True):
     return body, dof_pos, dof_vel
 
 
-def env_step(env_c, mlib, params):
+def env_step(env_c, mlib, params, timer=None):
+    if timer is not None:
+        _check(lib().phc_env_step_timed(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(params), timer.handle,
+                                        _stream()), "phc_env_step_timed")
+        return
     _check(lib().phc_env_step(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(params), _stream()),
            "phc_env_step")
+
+
+class KernelTimer:
+    """Start/stop events recorded by the kernel dispatch (phc_timer_*): per-launch kernel time
+    without the event-record overhead of stream events."""
+
+    def __init__(self, capacity=4096):
+        self.handle = lib().phc_timer_create(int(capacity))
+        if not self.handle:
+            _check(-1, "phc_timer_create")
+
+    def reset(self):
+        lib().phc_timer_reset(self.handle)
+
+    @property
+    def count(self):
+        return lib().phc_timer_count(self.handle)
+
+    def total_ms(self):
+        ms = lib().phc_timer_total_ms(self.handle)
+        if ms < 0:
+            raise RuntimeError("phc_timer_total_ms failed")
+        return ms
+
+    def __del__(self):
+        if getattr(self, "handle", None) and _lib is not None:
+            _lib.phc_timer_destroy(self.handle)
+            self.handle = None
 
 
 def reset_envs(env_c, mlib, params, mask=None, phase=None, seed=0, counter=0, num_envs=None):

@@ -10,6 +10,10 @@
 // writes its 934-float observation row once.
 #include "phc_common.h"
 
+#include <hip/hip_ext.h>
+
+#include <vector>
+
 namespace phc {
 
 struct StepConsts {
@@ -467,21 +471,81 @@ extern "C" int phc_motion_state(const phc_motion_lib *lib, const int64_t *ids, c
   return check_launch("motion_state");
 }
 
-extern "C" int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
-                            void *stream) {
+// Kernel timer: start/stop events recorded by the dispatch itself (hipExtLaunchKernel), so the
+// measured span is the kernel's own execution, as rocprofv3 reports it.
+struct phc_kernel_timer {
+  std::vector<hipEvent_t> start, stop;
+  int32_t used = 0;
+};
+
+extern "C" phc_kernel_timer *phc_timer_create(int32_t capacity) {
+  if (capacity <= 0) return nullptr;
+  auto *t = new phc_kernel_timer;
+  t->start.resize(capacity);
+  t->stop.resize(capacity);
+  for (int32_t i = 0; i < capacity; ++i) {
+    if (hipEventCreate(&t->start[i]) != hipSuccess || hipEventCreate(&t->stop[i]) != hipSuccess) {
+      set_error("timer: hipEventCreate failed");
+      return nullptr;  // events created so far are leaked on this error path only
+    }
+  }
+  return t;
+}
+
+extern "C" void phc_timer_destroy(phc_kernel_timer *t) {
+  if (!t) return;
+  for (size_t i = 0; i < t->start.size(); ++i) {
+    (void)hipEventDestroy(t->start[i]);
+    (void)hipEventDestroy(t->stop[i]);
+  }
+  delete t;
+}
+
+extern "C" void phc_timer_reset(phc_kernel_timer *t) {
+  if (t) t->used = 0;
+}
+
+extern "C" int32_t phc_timer_count(const phc_kernel_timer *t) { return t ? t->used : 0; }
+
+extern "C" double phc_timer_total_ms(phc_kernel_timer *t) {
+  if (!t) return -1.0;
+  double total = 0.0;
+  for (int32_t i = 0; i < t->used; ++i) {
+    if (hipEventSynchronize(t->stop[i]) != hipSuccess) return -1.0;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, t->start[i], t->stop[i]) != hipSuccess) return -1.0;
+    total += ms;
+  }
+  return total;
+}
+
+extern "C" int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                                  phc_kernel_timer *timer, void *stream) {
   if (int rc = check_env(env)) return rc;
   if (int rc = check_lib(lib)) return rc;
   PHC_REQUIRE(p && p->dt > 0.0f, "env_step: bad params");
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (timer && timer->used < (int32_t)timer->start.size()) {
+    ev0 = timer->start[timer->used];
+    ev1 = timer->stop[timer->used];
+    timer->used += 1;
+  }
+  const dim3 grid(grid_envs(env->num_envs)), block(kBlock);
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot && lib->dof_vel, "env_step: auto_reset needs local_rot and dof_vel");
     PHC_REQUIRE(env->rng_counter, "env_step: auto_reset needs rng_counter");
-    hipLaunchKernelGGL(k_env_step<true>, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
-                       env_view(env), lib_view(lib), make_consts(p));
+    hipExtLaunchKernelGGL(k_env_step<true>, grid, block, 0, as_stream(stream), ev0, ev1, 0, env_view(env),
+                          lib_view(lib), make_consts(p));
   } else {
-    hipLaunchKernelGGL(k_env_step<false>, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
-                       env_view(env), lib_view(lib), make_consts(p));
+    hipExtLaunchKernelGGL(k_env_step<false>, grid, block, 0, as_stream(stream), ev0, ev1, 0, env_view(env),
+                          lib_view(lib), make_consts(p));
   }
   return check_launch("env_step");
+}
+
+extern "C" int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                            void *stream) {
+  return phc_env_step_timed(env, lib, p, nullptr, stream);
 }
 
 extern "C" int phc_reset_envs(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,

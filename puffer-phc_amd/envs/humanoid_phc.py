@@ -76,7 +76,7 @@ class HumanoidPHC:
         self.physics = physics or ReplayPhysics(cfg.replay_pos_sigma, cfg.replay_force_scale, cfg.seed)
         self._rng_seed = int(cfg.seed) * 7919 + 17
         self._rng_counter = 0
-        self.kernel_events = None
+        self.kernel_timer = None  # bench: _native.KernelTimer timing every phc_env_step launch
         self._load_motion(cfg.motion_file if motion_data is None else motion_data)
 
     # ------------------------------------------------------------ setup --
@@ -265,14 +265,7 @@ class HumanoidPHC:
         _native.actions_to_pd(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale, self._pd_frozen)
         self.physics.step(self)
         params = self._step_params_auto if auto_reset else self._step_params
-        if self.kernel_events is not None:  # bench: HIP events around the fused kernel
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()
-            _native.env_step(self._env_c, self._motion_lib.packed.c, params)
-            ev1.record()
-            self.kernel_events.append((ev0, ev1))
-        else:
-            _native.env_step(self._env_c, self._motion_lib.packed.c, params)
+        _native.env_step(self._env_c, self._motion_lib.packed.c, params, timer=self.kernel_timer)
         if auto_reset and "terminals" in self._puffer:
             self.extras["terminate"] = self._puffer["terminals"]  # this step's outcome, written by the kernel
         else:
