@@ -96,12 +96,9 @@ __device__ __forceinline__ Blend frame_blend(float time, const MotionScalars &m)
   return {m.start + f0, m.start + f1, b};
 }
 
-// motion_lib.py:597-610: lerp of pos (+offset) / vel / ang vel, slerp of global rotation
-__device__ __forceinline__ BodyRec ref_body(const float *__restrict__ frames, const Blend &bl, int body,
-                                            const v3 *offset) {
-  const BodyRec a = load_body(frames + (bl.f0 * kBodies + body) * kRec);
-  const BodyRec c = load_body(frames + (bl.f1 * kBodies + body) * kRec);
-  const float t = bl.b;
+// motion_lib.py:597-610: lerp of pos (+offset) / vel / ang vel, slerp of global rotation, from
+// the two raw frame records of this body
+__device__ __forceinline__ BodyRec blend_body(const BodyRec &a, const BodyRec &c, float t, const v3 *offset) {
   const float s = 1.0f - t;
   BodyRec o;
   o.p = {s * a.p.x + t * c.p.x, s * a.p.y + t * c.p.y, s * a.p.z + t * c.p.z};
@@ -110,6 +107,20 @@ __device__ __forceinline__ BodyRec ref_body(const float *__restrict__ frames, co
   o.av = {s * a.av.x + t * c.av.x, s * a.av.y + t * c.av.y, s * a.av.z + t * c.av.z};
   o.r = slerp(a.r, c.r, t);
   return o;
+}
+
+struct RowPair {
+  BodyRec a, c;
+};
+
+__device__ __forceinline__ RowPair load_rows(const float *__restrict__ frames, const Blend &bl, int body) {
+  return {load_body(frames + (bl.f0 * kBodies + body) * kRec), load_body(frames + (bl.f1 * kBodies + body) * kRec)};
+}
+
+__device__ __forceinline__ BodyRec ref_body(const float *__restrict__ frames, const Blend &bl, int body,
+                                            const v3 *offset) {
+  const RowPair r = load_rows(frames, bl, body);
+  return blend_body(r.a, r.c, bl.b, offset);
 }
 
 // dof_pos of body `body` (>=1): exp map of slerped local rotation (motion_lib.py:605-606, 670-673)

@@ -160,17 +160,23 @@ __device__ __forceinline__ float reset_draw(const EnvView &e, int64_t env, unsig
   return uniform01(seed, ctr, (unsigned long long)env);
 }
 
-// Observation of one env from its sim state (this lane's body) and the reference at `t1`.
-__device__ __forceinline__ void env_obs(const EnvView &e, const LibView &l, int64_t env, int lane,
-                                        const MotionScalars &m, const BodyRec &s, float t1, v3 off, bool write) {
+// Observation of one env from its sim state (this lane's body) and the reference state ref1.
+__device__ __forceinline__ void env_obs_ref(const EnvView &e, int64_t env, int lane, const BodyRec &s,
+                                            const BodyRec &ref1, bool write) {
   const bool active = lane < kBodies;
   const int b = active ? lane : 0;
-  const BodyRec ref1 = ref_body(l.frames, frame_blend(t1, m), b, &off);
   const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
   const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
   Heading hinv, hrot;
   heading_quats(root_r, &hrot, &hinv);
   if (write && active) write_obs_body(e.obs + env * kObs, b, s, root_p, hinv, hrot, ref1);
+}
+
+// Observation of one env from its sim state and the reference at `t1` (+ offset `off`).
+__device__ __forceinline__ void env_obs(const EnvView &e, const LibView &l, int64_t env, int lane,
+                                        const MotionScalars &m, const BodyRec &s, float t1, v3 off, bool write) {
+  const int b = lane < kBodies ? lane : 0;
+  env_obs_ref(e, env, lane, s, ref_body(l.frames, frame_blend(t1, m), b, &off), write);
 }
 
 __global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, StepConsts c,
@@ -220,10 +226,15 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
   const v3 go = {e.goff[3 * ei], e.goff[3 * ei + 1], e.goff[3 * ei + 2]};
   const MotionScalars m = load_motion(l, e.motion_ids[ei]);
   const float t = (float)prog * c.dt + st + so;
+  const float t1n = (float)(prog + 1) * c.dt + st + so;  // observation time unless the env resets
   const Blend bl0 = frame_blend(t, m);
+  Blend bl1 = frame_blend(t1n, m);
 
+  // one memory round for the sim record and all four reference rows (t and t+dt)
   BodyRec s = load_body(e.rb + (ei * kBodies + b) * kRec);
-  const BodyRec ref0 = ref_body(l.frames, bl0, b, &go);
+  const RowPair rows0 = load_rows(l.frames, bl0, b);
+  RowPair rows1 = load_rows(l.frames, bl1, b);
+  const BodyRec ref0 = blend_body(rows0.a, rows0.c, bl0.b, &go);
 
   // ---- reward terms (common.py:271-322) ----
   const v3 dp = vsub(ref0.p, s.p);
@@ -231,12 +242,7 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
   e_pos = e_pos + dp.y * dp.y;
   e_pos = (e_pos + dp.z * dp.z) / 3.0f;
   float sin_t;
-#ifdef PHC_EXP_NO_REWARD_TRIG  // timing ablation only
-  const float ang = ref0.r.w - s.r.w;
-  sin_t = 0.0f;
-#else
   const float ang = quat_angle_masked(quat_mul(ref0.r, quat_conj(s.r)), &sin_t);
-#endif
   float e_rot = ang * ang;
   const v3 dv = vsub(ref0.v, s.v);
   float e_vel = dv.x * dv.x;
@@ -318,30 +324,24 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
   }
 
   // ---- observation (and in-launch reset) ----
-  float t1 = (float)(prog + 1) * c.dt + st + so;
   v3 off1 = go;
-  if (AUTO && valid && reset) {
+  if (AUTO && valid && reset) {  // uniform per half-wave
     float mt;
     s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull), &mt);
-    t1 = (float)(0 + 1) * c.dt + mt + 0.0f;
-    off1 = {0.0f, 0.0f, 0.0f};
     if (lane == 0) {
       reset_env_counters(e, ei, mt);
       if (e.rng) e.rng[ei] += 1u;
     }
+    // obs of the re-initialised env: progress 0, start = mt, offsets 0 (humanoid_phc.py:1061-1065)
+    bl1 = frame_blend((float)(0 + 1) * c.dt + mt + 0.0f, m);
+    rows1 = load_rows(l.frames, bl1, b);
+    off1 = {0.0f, 0.0f, 0.0f};
   } else if (valid && lane == 0) {
     e.progress[ei] = (int16_t)prog;
     e.reset[ei] = reset;
     e.term[ei] = terminated;
   }
-#ifdef PHC_EXP_NO_OBS  // timing ablation only: gather the t+dt rows, skip the observation math
-  {
-    const BodyRec r1 = ref_body(l.frames, frame_blend(t1, m), b, &off1);
-    if (valid && active) e.obs[ei * kObs + b] = r1.p.x + r1.r.w + s.v.x;
-  }
-#else
-  env_obs(e, l, ei, lane, m, s, t1, off1, valid);
-#endif
+  env_obs_ref(e, ei, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
 
   if (e.stats) {
     if (lane == 0) {
