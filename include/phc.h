@@ -100,6 +100,8 @@ typedef struct phc_step_params {
   uint32_t reset_body_mask;      /* bit b set = body b counts for termination */
   float termination_distance[PHC_NUM_BODIES];
   int32_t auto_reset;            /* phc_env_step also re-initialises envs that reset (R15 fused) */
+  int32_t reset_at_start;        /* reset to motion time 0 (StateInit.Start / eval flag_test,
+                                    humanoid_phc.py:843-855) instead of a sampled time */
   uint64_t seed;                 /* RNG seed of the reset time draw (with env->rng_counter) */
 } phc_step_params;
 

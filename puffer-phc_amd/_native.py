@@ -55,7 +55,7 @@ class StepParamsC(ctypes.Structure):
                 ("power_coef", ctypes.c_float), ("use_power_reward", ctypes.c_int32),
                 ("enable_early_termination", ctypes.c_int32), ("use_mean_termination", ctypes.c_int32),
                 ("reset_body_mask", ctypes.c_uint32), ("termination_distance", ctypes.c_float * NUM_BODIES),
-                ("auto_reset", ctypes.c_int32), ("seed", ctypes.c_uint64)]
+                ("auto_reset", ctypes.c_int32), ("reset_at_start", ctypes.c_int32), ("seed", ctypes.c_uint64)]
 
 
 class RowFieldC(ctypes.Structure):
@@ -184,9 +184,10 @@ def motion_lib_struct(frames, local_rot, dof_vel, motion_len, motion_dt, num_fra
 
 
 def step_params_struct(dt, reward, power_coef, use_power_reward, enable_early_termination, use_mean,
-                       reset_body_ids, termination_distances, auto_reset=False, seed=0):
+                       reset_body_ids, termination_distances, auto_reset=False, seed=0, reset_at_start=False):
     p = StepParamsC()
     p.auto_reset = int(bool(auto_reset))
+    p.reset_at_start = int(bool(reset_at_start))
     p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     p.dt = float(dt)
     p.k_pos, p.k_rot, p.k_vel, p.k_ang_vel = reward.k_pos, reward.k_rot, reward.k_vel, reward.k_ang_vel

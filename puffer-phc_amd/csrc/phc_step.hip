@@ -28,6 +28,7 @@ struct StepConsts {
   float td[kBodies];
   float td_first;     // termination_distance[first reset body] (eval mean rule)
   float inv_nreset;   // 1 / number of reset bodies
+  int reset_at_start;  // reset to motion time 0
   unsigned long long seed;
 };
 
@@ -51,6 +52,7 @@ static StepConsts make_consts(const phc_step_params *p) {
   }
   c.td_first = first >= 0 ? p->termination_distance[first] : 0.0f;
   c.inv_nreset = n > 0 ? 1.0f / (float)n : 0.0f;
+  c.reset_at_start = p->reset_at_start;
   c.seed = p->seed;
   return c;
 }
@@ -155,7 +157,8 @@ __device__ __forceinline__ void reset_env_counters(const EnvView &e, int64_t env
 }
 
 __device__ __forceinline__ float reset_draw(const EnvView &e, int64_t env, unsigned long long seed,
-                                            unsigned long long counter) {
+                                            unsigned long long counter, bool at_start) {
+  if (at_start) return 0.0f;  // StateInit.Start / flag_test: motion_times[:] = 0
   const unsigned long long ctr = e.rng ? (unsigned long long)e.rng[env] : counter;
   return uniform01(seed, ctr, (unsigned long long)env);
 }
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, Ste
   if (env >= e.n) return;
   if (!(mask ? mask[env] : e.reset[env])) return;  // uniform per half-wave
   const MotionScalars m = load_motion(l, e.motion_ids[env]);
-  const float u = phase ? phase[env] : reset_draw(e, env, seed, counter);
+  const float u = phase ? phase[env] : reset_draw(e, env, seed, counter, c.reset_at_start != 0);
   float mt;
   const BodyRec s = reset_env_state(e, l, env, lane, m, u, &mt);
   // obs of the reset env: progress 0, start = mt, offsets 0 (humanoid_phc.py:1061-1065)
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
   v3 off1 = go;
   if (AUTO && valid && reset) {  // uniform per half-wave
     float mt;
-    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull), &mt);
+    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0), &mt);
     if (lane == 0) {
       reset_env_counters(e, ei, mt);
       if (e.rng) e.rng[ei] += 1u;

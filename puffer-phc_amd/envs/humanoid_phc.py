@@ -194,8 +194,11 @@ class HumanoidPHC:
                 self.cfg.enable_early_termination, self.flag_im_eval, self._reset_bodies_id,
                 self._termination_distances.detach().cpu().tolist())
         seed = int(self.cfg.seed) * 7919 + 17
-        self._step_params = _native.step_params_struct(*args, auto_reset=False, seed=seed)
-        self._step_params_auto = _native.step_params_struct(*args, auto_reset=True, seed=seed)
+        # _sample_ref_state (humanoid_phc.py:843-855): StateInit.Start or eval (flag_test) -> time 0
+        at_start = self.flag_test or self.cfg.state_init == StateInit.Start
+        self._step_params = _native.step_params_struct(*args, auto_reset=False, seed=seed, reset_at_start=at_start)
+        self._step_params_auto = _native.step_params_struct(*args, auto_reset=True, seed=seed,
+                                                            reset_at_start=at_start)
 
     def _load_motion(self, motion_train_file):
         """humanoid_phc.py:620-657: train + eval libraries, even initial sampling."""
@@ -264,9 +267,12 @@ class HumanoidPHC:
             actions = actions.float().contiguous()
         _native.actions_to_pd(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale, self._pd_frozen)
         self.physics.step(self)
-        params = self._step_params_auto if auto_reset else self._step_params
+        # eval mode records MPJPE / positions of the step's own outcome before the envs reset
+        # (the reference resets after HumanoidPHC.step returns): no in-launch reset there
+        fused_reset = auto_reset and not self.flag_im_eval
+        params = self._step_params_auto if fused_reset else self._step_params
         _native.env_step(self._env_c, self._motion_lib.packed.c, params, timer=self.kernel_timer)
-        if auto_reset and "terminals" in self._puffer:
+        if fused_reset and "terminals" in self._puffer:
             self.extras["terminate"] = self._puffer["terminals"]  # this step's outcome, written by the kernel
         else:
             self.extras["terminate"] = self._terminate_buf.clone()
@@ -282,6 +288,8 @@ class HumanoidPHC:
             self.extras["mpjpe"] = (self._rigid_body_pos - res["rg_pos"]).norm(dim=-1).mean(dim=-1)
             self.extras["body_pos"] = self._rigid_body_pos.cpu().numpy()
             self.extras["body_pos_gt"] = res["rg_pos"].cpu().numpy()
+        if auto_reset and not fused_reset:
+            self.reset_done()  # PHCPufferEnv.step's env.reset(reset_indices), clean_pufferl/env.py:114-116
         return self.obs_buf, self.rew_buf, self.reset_buf, self.extras
 
     def render(self):

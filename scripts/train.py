@@ -1,4 +1,4 @@
-"""Training entry point, drop-in for the reference's scripts/train.py (modes train | play).
+"""Training entry point, drop-in for the reference's scripts/train.py (modes train | play | eval).
 
     python scripts/train.py --env.motion-file data/motion/amass_train.pkl --train.total-timesteps 1e9
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 scripts/train.py ...   # one rank per GPU
@@ -26,6 +26,7 @@ from puffer_phc_amd import clean_pufferl, cli  # noqa: E402
 from puffer_phc_amd import distributed as D  # noqa: E402
 from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv  # noqa: E402
 from puffer_phc_amd.config import EnvConfig, PolicyConfig, RNNConfig, TrainConfig  # noqa: E402
+from puffer_phc_amd.eval_stats import EvalStats, eval_rollout  # noqa: E402
 from puffer_phc_amd.policies import PHCPolicy, Policy  # noqa: E402
 
 
@@ -70,8 +71,16 @@ def make_policy(env, args):
 def train(args, vec_env, policy):
     cfg = args.train
     components, state, utilization = clean_pufferl.create(args.exp_id, cfg, args.env, vec_env, policy)
+    data_dir = os.path.join(cfg.data_dir, args.exp_id)
+    os.makedirs(data_dir, exist_ok=True)
+    results = {}
     while state.global_step < cfg.total_timesteps:
         if not args.skip_resample and state.epoch > 0 and state.epoch % cfg.motion_resample_interval == 0:
+            if state.epoch % cfg.checkpoint_interval == 0:  # scripts/train.py:318-327
+                eval_stats = EvalStats(vec_env, failed_save_path=os.path.join(data_dir, f"failed_{state.epoch:06d}.pkl"),
+                                       progress=D.rank() == 0)
+                eval_rollout(vec_env, policy, eval_stats)
+                eval_stats.update_env_and_close()
             vec_env.env.resample_motions()
             vec_env.reset()
         clean_pufferl.evaluate(components, state)
@@ -87,7 +96,32 @@ def train(args, vec_env, policy):
         if D.rank() == 0:
             print(f"epoch {state.epoch} step {state.global_step} SPS {state.profile.SPS:.0f} "
                   f"pg {losses.policy_loss:.4f} v {losses.value_loss:.4f} kl {losses.approx_kl:.5f}", flush=True)
+    if args.final_eval:
+        eval_stats = EvalStats(vec_env, progress=D.rank() == 0)
+        eval_rollout(vec_env, policy, eval_stats)
+        results.update(eval_stats.update_env_and_close())
     clean_pufferl.close(components, state, utilization)
+    return results
+
+
+def evaluate_policy(vec_env, policy, out_prefix="eval"):
+    """--mode eval (scripts/train.py:468-482): success rate / MPJPE over every motion, written as
+    a JSON summary and a per-motion TSV."""
+    import json
+    from datetime import datetime
+
+    eval_stats = EvalStats(vec_env)
+    eval_rollout(vec_env, policy, eval_stats)
+    stamp = datetime.now().strftime("%m%d_%H%M")
+    with open(f"{out_prefix}_summary_{stamp}.json", "w") as f:
+        json.dump(eval_stats.results, f, indent=4)
+    rbm = eval_stats.results_by_motion
+    with open(f"results_by_motion_{stamp}.tsv", "w") as f:
+        f.write("\t".join(rbm) + "\n")
+        for row in zip(*rbm.values()):
+            f.write("\t".join(str(x) for x in row) + "\n")
+    eval_stats.update_env_and_close()
+    return eval_stats.results
 
 
 def rollout(vec_env, policy, steps=1000):
@@ -120,8 +154,10 @@ def main(argv=None):
     elif args.mode == "play":
         vec_env.env.set_termination_distances(10)
         rollout(vec_env, policy)
+    elif args.mode == "eval":
+        print(evaluate_policy(vec_env, policy))
     else:
-        raise NotImplementedError(f"mode {args.mode}: eval (EvalStats) is a SURVEY §8f N2 item, not built yet")
+        raise ValueError(f"unknown mode {args.mode!r} (train | play | eval)")
 
 
 if __name__ == "__main__":
