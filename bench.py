@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--max-len", type=int, default=300)
     ap.add_argument("--precision", default="xf32", choices=["xf32", "fp16", "bf16"],
                     help="policy GEMM arithmetic (TrainConfig.precision)")
+    ap.add_argument("--amp", action="store_true",
+                    help="AMP discriminator obs + discriminator loss (BASELINE config C5, with --precision bf16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic-file", default=None)
@@ -95,7 +97,7 @@ def build_env(args, rank):
     q, t, counts, fps = synthetic_clips(args.envs, args.min_len, args.max_len, seed=1000 + rank, device=device)
     packed = PackedMotions.from_global_rotations(q, t, counts, fps)
     del q, t
-    cfg = EnvConfig(num_envs=args.envs, device_id=torch.cuda.current_device(), seed=rank)
+    cfg = EnvConfig(num_envs=args.envs, device_id=torch.cuda.current_device(), seed=rank, use_amp_obs=args.amp)
     env = PHCPufferEnv(cfg, motion_data=packed)
     env.reset()
     return env, packed, cfg
@@ -181,6 +183,8 @@ class Runner:
         g0 = self.info.global_step
         self.cp.evaluate(self.components, self.info)
         self.policy.policy.update_obs_rms(self.components.experience.obs)
+        if self.args.amp:
+            self.policy.policy.update_amp_obs_rms(self.components.experience.amp_obs)
         self.cp.train(self.components, self.info, self.util)
         return self.info.global_step - g0
 
@@ -261,6 +265,7 @@ def main():
             "config": {"workload": workloads[args.mode], "mode": args.mode, "envs_per_gpu": args.envs,
                        "global_envs": args.envs * world, "motions_per_gpu": args.envs,
                        "parallelism": f"dp{world} (env shards, RCCL grad all-reduce)",
+                       "amp_obs": bool(args.amp),
                        "policy_gemm": {"xf32": "fp32 storage, hipBLASLt xf32 (torch 'high', as the reference)",
                                        "fp16": "autocast fp16 MFMA + dynamic loss scaling",
                                        "bf16": "autocast bf16 MFMA"}[args.precision] if args.mode != "env"
