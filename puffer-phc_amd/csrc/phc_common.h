@@ -153,8 +153,9 @@ __device__ __forceinline__ float group_bcast(float v) { return __shfl(v, 0, kGro
 // The heading rotations use the exact specialisations of phc_quat.h (rot_heading,
 // qmul_heading_*, tan_norm_fast): same float32 values as the generic formulas (only the sign
 // of some exact zeros can differ; checked over 40 steps x 2048 envs with tools/ab_compare.py).
-__device__ __forceinline__ void write_obs_body(float *__restrict__ o, int b, const BodyRec &s, v3 root_p,
-                                               const Heading &hinv, const Heading &hrot, const BodyRec &ref) {
+// self observation slices of body b (common.py:23-103)
+__device__ __forceinline__ void write_self_obs(float *__restrict__ o, int b, const BodyRec &s, v3 root_p,
+                                               const Heading &hinv) {
   float t6[6];
   if (b == 0) {
     o[0] = root_p.z;
@@ -170,8 +171,13 @@ __device__ __forceinline__ void write_obs_body(float *__restrict__ o, int b, con
   o[214 + 3 * b] = x.x; o[215 + 3 * b] = x.y; o[216 + 3 * b] = x.z;
   x = rot_heading(hinv, s.av);
   o[286 + 3 * b] = x.x; o[287 + 3 * b] = x.y; o[288 + 3 * b] = x.z;
-  // task obs
-  x = rot_heading(hinv, vsub(ref.p, s.p));
+}
+
+// imitation (task) observation slices of body b (common.py:107-176, v6, one time step)
+__device__ __forceinline__ void write_task_obs(float *__restrict__ o, int b, const BodyRec &s, v3 root_p,
+                                               const Heading &hinv, const Heading &hrot, const BodyRec &ref) {
+  float t6[6];
+  v3 x = rot_heading(hinv, vsub(ref.p, s.p));
   o[358 + 3 * b] = x.x; o[359 + 3 * b] = x.y; o[360 + 3 * b] = x.z;
   tan_norm_fast(qmul_heading_right(qmul_heading_left(hinv, quat_mul(ref.r, quat_conj(s.r))), hrot), t6);
 #pragma unroll
@@ -185,6 +191,12 @@ __device__ __forceinline__ void write_obs_body(float *__restrict__ o, int b, con
   tan_norm_fast(qmul_heading_left(hinv, ref.r), t6);
 #pragma unroll
   for (int k = 0; k < 6; ++k) o[790 + 6 * b + k] = t6[k];
+}
+
+__device__ __forceinline__ void write_obs_body(float *__restrict__ o, int b, const BodyRec &s, v3 root_p,
+                                               const Heading &hinv, const Heading &hrot, const BodyRec &ref) {
+  write_self_obs(o, b, s, root_p, hinv);
+  write_task_obs(o, b, s, root_p, hinv, hrot, ref);
 }
 
 }  // namespace phc

@@ -208,18 +208,127 @@ __global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, Ste
 //   obs with the reference at t+dt (:935-959, 1061-1112); then PHCPufferEnv.step's
 //   terminals/truncations/masks and episode return/length (clean_pufferl/env.py:103-140)
 //   and, with AUTO, the env.reset(reset_indices) of the envs that came up for reset.
+
+struct Outcome {
+  float rew, r_pos, r_rot, r_vel, r_ang, pr;
+  bool reset, terminated;
+};
+
+// reward (common.py:271-322 + power :1295-1303) and reset (common.py:326-364) of one env from
+// its half-wave; every lane returns the env's totals
+__device__ __forceinline__ Outcome env_reward(const EnvView &e, const StepConsts &c, int64_t ei, int lane, int prog,
+                                              float t, const MotionScalars &m, const BodyRec &s,
+                                              const BodyRec &ref0) {
+  const bool active = lane < kBodies;
+  const int b = active ? lane : 0;
+  const v3 dp = vsub(ref0.p, s.p);
+  float e_pos = dp.x * dp.x;
+  e_pos = e_pos + dp.y * dp.y;
+  e_pos = (e_pos + dp.z * dp.z) / 3.0f;
+  float sin_t;
+  const float ang = quat_angle_masked(quat_mul(ref0.r, quat_conj(s.r)), &sin_t);
+  float e_rot = ang * ang;
+  const v3 dv = vsub(ref0.v, s.v);
+  float e_vel = dv.x * dv.x;
+  e_vel = e_vel + dv.y * dv.y;
+  e_vel = (e_vel + dv.z * dv.z) / 3.0f;
+  const v3 da = vsub(ref0.av, s.av);
+  float e_ang = da.x * da.x;
+  e_ang = e_ang + da.y * da.y;
+  e_ang = (e_ang + da.z * da.z) / 3.0f;
+  // termination distance
+  const float dist = norm3(vsub(s.p, ref0.p));
+  const bool counted = active && ((c.reset_mask >> b) & 1u);
+  float fall = (counted && dist > c.td[b]) ? 1.0f : 0.0f;
+  float dsum = counted ? dist : 0.0f;
+  // power: lane j < 23 owns dofs 3j..3j+2
+  float pw = 0.0f;
+  if (lane < kBodies - 1) {
+    const float *f = e.dof_force + ei * PHC_NUM_DOF + 3 * lane;
+    const float *ds = e.dof_state + (ei * PHC_NUM_DOF + 3 * lane) * 2;
+    pw = fabsf(f[0] * ds[1]);
+    pw = pw + fabsf(f[1] * ds[3]);
+    pw = pw + fabsf(f[2] * ds[5]);
+  }
+  if (!active) e_pos = e_rot = e_vel = e_ang = 0.0f;
+  e_pos = group_sum(e_pos);
+  e_rot = group_sum(e_rot);
+  e_vel = group_sum(e_vel);
+  e_ang = group_sum(e_ang);
+  fall = group_sum(fall);
+  dsum = group_sum(dsum);
+  pw = group_sum(pw);
+
+  Outcome o;
+  o.r_pos = expf(-c.k_pos * (e_pos / (float)kBodies));
+  o.r_rot = expf(-c.k_rot * (e_rot / (float)kBodies));
+  o.r_vel = expf(-c.k_vel * (e_vel / (float)kBodies));
+  o.r_ang = expf(-c.k_ang * (e_ang / (float)kBodies));
+  o.rew = c.w_pos * o.r_pos + c.w_rot * o.r_rot + c.w_vel * o.r_vel + c.w_ang * o.r_ang;
+  o.pr = 0.0f;
+  if (c.use_power) {
+    o.pr = -c.power_coef * pw;
+    if (prog <= 3) o.pr = 0.0f;
+    o.rew = o.rew + o.pr;
+  }
+  const bool pass_time = t >= m.len;
+  o.terminated = false;
+  if (c.enable_et) {
+    const bool fallen = c.use_mean ? (dsum * c.inv_nreset > c.td_first) : (fall > 0.0f);
+    o.terminated = fallen && (prog > 1);
+  }
+  o.reset = pass_time || o.terminated;
+  return o;
+}
+
+// lane 0: reward buffers, PHCPufferEnv bookkeeping, this env's logging row
+__device__ __forceinline__ void env_bookkeeping(const EnvView &e, int64_t ei, const Outcome &o, double st_row[10]) {
+  e.rew[ei] = o.rew;
+  float *raw = e.raw + ei * 5;
+  raw[0] = o.r_pos; raw[1] = o.r_rot; raw[2] = o.r_vel; raw[3] = o.r_ang; raw[4] = o.pr;
+  const bool trunc = o.reset && !o.terminated;
+  if (e.terminals) e.terminals[ei] = o.terminated;
+  if (e.truncs) e.truncs[ei] = trunc;
+  if (e.masks) e.masks[ei] = !trunc;
+  if (e.ep_ret) {
+    float ret = e.ep_ret[ei];
+    int len = e.ep_len[ei];
+    if (o.reset) {
+      st_row[5] = ret;
+      st_row[6] = len;
+      st_row[7] = 1.0;
+      st_row[8] = trunc ? 1.0 : 0.0;
+      st_row[9] = o.terminated ? 1.0 : 0.0;
+      ret = 0.0f;
+      len = 0;
+    }
+    e.ep_ret[ei] = ret + o.rew;
+    e.ep_len[ei] = len + 1;
+  }
+  st_row[0] = o.r_pos; st_row[1] = o.r_rot; st_row[2] = o.r_vel; st_row[3] = o.r_ang; st_row[4] = o.pr;
+}
+
+// one stats row per workgroup, summed over its envs in LDS (no atomics)
+template <int kEnvs>
+__device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10]) {
+  __syncthreads();
+  if (threadIdx.x < 10) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < kEnvs; ++j) acc += sh[j][threadIdx.x];
+    e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] += acc;
+  }
+}
+
+// Half-wave per env, 8 envs per workgroup: the throughput form (large env counts).
 template <bool AUTO>
-#ifndef PHC_ENV_WAVES_PER_SIMD
-#define PHC_ENV_WAVES_PER_SIMD 3
-#endif
-__global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(EnvView e, LibView l, StepConsts c) {
+__global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, StepConsts c) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
   const int g = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + g;
   const int lane = threadIdx.x % kGroup;
   const bool valid = env < e.n;
-  const bool active = lane < kBodies;
-  const int b = active ? lane : 0;
+  const int b = lane < kBodies ? lane : 0;
   const int64_t ei = valid ? env : 0;
 
   // per-env scalars (broadcast loads: every lane of the half-wave reads the same word)
@@ -239,96 +348,13 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
   RowPair rows1 = load_rows(l.frames, bl1, b);
   const BodyRec ref0 = blend_body(rows0.a, rows0.c, bl0.b, &go);
 
-  // ---- reward terms (common.py:271-322) ----
-  const v3 dp = vsub(ref0.p, s.p);
-  float e_pos = dp.x * dp.x;
-  e_pos = e_pos + dp.y * dp.y;
-  e_pos = (e_pos + dp.z * dp.z) / 3.0f;
-  float sin_t;
-  const float ang = quat_angle_masked(quat_mul(ref0.r, quat_conj(s.r)), &sin_t);
-  float e_rot = ang * ang;
-  const v3 dv = vsub(ref0.v, s.v);
-  float e_vel = dv.x * dv.x;
-  e_vel = e_vel + dv.y * dv.y;
-  e_vel = (e_vel + dv.z * dv.z) / 3.0f;
-  const v3 da = vsub(ref0.av, s.av);
-  float e_ang = da.x * da.x;
-  e_ang = e_ang + da.y * da.y;
-  e_ang = (e_ang + da.z * da.z) / 3.0f;
-  // ---- termination distance (common.py:326-364) ----
-  const float dist = norm3(vsub(s.p, ref0.p));
-  const bool counted = active && ((c.reset_mask >> b) & 1u);
-  float fall = (counted && dist > c.td[b]) ? 1.0f : 0.0f;
-  float dsum = counted ? dist : 0.0f;
-  // ---- power (humanoid_phc.py:1295-1303): lane j < 23 owns dofs 3j..3j+2 ----
-  float pw = 0.0f;
-  if (lane < kBodies - 1) {
-    const float *f = e.dof_force + ei * PHC_NUM_DOF + 3 * lane;
-    const float *ds = e.dof_state + (ei * PHC_NUM_DOF + 3 * lane) * 2;
-    pw = fabsf(f[0] * ds[1]);
-    pw = pw + fabsf(f[1] * ds[3]);
-    pw = pw + fabsf(f[2] * ds[5]);
-  }
-  if (!active) e_pos = e_rot = e_vel = e_ang = 0.0f;
-  e_pos = group_sum(e_pos);
-  e_rot = group_sum(e_rot);
-  e_vel = group_sum(e_vel);
-  e_ang = group_sum(e_ang);
-  fall = group_sum(fall);
-  dsum = group_sum(dsum);
-  pw = group_sum(pw);
-
-  // every lane holds the totals: the per-env decisions are uniform over the half-wave
-  const float r_pos = expf(-c.k_pos * (e_pos / (float)kBodies));
-  const float r_rot = expf(-c.k_rot * (e_rot / (float)kBodies));
-  const float r_vel = expf(-c.k_vel * (e_vel / (float)kBodies));
-  const float r_ang = expf(-c.k_ang * (e_ang / (float)kBodies));
-  float rew = c.w_pos * r_pos + c.w_rot * r_rot + c.w_vel * r_vel + c.w_ang * r_ang;
-  float pr = 0.0f;
-  if (c.use_power) {
-    pr = -c.power_coef * pw;
-    if (prog <= 3) pr = 0.0f;
-    rew = rew + pr;
-  }
-  const bool pass_time = t >= m.len;
-  bool terminated = false;
-  if (c.enable_et) {
-    const bool fallen = c.use_mean ? (dsum * c.inv_nreset > c.td_first) : (fall > 0.0f);
-    terminated = fallen && (prog > 1);
-  }
-  const bool reset = pass_time || terminated;
-
+  const Outcome o = env_reward(e, c, ei, lane, prog, t, m, s, ref0);
   double st_row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (valid && lane == 0) {
-    e.rew[ei] = rew;
-    float *raw = e.raw + ei * 5;
-    raw[0] = r_pos; raw[1] = r_rot; raw[2] = r_vel; raw[3] = r_ang; raw[4] = pr;
-    // PHCPufferEnv.step bookkeeping
-    const bool trunc = reset && !terminated;
-    if (e.terminals) e.terminals[ei] = terminated;
-    if (e.truncs) e.truncs[ei] = trunc;
-    if (e.masks) e.masks[ei] = !trunc;
-    if (e.ep_ret) {
-      float ret = e.ep_ret[ei];
-      int len = e.ep_len[ei];
-      if (reset) {
-        st_row[5] = ret;
-        st_row[6] = len;
-        st_row[7] = 1.0;
-        st_row[8] = trunc ? 1.0 : 0.0;
-        st_row[9] = terminated ? 1.0 : 0.0;
-        ret = 0.0f;
-        len = 0;
-      }
-      e.ep_ret[ei] = ret + rew;
-      e.ep_len[ei] = len + 1;
-    }
-    st_row[0] = r_pos; st_row[1] = r_rot; st_row[2] = r_vel; st_row[3] = r_ang; st_row[4] = pr;
-  }
+  if (valid && lane == 0) env_bookkeeping(e, ei, o, st_row);
 
   // ---- observation (and in-launch reset) ----
   v3 off1 = go;
-  if (AUTO && valid && reset) {  // uniform per half-wave
+  if (AUTO && valid && o.reset) {  // uniform per half-wave
     float mt;
     s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0), &mt);
     if (lane == 0) {
@@ -341,8 +367,8 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
     off1 = {0.0f, 0.0f, 0.0f};
   } else if (valid && lane == 0) {
     e.progress[ei] = (int16_t)prog;
-    e.reset[ei] = reset;
-    e.term[ei] = terminated;
+    e.reset[ei] = o.reset;
+    e.term[ei] = o.terminated;
   }
   env_obs_ref(e, ei, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
 
@@ -351,13 +377,7 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES_PER_SIMD) void k_env_step(Env
 #pragma unroll
       for (int k = 0; k < 10; ++k) sh_stats[g][k] = st_row[k];
     }
-    __syncthreads();
-    if (threadIdx.x < 10) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < kEnvsPerBlock; ++j) acc += sh_stats[j][threadIdx.x];
-      e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] += acc;
-    }
+    flush_stats<kEnvsPerBlock>(e, sh_stats);
   }
 }
 
@@ -438,6 +458,7 @@ __global__ __launch_bounds__(kBlock) void k_actions_to_pd(const float *__restric
 }
 
 static int grid_envs(int64_t n) { return (int)((n + kEnvsPerBlock - 1) / kEnvsPerBlock); }
+
 
 static int check_lib(const phc_motion_lib *l) {
   PHC_REQUIRE(l && l->frames && l->motion_len && l->motion_dt && l->num_frames && l->length_starts,
@@ -533,15 +554,17 @@ extern "C" int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_l
     ev1 = timer->stop[timer->used];
     timer->used += 1;
   }
-  const dim3 grid(grid_envs(env->num_envs)), block(kBlock);
+  const dim3 block(kBlock), grid(grid_envs(env->num_envs));
+  hipStream_t st = as_stream(stream);
+  const EnvView ev = env_view(env);
+  const LibView lv = lib_view(lib);
+  const StepConsts cs = make_consts(p);
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot && lib->dof_vel, "env_step: auto_reset needs local_rot and dof_vel");
     PHC_REQUIRE(env->rng_counter, "env_step: auto_reset needs rng_counter");
-    hipExtLaunchKernelGGL(k_env_step<true>, grid, block, 0, as_stream(stream), ev0, ev1, 0, env_view(env),
-                          lib_view(lib), make_consts(p));
+    hipExtLaunchKernelGGL(k_env_step<true>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs);
   } else {
-    hipExtLaunchKernelGGL(k_env_step<false>, grid, block, 0, as_stream(stream), ev0, ev1, 0, env_view(env),
-                          lib_view(lib), make_consts(p));
+    hipExtLaunchKernelGGL(k_env_step<false>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs);
   }
   return check_launch("env_step");
 }
