@@ -9,7 +9,7 @@ from torch import nn
 
 from .discriminator_policy import DiscriminatorPolicy
 from .pufferl_policy import Linear, layer_init
-from .twin_mlp import TwinWeights, twin_trunks
+from .twin_mlp import TwinWeights, head_linear, twin_trunks
 
 
 def mlp(layer_sizes, activation):
@@ -47,7 +47,10 @@ class PHCPolicy(DiscriminatorPolicy):
         return self.actor_mlp(self.obs_pointer), None
 
     def decode_actions(self, hidden, lookup=None):
-        mu = self.mu(hidden).float()  # fp32 head under autocast
+        if self._critic_trunk is not None:  # device path: heads with split-K / chunked-sum gradients
+            mu = head_linear(hidden, self.mu[0]).float()
+        else:
+            mu = self.mu(hidden).float()  # fp32 head under autocast
         std = torch.exp(self.sigma).expand_as(mu)
         if self._deterministic_action is True:
             std = torch.clamp(std, max=1e-6)
@@ -56,7 +59,7 @@ class PHCPolicy(DiscriminatorPolicy):
             self.mean_bound_loss = self.bound_loss(mu)
         if self._critic_trunk is not None:
             h, c = self._head, self.critic_mlp
-            value = c[h + 2](c[h + 1](c[h](self._critic_trunk))).float()
+            value = head_linear(c[h + 1](c[h](self._critic_trunk)), c[h + 2]).float()
             self._critic_trunk = None
         else:
             value = self.critic_mlp(self.obs_pointer).float()

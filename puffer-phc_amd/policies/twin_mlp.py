@@ -196,3 +196,45 @@ def twin_trunks(x, weights):
         raise RuntimeError("twin_trunks runs on the HIP path only (no CPU fallback)")
     need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in weights.params())
     return TwinTrunkFn.apply(x, weights, need_grad, *weights.params())
+
+
+def _row_sum(g):
+    """sum over rows of g [M, N] in fp32 as a two-level reduction: torch's dim-0 sum of a
+    [32768, 69] tensor runs on 128 threads (0.33 ms, rocprofv3), the chunked form on thousands."""
+    M = g.shape[0]
+    S = 1
+    while S < 256 and M % (S * 2) == 0:
+        S *= 2
+    return g.float().reshape(S, M // S, -1).sum(1).sum(0)
+
+
+class HeadLinearFn(torch.autograd.Function):
+    """nn.Linear with few outputs (the actor's mu head 512 -> 69, the critic's value head 512 -> 1)
+    with a split-K weight gradient and a chunked bias gradient: torch's backward for these shapes
+    picks 32x16/32x64-tile GEMMs and a 128-thread bias reduction (~0.8 ms per minibatch)."""
+    # (fp32 head: see forward)
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        # float32 storage in every precision mode: the heads are < 1 % of the FLOPs, and the
+        # odd-width (69, 1) half-precision GEMMs cost more in hipBLASLt solution lookup than math
+        with torch.autocast("cuda", enabled=False):
+            xc = x.float()
+            y = torch.mm(xc, w.t()) + b
+        ctx.save_for_backward(xc, w)
+        ctx.x_dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, wc = ctx.saved_tensors
+        with torch.autocast("cuda", enabled=False):
+            g = gy.to(xc.dtype).contiguous()
+            gx = torch.mm(g, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+            gw = _weight_grad(g[None], xc[None])[0]
+            gb = _row_sum(g)
+        return gx, gw, gb
+
+
+def head_linear(x, lin):
+    return HeadLinearFn.apply(x, lin.weight, lin.bias)
