@@ -243,6 +243,27 @@ size_t phc_compact_workspace_bytes(int64_t n);
 int phc_compact_rows(const phc_row_field *fields, int32_t num_fields, const uint8_t *mask, int64_t n,
                      int64_t *cursor, int64_t capacity, int64_t *counts, void *workspace, void *stream);
 
+/* R21: the PPO minibatch objective (clean_pufferl/core.py:298-352 with the fixed-sigma Normal
+ * log-prob / entropy of pufferlib.sample_logits and PHCPolicy.bound_loss).  Forward: stats[0] =
+ * loss = pg - ent_coef*ent + vf_coef*v + bound_coef*bound, stats[1..7] = pg, v, ent,
+ * old_approx_kl, approx_kl, clipfrac, bound (means); row_coef [m,2] saved for the backward;
+ * adv_mean_std = {mean, std} of the advantages (device, from the global statistics).
+ * Backward: d loss / d mu [m,a] and d loss / d value [m] scaled by grad_loss[0] (device). */
+#define PHC_PPO_STATS 7
+typedef struct phc_ppo_coefs {
+  float clip_coef, vf_clip_coef, vf_coef, ent_coef, bound_coef, soft_bound;
+  int32_t clip_vloss;
+  int32_t reserved;
+} phc_ppo_coefs;
+size_t phc_ppo_workspace_bytes(int64_t m);
+int phc_ppo_loss_fwd(const float *mu, const float *log_sigma, const float *actions, const float *old_logprob,
+                     const float *adv, const float *adv_mean_std, const float *value, const float *old_value,
+                     const float *returns, int64_t m, int32_t a, const phc_ppo_coefs *coefs, float *row_coef,
+                     float *stats, void *workspace, void *stream);
+int phc_ppo_loss_bwd(const float *mu, const float *log_sigma, const float *actions, const float *row_coef,
+                     const float *grad_loss, int64_t m, int32_t a, const phc_ppo_coefs *coefs, float *grad_mu,
+                     float *grad_value, void *stream);
+
 /* Library version and last error (thread-local). */
 int phc_version(void);
 const char *phc_last_error(void);

@@ -67,6 +67,15 @@ MAX_ROW_FIELDS = 12
 ROW_COPY32, ROW_COPY64, ROW_U8_TO_F32 = 0, 1, 2
 
 
+class PpoCoefsC(ctypes.Structure):
+    _fields_ = [("clip_coef", ctypes.c_float), ("vf_clip_coef", ctypes.c_float), ("vf_coef", ctypes.c_float),
+                ("ent_coef", ctypes.c_float), ("bound_coef", ctypes.c_float), ("soft_bound", ctypes.c_float),
+                ("clip_vloss", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+PPO_STATS = 7
+
+
 class AmpBuffersC(ctypes.Structure):
     _fields_ = [("amp_obs", c_vp), ("amp_obs_demo", c_vp), ("num_steps", ctypes.c_int32)]
 
@@ -95,6 +104,11 @@ _EXPORTS = {
     "phc_compact_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_compact_rows": (ctypes.c_int, [ctypes.POINTER(RowFieldC), ctypes.c_int32, c_vp, c_i64, c_vp, c_i64, c_vp,
                                          c_vp, c_vp]),
+    "phc_ppo_workspace_bytes": (ctypes.c_size_t, [c_i64]),
+    "phc_ppo_loss_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
+                                         ctypes.POINTER(PpoCoefsC), c_vp, c_vp, c_vp, c_vp]),
+    "phc_ppo_loss_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
+                                         ctypes.POINTER(PpoCoefsC), c_vp, c_vp, c_vp]),
     "phc_bias_act_fwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, c_vp, c_vp, ctypes.c_int32, c_i64, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp]),
     "phc_act_bwd_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
@@ -380,6 +394,43 @@ def act_bwd(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, bias_grad
                              gp_layout, _ptr(bias_grad, torch.float32, (groups * cols,), "bias_grad", nullable=True),
                              rows, groups, cols, act, DTYPE_CODE[dt], ws, _stream()),
            "phc_act_bwd")
+
+
+# ------------------------------------------------------------ PPO objective --
+def ppo_coefs(clip_coef, vf_clip_coef, vf_coef, ent_coef, bound_coef, soft_bound, clip_vloss):
+    return PpoCoefsC(float(clip_coef), float(vf_clip_coef), float(vf_coef), float(ent_coef), float(bound_coef),
+                     float(soft_bound), int(bool(clip_vloss)), 0)
+
+
+def ppo_loss_fwd(mu, log_sigma, actions, old_logprob, adv, adv_mean_std, value, old_value, returns, coefs):
+    """(stats [1 + PPO_STATS], row_coef [m, 2]) of phc_ppo_loss_fwd."""
+    m, a = mu.shape
+    dev = mu.device
+    stats = torch.empty(1 + PPO_STATS, dtype=torch.float32, device=dev)
+    row_coef = torch.empty((m, 2), dtype=torch.float32, device=dev)
+    ws = _workspace(lib().phc_ppo_workspace_bytes(m), dev)
+    f32 = torch.float32
+    _check(lib().phc_ppo_loss_fwd(_ptr(mu, f32, (m, a), "mu"), _ptr(log_sigma, f32, (a,), "log_sigma"),
+                                  _ptr(actions, f32, (m, a), "actions"), _ptr(old_logprob, f32, (m,), "old_logprob"),
+                                  _ptr(adv, f32, (m,), "adv"), _ptr(adv_mean_std, f32, (2,), "adv_mean_std"),
+                                  _ptr(value, f32, (m,), "value"), _ptr(old_value, f32, (m,), "old_value"),
+                                  _ptr(returns, f32, (m,), "returns"), m, a, ctypes.byref(coefs),
+                                  row_coef.data_ptr(), stats.data_ptr(), ws.data_ptr(), _stream()),
+           "phc_ppo_loss_fwd")
+    return stats, row_coef
+
+
+def ppo_loss_bwd(mu, log_sigma, actions, row_coef, grad_loss, coefs):
+    m, a = mu.shape
+    f32 = torch.float32
+    gmu = torch.empty_like(mu)
+    gv = torch.empty(m, dtype=f32, device=mu.device)
+    _check(lib().phc_ppo_loss_bwd(_ptr(mu, f32, (m, a), "mu"), _ptr(log_sigma, f32, (a,), "log_sigma"),
+                                  _ptr(actions, f32, (m, a), "actions"), _ptr(row_coef, f32, (m, 2), "row_coef"),
+                                  _ptr(grad_loss, f32, (), "grad_loss"), m, a, ctypes.byref(coefs),
+                                  gmu.data_ptr(), gv.data_ptr(), _stream()),
+           "phc_ppo_loss_bwd")
+    return gmu, gv
 
 
 # ------------------------------------------------------- experience store --

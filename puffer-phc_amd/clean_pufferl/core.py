@@ -20,6 +20,7 @@ import torch
 
 from .. import _native
 from .. import distributed as D
+from .ppo_loss import ppo_objective
 from .structs import Experience, LossComponents, Profile, StatsData, TrainComponents, TrainInfo, Utilization
 from .utils import count_params, save_checkpoint, seed_everything
 
@@ -260,6 +261,8 @@ def train(components, info, utilization=None):
                 amp_obs_demo = components.vecenv.fetch_amp_obs_demo()
                 amp_mb = amp_obs_demo.shape[0]
         total_minibatches = experience.num_minibatches * cfg.update_epochs
+        fused_loss = (cfg.fused_loss and hasattr(pol, "forward_train") and getattr(pol, "fused", False)
+                      and experience.lstm_h is None)
         obs_dim = components.vecenv.single_observation_space.shape[0]
         for _epoch in range(cfg.update_epochs):
             for mb in range(experience.num_minibatches):
@@ -270,31 +273,45 @@ def train(components, info, utilization=None):
                     val = experience.b_values[mb]
                     adv = experience.b_advantages[mb]
                     ret = experience.b_returns[mb]
+                fused_obj = fused_loss and obs.is_cuda
                 with profile.train_forward, autocast(cfg):
-                    _, newlogprob, entropy, newvalue = components.policy(obs, action=atn)
-                with profile.train_misc:
-                    logratio = newlogprob - log_probs
-                    ratio = logratio.exp()
-                    with torch.no_grad():
-                        old_approx_kl = (-logratio).mean()
-                        approx_kl = ((ratio - 1) - logratio).mean()
-                        clipfrac = ((ratio - 1.0).abs() > cfg.clip_coef).float().mean()
-                    adv = adv.reshape(-1)
-                    if cfg.norm_adv:
-                        mean, std = D.global_mean_std(adv)
-                        adv = (adv - mean) / (std + 1e-8)
-                    pg_loss1 = -adv * ratio
-                    pg_loss2 = -adv * torch.clamp(ratio, 1 - cfg.clip_coef, 1 + cfg.clip_coef)
-                    pg_loss = torch.max(pg_loss1, pg_loss2).mean()
-                    newvalue = newvalue.view(-1)
-                    if cfg.clip_vloss:
-                        v_unclipped = (newvalue - ret) ** 2
-                        v_clipped = val + torch.clamp(newvalue - val, -cfg.vf_clip_coef, cfg.vf_clip_coef)
-                        v_loss = torch.max(v_unclipped, (v_clipped - ret) ** 2).mean()
+                    if fused_obj:
+                        mu, newvalue = pol.forward_train(obs)
                     else:
-                        v_loss = ((newvalue - ret) ** 2).mean()
-                    entropy_loss = entropy.mean()
-                    loss = pg_loss - cfg.ent_coef * entropy_loss + v_loss * cfg.vf_coef
+                        _, newlogprob, entropy, newvalue = components.policy(obs, action=atn)
+                with profile.train_misc:
+                    adv = adv.reshape(-1)
+                    if fused_obj:
+                        # PPO objective in two HIP kernels (clean_pufferl/ppo_loss.py)
+                        if cfg.norm_adv:
+                            mean, std = D.global_mean_std(adv)
+                        else:
+                            mean, std = 0.0, 1.0
+                        loss, st = ppo_objective(mu, newvalue, pol.sigma, atn, log_probs, adv, mean, std, val, ret,
+                                                 cfg, pol.soft_bound)
+                        pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac, mbl_f = st.unbind(0)
+                    else:
+                        logratio = newlogprob - log_probs
+                        ratio = logratio.exp()
+                        with torch.no_grad():
+                            old_approx_kl = (-logratio).mean()
+                            approx_kl = ((ratio - 1) - logratio).mean()
+                            clipfrac = ((ratio - 1.0).abs() > cfg.clip_coef).float().mean()
+                        if cfg.norm_adv:
+                            mean, std = D.global_mean_std(adv)
+                            adv = (adv - mean) / (std + 1e-8)
+                        pg_loss1 = -adv * ratio
+                        pg_loss2 = -adv * torch.clamp(ratio, 1 - cfg.clip_coef, 1 + cfg.clip_coef)
+                        pg_loss = torch.max(pg_loss1, pg_loss2).mean()
+                        newvalue = newvalue.view(-1)
+                        if cfg.clip_vloss:
+                            v_unclipped = (newvalue - ret) ** 2
+                            v_clipped = val + torch.clamp(newvalue - val, -cfg.vf_clip_coef, cfg.vf_clip_coef)
+                            v_loss = torch.max(v_unclipped, (v_clipped - ret) ** 2).mean()
+                        else:
+                            v_loss = ((newvalue - ret) ** 2).mean()
+                        entropy_loss = entropy.mean()
+                        loss = pg_loss - cfg.ent_coef * entropy_loss + v_loss * cfg.vf_coef
                     disc_loss = torch.zeros((), device=cfg.device)
                     if info.use_amp_obs:
                         amp_agent = torch.cat([experience.b_amp_obs[mb][:amp_mb],
@@ -306,9 +323,12 @@ def train(components, info, utilization=None):
                         disc_loss = 0.5 * (bce(d_agent, torch.zeros_like(d_agent)) + bce(d_demo, torch.ones_like(d_demo)))
                         if cfg.disc_coef > 0:
                             loss = loss + disc_loss * cfg.disc_coef
-                    mbl = getattr(pol, "mean_bound_loss", None)
-                    if cfg.bound_coef > 0 and mbl is not None:
-                        loss = loss + mbl * cfg.bound_coef
+                    if fused_obj:
+                        mbl = mbl_f  # already inside `loss` (bound_coef term of the fused objective)
+                    else:
+                        mbl = getattr(pol, "mean_bound_loss", None)
+                        if cfg.bound_coef > 0 and mbl is not None:
+                            loss = loss + mbl * cfg.bound_coef
                     l2 = _l2_init_reg(list(components.policy.named_parameters()), info.initial_params,
                                       cfg.l2_reg_coef > 0)
                     if cfg.l2_reg_coef > 0:

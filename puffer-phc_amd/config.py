@@ -181,3 +181,6 @@ class TrainConfig(DeviceConfig):
     # replay policy inference + experience store of each rollout step from a captured hipGraph
     # (the env step itself stays eager); False = the reference's eager loop
     rollout_graph: bool = True
+    # PPO objective (ratio / clipping / value / bound losses and their gradients) in two HIP
+    # kernels (clean_pufferl/ppo_loss.py); False = the reference's eager expression
+    fused_loss: bool = True

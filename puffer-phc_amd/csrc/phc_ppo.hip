@@ -1,0 +1,197 @@
+// phc_ppo.hip — the PPO minibatch objective (R21) as two kernels instead of ~60 small torch ops.
+//
+// clean_pufferl/core.py:298-352 (+ policies/phc_policy.py bound loss, pufferlib sample_logits
+// log-prob / entropy of the fixed-sigma Normal): per row r with mu[r, :], action a[r, :]
+//   lp     = sum_j ( -(a - mu)^2 / (2 sigma^2) - log sigma - log sqrt(2 pi) )
+//   ratio  = exp(lp - lp_old);  A = (adv - mean) / (std + 1e-8)
+//   pg     = mean_r max(-A ratio, -A clamp(ratio, 1 - c, 1 + c))
+//   v      = mean_r max((v - R)^2, (v_old + clamp(v - v_old, -vc, vc) - R)^2)   (clip_vloss)
+//   ent    = mean_r sum_j (0.5 + log sqrt(2 pi) + log sigma)
+//   bound  = mean_{r,j} (mu > b) (mu - b)^2 + (mu < -b) (mu + b)^2
+//   loss   = pg - ent_coef ent + vf_coef v + bound_coef bound
+// plus the logged statistics (old_approx_kl, approx_kl, clipfrac).  The forward saves two
+// per-row coefficients (d pg / d lp, d v / d value); the backward forms d loss / d mu and
+// d loss / d value from them.  torch.maximum's tie rule (gradient split evenly) and clamp's
+// inclusive bounds are reproduced.  Statistics reduce through per-block partials (no atomics).
+#include "phc_common.h"
+
+namespace phc {
+
+constexpr int kPpoBlock = 256;
+constexpr int kPpoStats = PHC_PPO_STATS;
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+
+struct PpoArgs {
+  const float *mu, *log_sigma, *actions, *old_logprob, *adv, *adv_mean_std, *value, *old_value, *returns;
+  int64_t m;
+  int a;
+  phc_ppo_coefs c;
+};
+
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// d max(x, y) / dx and / dy with torch.maximum's rule: ties split the gradient evenly
+__device__ __forceinline__ void dmax(float x, float y, float *gx, float *gy) {
+  if (x > y) { *gx = 1.0f; *gy = 0.0f; }
+  else if (x < y) { *gx = 0.0f; *gy = 1.0f; }
+  else { *gx = 0.5f; *gy = 0.5f; }
+}
+
+__global__ __launch_bounds__(kPpoBlock) void k_ppo_fwd(PpoArgs p, float *__restrict__ row_coef,
+                                                       float *__restrict__ partial) {
+  __shared__ float red[kPpoStats][kPpoBlock / 64];
+  const int64_t r = (int64_t)blockIdx.x * kPpoBlock + threadIdx.x;
+  float s[kPpoStats];
+#pragma unroll
+  for (int k = 0; k < kPpoStats; ++k) s[k] = 0.0f;
+  if (r < p.m) {
+    const float *mu = p.mu + r * p.a;
+    const float *act = p.actions + r * p.a;
+    const float b = p.c.soft_bound;
+    float lp = 0.0f, ent = 0.0f, bound = 0.0f;
+    for (int j = 0; j < p.a; ++j) {
+      const float sg = expf(p.log_sigma[j]);  // std = exp(sigma) (phc_policy.py decode_actions)
+      const float ls = logf(sg);               // Normal.log_prob / entropy use scale.log()
+      const float var = sg * sg;
+      const float d = act[j] - mu[j];
+      lp += -(d * d) / (2.0f * var) - ls - kLogSqrt2Pi;
+      ent += 0.5f + kLogSqrt2Pi + ls;
+      const float m = mu[j];
+      bound += m > b ? (m - b) * (m - b) : (m < -b ? (m + b) * (m + b) : 0.0f);
+    }
+    const float logratio = lp - p.old_logprob[r];
+    const float ratio = expf(logratio);
+    const float A = (p.adv[r] - p.adv_mean_std[0]) / (p.adv_mean_std[1] + 1e-8f);
+    const float lo = 1.0f - p.c.clip_coef, hi = 1.0f + p.c.clip_coef;
+    const float t1 = -A * ratio, t2 = -A * clampf(ratio, lo, hi);
+    float g1, g2;
+    dmax(t1, t2, &g1, &g2);
+    const float inside = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+    const float dpg_dratio = -A * g1 + -A * inside * g2;  // per row, before the 1/M of the mean
+    const float v = p.value[r], ret = p.returns[r];
+    float vl, dv;
+    if (p.c.clip_vloss) {
+      const float vu = (v - ret) * (v - ret);
+      const float dvv = v - p.old_value[r];
+      const float vcl = p.old_value[r] + clampf(dvv, -p.c.vf_clip_coef, p.c.vf_clip_coef);
+      const float vc = (vcl - ret) * (vcl - ret);
+      float gu, gc;
+      dmax(vu, vc, &gu, &gc);
+      const float in_v = (dvv >= -p.c.vf_clip_coef && dvv <= p.c.vf_clip_coef) ? 1.0f : 0.0f;
+      vl = vu > vc ? vu : vc;
+      dv = gu * 2.0f * (v - ret) + gc * 2.0f * (vcl - ret) * in_v;
+    } else {
+      vl = (v - ret) * (v - ret);
+      dv = 2.0f * (v - ret);
+    }
+    row_coef[2 * r] = dpg_dratio * ratio;  // d pg_row / d lp
+    row_coef[2 * r + 1] = dv;              // d v_row / d value
+    s[0] = t1 > t2 ? t1 : t2;
+    s[1] = vl;
+    s[2] = ent;
+    s[3] = -logratio;
+    s[4] = (ratio - 1.0f) - logratio;
+    s[5] = fabsf(ratio - 1.0f) > p.c.clip_coef ? 1.0f : 0.0f;
+    s[6] = bound;
+  }
+  // block reduction: wave sums by butterfly, then the 4 wave partials
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kPpoStats; ++k) {
+    float v = s[k];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[k][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kPpoStats) {
+    const int k = threadIdx.x;
+    partial[(int64_t)blockIdx.x * kPpoStats + k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+  }
+}
+
+// stats[0] = loss, then pg, v, ent, old_approx_kl, approx_kl, clipfrac, bound (means); one wave
+__global__ __launch_bounds__(64) void k_ppo_reduce(const float *__restrict__ partial, int blocks, int64_t m, int a,
+                                                   phc_ppo_coefs c, float *__restrict__ stats) {
+  const int k = threadIdx.x;
+  double acc = 0.0;
+  if (k < kPpoStats)
+    for (int i = 0; i < blocks; ++i) acc += partial[(int64_t)i * kPpoStats + k];
+  const float mean = (float)(k == 6 ? acc / ((double)m * a) : acc / (double)m);
+  if (k < kPpoStats) stats[1 + k] = mean;
+  const float pg = __shfl(mean, 0, 64), v = __shfl(mean, 1, 64), ent = __shfl(mean, 2, 64),
+              bound = __shfl(mean, 6, 64);
+  if (k == 0) stats[0] = pg - c.ent_coef * ent + c.vf_coef * v + c.bound_coef * bound;
+}
+
+__global__ __launch_bounds__(kPpoBlock) void k_ppo_bwd(PpoArgs p, const float *__restrict__ row_coef,
+                                                       const float *__restrict__ grad_loss, float *__restrict__ gmu,
+                                                       float *__restrict__ gvalue) {
+  const int64_t i = (int64_t)blockIdx.x * kPpoBlock + threadIdx.x;  // element of [m, a]
+  const float gl = grad_loss[0];
+  const float inv_m = 1.0f / (float)p.m;
+  if (i < p.m * p.a) {
+    const int64_t r = i / p.a;
+    const int j = (int)(i - r * p.a);
+    const float sg = expf(p.log_sigma[j]);
+    const float var = sg * sg;
+    const float mu = p.mu[i];
+    const float d = p.actions[i] - mu;
+    const float b = p.c.soft_bound;
+    const float db = mu > b ? 2.0f * (mu - b) : (mu < -b ? 2.0f * (mu + b) : 0.0f);
+    gmu[i] = gl * (row_coef[2 * r] * inv_m * (d / var) +
+                   p.c.bound_coef * db * (1.0f / ((float)p.m * (float)p.a)));
+  }
+  if (i < p.m) gvalue[i] = gl * p.c.vf_coef * row_coef[2 * i + 1] * inv_m;
+}
+
+static int check_ppo(const PpoArgs &p) {
+  PHC_REQUIRE(p.m > 0 && p.a > 0, "ppo_loss: empty minibatch");
+  PHC_REQUIRE(p.mu && p.log_sigma && p.actions && p.old_logprob && p.adv && p.adv_mean_std && p.value &&
+                  p.old_value && p.returns,
+              "ppo_loss: null input");
+  return PHC_OK;
+}
+
+}  // namespace phc
+
+using namespace phc;
+
+extern "C" size_t phc_ppo_workspace_bytes(int64_t m) {
+  return m <= 0 ? 0 : (size_t)((m + kPpoBlock - 1) / kPpoBlock) * kPpoStats * sizeof(float);
+}
+
+extern "C" int phc_ppo_loss_fwd(const float *mu, const float *log_sigma, const float *actions,
+                                const float *old_logprob, const float *adv, const float *adv_mean_std,
+                                const float *value, const float *old_value, const float *returns, int64_t m,
+                                int32_t a, const phc_ppo_coefs *coefs, float *row_coef, float *stats,
+                                void *workspace, void *stream) {
+  PHC_REQUIRE(coefs && row_coef && stats && workspace, "ppo_loss_fwd: null output/workspace");
+  const PpoArgs p{mu, log_sigma, actions, old_logprob, adv, adv_mean_std, value, old_value, returns, m, a, *coefs};
+  if (int rc = check_ppo(p)) return rc;
+  const int blocks = (int)((m + kPpoBlock - 1) / kPpoBlock);
+  float *partial = static_cast<float *>(workspace);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(k_ppo_fwd, dim3(blocks), dim3(kPpoBlock), 0, st, p, row_coef, partial);
+  hipLaunchKernelGGL(k_ppo_reduce, dim3(1), dim3(64), 0, st, partial, blocks, m, (int)a, *coefs, stats);
+  return check_launch("ppo_loss_fwd");
+}
+
+extern "C" int phc_ppo_loss_bwd(const float *mu, const float *log_sigma, const float *actions,
+                                const float *row_coef, const float *grad_loss, int64_t m, int32_t a,
+                                const phc_ppo_coefs *coefs, float *grad_mu, float *grad_value, void *stream) {
+  PHC_REQUIRE(coefs && row_coef && grad_loss && grad_mu && grad_value && mu && log_sigma && actions,
+              "ppo_loss_bwd: null argument");
+  PHC_REQUIRE(m > 0 && a > 0, "ppo_loss_bwd: empty minibatch");
+  PpoArgs p{};
+  p.mu = mu;
+  p.log_sigma = log_sigma;
+  p.actions = actions;
+  p.m = m;
+  p.a = a;
+  p.c = *coefs;
+  const int64_t n = m * a;
+  hipLaunchKernelGGL(k_ppo_bwd, dim3((unsigned)((n + kPpoBlock - 1) / kPpoBlock)), dim3(kPpoBlock), 0,
+                     as_stream(stream), p, row_coef, grad_loss, grad_mu, grad_value);
+  return check_launch("ppo_loss_bwd");
+}

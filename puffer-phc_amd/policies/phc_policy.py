@@ -46,6 +46,18 @@ class PHCPolicy(DiscriminatorPolicy):
         self._critic_trunk = None
         return self.actor_mlp(self.obs_pointer), None
 
+    def forward_train(self, obs):
+        """(mu [M, A], value [M, 1]) for the fused PPO objective (clean_pufferl/ppo_loss.py): the
+        device path of encode_observations + decode_actions without the Normal distribution."""
+        hidden, _ = self.encode_observations(obs)
+        if self._critic_trunk is None:
+            raise RuntimeError("forward_train needs the device (twin-trunk) path")
+        h, c = self._head, self.critic_mlp
+        mu = head_linear(hidden, self.mu[0]).float()
+        value = head_linear(c[h + 1](c[h](self._critic_trunk)), c[h + 2]).float()
+        self._critic_trunk = None
+        return mu, value
+
     def decode_actions(self, hidden, lookup=None):
         if self._critic_trunk is not None:  # device path: heads with split-K / chunked-sum gradients
             mu = head_linear(hidden, self.mu[0]).float()
