@@ -225,6 +225,18 @@ int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, 
                 const float *pre_bias, void *grad_pre, int32_t grad_pre_layout, float *bias_grad, int64_t rows,
                 int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *workspace, void *stream);
 
+/* R19/R21: the twin trunks' LayerNorm(cols) + SiLU (policies/phc_policy.py:16-30) over a GROUPED
+ * [groups, rows, cols] tensor y (dtype) with per-group gamma/beta [groups*cols] fp32:
+ * z = silu((y - mean) * rstd * gamma + beta) in fp32, mean_rstd [groups*rows, 2] saved.
+ * Backward: dy (dtype) and dgamma / dbeta [groups*cols] fp32 from dz [groups, rows, cols] fp32
+ * (workspace: phc_ln_silu_workspace_bytes).  cols % 256 == 0, cols <= 1024. */
+int phc_ln_silu_fwd(const void *y, const float *gamma, const float *beta, float *z, float *mean_rstd, int64_t rows,
+                    int32_t groups, int32_t cols, float eps, int32_t dtype, void *stream);
+size_t phc_ln_silu_workspace_bytes(int64_t rows, int32_t groups, int32_t cols);
+int phc_ln_silu_bwd(const void *y, const float *gamma, const float *beta, const float *mean_rstd, const float *dz,
+                    void *dy, float *dgamma, float *dbeta, int64_t rows, int32_t groups, int32_t cols, int32_t dtype,
+                    void *workspace, void *stream);
+
 /* R18: Experience.store (clean_pufferl/structs.py:113-131) on the device.  Each field copies
  * row r of src [n, row_elems] to row (*cursor + rank(r)) of dst [capacity, row_elems] for the
  * rows whose mask byte is set (mask NULL = all rows), in row order, while rows remain;

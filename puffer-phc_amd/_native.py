@@ -104,6 +104,11 @@ _EXPORTS = {
     "phc_compact_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_compact_rows": (ctypes.c_int, [ctypes.POINTER(RowFieldC), ctypes.c_int32, c_vp, c_i64, c_vp, c_i64, c_vp,
                                          c_vp, c_vp]),
+    "phc_ln_silu_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_float, ctypes.c_int32, c_vp]),
+    "phc_ln_silu_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
+    "phc_ln_silu_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
+                                        ctypes.c_int32, ctypes.c_int32, c_vp, c_vp]),
     "phc_ppo_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_ppo_loss_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
                                          ctypes.POINTER(PpoCoefsC), c_vp, c_vp, c_vp, c_vp]),
@@ -364,6 +369,35 @@ def bias_act_fwd(y, y_layout, bias, pre, out, out_layout, rows, groups, cols, ac
                                   _twin(out, dt, out_layout, rows, groups, cols, "out", nullable=True), out_layout,
                                   rows, groups, cols, act, DTYPE_CODE[dt], _stream()),
            "phc_bias_act_fwd")
+
+
+def ln_silu_fwd(y, gamma, beta, eps):
+    """z = silu(LayerNorm(y)) per group of a GROUPED [G, M, N] tensor (phc_ln_silu_fwd)."""
+    G, M, N_ = y.shape
+    dt = y.dtype
+    z = torch.empty((G, M, N_), dtype=torch.float32, device=y.device)
+    mr = torch.empty((G * M, 2), dtype=torch.float32, device=y.device)
+    _check(lib().phc_ln_silu_fwd(_ptr(y, dt, (G, M, N_), "y"), _ptr(gamma, torch.float32, (G * N_,), "gamma"),
+                                 _ptr(beta, torch.float32, (G * N_,), "beta"), z.data_ptr(), mr.data_ptr(), M, G, N_,
+                                 float(eps), DTYPE_CODE[dt], _stream()),
+           "phc_ln_silu_fwd")
+    return z, mr
+
+
+def ln_silu_bwd(y, gamma, beta, mean_rstd, dz):
+    G, M, N_ = y.shape
+    dt = y.dtype
+    dy = torch.empty_like(y)
+    dg = torch.empty(G * N_, dtype=torch.float32, device=y.device)
+    db = torch.empty(G * N_, dtype=torch.float32, device=y.device)
+    ws = _workspace(lib().phc_ln_silu_workspace_bytes(M, G, N_), y.device)
+    _check(lib().phc_ln_silu_bwd(_ptr(y, dt, (G, M, N_), "y"), _ptr(gamma, torch.float32, (G * N_,), "gamma"),
+                                 _ptr(beta, torch.float32, (G * N_,), "beta"),
+                                 _ptr(mean_rstd, torch.float32, (G * M, 2), "mean_rstd"),
+                                 _ptr(dz, torch.float32, (G, M, N_), "dz"), dy.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                                 M, G, N_, DTYPE_CODE[dt], ws.data_ptr(), _stream()),
+           "phc_ln_silu_bwd")
+    return dy, dg, db
 
 
 _WS = {}

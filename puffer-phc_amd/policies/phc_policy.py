@@ -9,7 +9,7 @@ from torch import nn
 
 from .discriminator_policy import DiscriminatorPolicy
 from .pufferl_policy import Linear, layer_init
-from .twin_mlp import TwinWeights, head_linear, twin_trunks
+from .twin_mlp import TwinWeights, head_linear, twin_ln_silu, twin_trunks
 
 
 def mlp(layer_sizes, activation):
@@ -34,6 +34,7 @@ class PHCPolicy(DiscriminatorPolicy):
         self._twin = TwinWeights([self.actor_mlp[i] for i in lin], [self.critic_mlp[i] for i in lin])
         self._head = len(lin) * 2 - 1  # index of the actor LayerNorm in the Sequential
         self.fused = True
+        self.fused_ln = True  # LayerNorm + SiLU of both trunks in one kernel (False: torch modules)
         self._critic_trunk = None
 
     def encode_observations(self, obs):
@@ -41,8 +42,13 @@ class PHCPolicy(DiscriminatorPolicy):
         if self.fused and obs.is_cuda:
             y = twin_trunks(self.obs_pointer, self._twin)  # [2, M, hidden]: actor, critic
             h = self._head
-            self._critic_trunk = y[1]
-            return self.actor_mlp[h + 1](self.actor_mlp[h](y[0])), None
+            if self.fused_ln:
+                z = twin_ln_silu(y, self.actor_mlp[h], self.critic_mlp[h])  # LayerNorm + SiLU of both trunks
+            else:
+                z = [self.critic_mlp[h + 1](m[h](y[i])) if i else self.actor_mlp[h + 1](m[h](y[i]))
+                     for i, m in enumerate((self.actor_mlp, self.critic_mlp))]
+            self._critic_trunk = z[1]
+            return z[0], None
         self._critic_trunk = None
         return self.actor_mlp(self.obs_pointer), None
 
@@ -52,9 +58,8 @@ class PHCPolicy(DiscriminatorPolicy):
         hidden, _ = self.encode_observations(obs)
         if self._critic_trunk is None:
             raise RuntimeError("forward_train needs the device (twin-trunk) path")
-        h, c = self._head, self.critic_mlp
         mu = head_linear(hidden, self.mu[0]).float()
-        value = head_linear(c[h + 1](c[h](self._critic_trunk)), c[h + 2]).float()
+        value = head_linear(self._critic_trunk, self.critic_mlp[self._head + 2]).float()
         self._critic_trunk = None
         return mu, value
 
@@ -70,8 +75,7 @@ class PHCPolicy(DiscriminatorPolicy):
         if self.training:
             self.mean_bound_loss = self.bound_loss(mu)
         if self._critic_trunk is not None:
-            h, c = self._head, self.critic_mlp
-            value = head_linear(c[h + 1](c[h](self._critic_trunk)), c[h + 2]).float()
+            value = head_linear(self._critic_trunk, self.critic_mlp[self._head + 2]).float()
             self._critic_trunk = None
         else:
             value = self.critic_mlp(self.obs_pointer).float()

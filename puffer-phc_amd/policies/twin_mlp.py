@@ -238,3 +238,30 @@ class HeadLinearFn(torch.autograd.Function):
 
 def head_linear(x, lin):
     return HeadLinearFn.apply(x, lin.weight, lin.bias)
+
+
+class TwinLNSiLUFn(torch.autograd.Function):
+    """silu(LayerNorm_g(y[g])) for the two trunks (actor g = 0, critic g = 1) in one HIP kernel each
+    way (phc_ln_silu_fwd / _bwd); float32 output as torch's LayerNorm under autocast."""
+
+    @staticmethod
+    def forward(ctx, y, g_a, b_a, g_c, b_c, eps):
+        gamma = torch.cat([g_a, g_c]).float().contiguous()
+        beta = torch.cat([b_a, b_c]).float().contiguous()
+        yc = y.contiguous()
+        z, mr = N.ln_silu_fwd(yc, gamma, beta, eps)
+        ctx.save_for_backward(yc, gamma, beta, mr)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        y, gamma, beta, mr = ctx.saved_tensors
+        dy, dg, db = N.ln_silu_bwd(y, gamma, beta, mr, dz.float().contiguous())
+        n = y.shape[2]
+        return dy, dg[:n], db[:n], dg[n:], db[n:], None
+
+
+def twin_ln_silu(y, ln_a, ln_c):
+    """[2, M, H] trunk outputs -> [2, M, H] float32 silu(LayerNorm(.)) with the actor's / critic's
+    nn.LayerNorm parameters (same eps)."""
+    return TwinLNSiLUFn.apply(y, ln_a.weight, ln_a.bias, ln_c.weight, ln_c.bias, ln_a.eps)

@@ -145,3 +145,28 @@ def test_twin_cache_follows_optimizer_updates():
         a2 = pol(obs)[3]
     assert not torch.equal(a0, a1)
     assert rel(a1, a2) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_ln_silu_kernels_vs_torch(dtype):
+    """phc_ln_silu_fwd / _bwd vs torch LayerNorm + SiLU per group (fp32 math; inputs in dtype)."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    G, M, H = 2, 777, 512  # ragged rows: partial last wave of the backward
+    y = (torch.randn((G, M, H), device=DEV, generator=g) * 2 + 0.5).to(dtype)
+    gamma = torch.randn(G * H, device=DEV, generator=g)
+    beta = torch.randn(G * H, device=DEV, generator=g)
+    z, mr = N.ln_silu_fwd(y.contiguous(), gamma, beta, 1e-5)
+    yr = y.float().clone().requires_grad_(True)
+    gr = gamma.view(G, 1, H).clone().requires_grad_(True)
+    br = beta.view(G, 1, H).clone().requires_grad_(True)
+    ref = torch.nn.functional.silu(torch.nn.functional.layer_norm(yr, (H,), eps=1e-5) * gr + br)
+    torch.testing.assert_close(z, ref.detach(), atol=2e-5, rtol=2e-5)
+    dz = torch.randn((G, M, H), device=DEV, generator=g)
+    ref.backward(dz)
+    dy, dg, db = N.ln_silu_bwd(y.contiguous(), gamma, beta, mr, dz)
+    tol = 2e-5 if dtype == torch.float32 else 2e-3
+    torch.testing.assert_close(dy.float(), yr.grad, atol=tol, rtol=tol)
+    torch.testing.assert_close(dg, gr.grad.view(-1), atol=1e-3, rtol=1e-4)
+    torch.testing.assert_close(db, br.grad.view(-1), atol=1e-3, rtol=1e-4)
