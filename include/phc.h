@@ -211,19 +211,23 @@ enum { PHC_DT_F32 = 0, PHC_DT_F16 = 1, PHC_DT_BF16 = 2 };
 enum { PHC_LAYOUT_SPLIT = 0, PHC_LAYOUT_GROUPED = 1 };
 enum { PHC_ACT_NONE = 0, PHC_ACT_SILU = 1 };
 
-/* pre = y + bias (same layout as y; may be y itself, nullable), out = act(pre) in out_layout
- * (nullable). */
+/* pre = y + bias (same layout and type as y; may be y itself, nullable), out = act(pre) in
+ * out_layout (nullable) as out_dtype: equal to dtype, or f16 / bf16 from an f32 y (fp32 GEMM
+ * outputs feeding half-precision operands of the next GEMM). */
 int phc_bias_act_fwd(const void *y, int32_t y_layout, const float *bias, void *pre, void *out, int32_t out_layout,
-                     int64_t rows, int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *stream);
+                     int64_t rows, int32_t groups, int32_t cols, int32_t act, int32_t dtype, int32_t out_dtype,
+                     void *stream);
 
 /* grad_pre = grad_out * act'(pre + pre_bias) (nullable; may be grad_out or pre itself when the
- * layouts agree; pre_bias fp32 [groups*cols] nullable, so the forward may keep the raw GEMM output
- * instead of writing pre) and bias_grad = column sums of grad_pre in fp32 (nullable; needs
- * phc_act_bwd_workspace_bytes of workspace). */
+ * layouts and types agree; pre_bias fp32 [groups*cols] nullable, so the forward may keep the raw
+ * GEMM output instead of writing pre) and bias_grad = column sums of grad_pre in fp32 (nullable;
+ * needs phc_act_bwd_workspace_bytes of workspace).  grad_out and pre are dtype, grad_pre is
+ * out_dtype (as phc_bias_act_fwd). */
 size_t phc_act_bwd_workspace_bytes(int64_t rows, int32_t groups, int32_t cols);
 int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, int32_t pre_layout,
                 const float *pre_bias, void *grad_pre, int32_t grad_pre_layout, float *bias_grad, int64_t rows,
-                int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *workspace, void *stream);
+                int32_t groups, int32_t cols, int32_t act, int32_t dtype, int32_t out_dtype, void *workspace,
+                void *stream);
 
 /* R19/R21: the twin trunks' LayerNorm(cols) + SiLU (policies/phc_policy.py:16-30) over a GROUPED
  * [groups, rows, cols] tensor y (dtype) with per-group gamma/beta [groups*cols] fp32:

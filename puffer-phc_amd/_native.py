@@ -115,11 +115,11 @@ _EXPORTS = {
     "phc_ppo_loss_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
                                          ctypes.POINTER(PpoCoefsC), c_vp, c_vp, c_vp]),
     "phc_bias_act_fwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, c_vp, c_vp, ctypes.c_int32, c_i64, ctypes.c_int32,
-                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp]),
+                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp]),
     "phc_act_bwd_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
     "phc_act_bwd": (ctypes.c_int, [c_vp, ctypes.c_int32, c_vp, ctypes.c_int32, c_vp, c_vp, ctypes.c_int32, c_vp,
-                                    c_i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_vp,
-                                    c_vp]),
+                                    c_i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_int32, c_vp, c_vp]),
     "phc_physics_replay": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                            ctypes.POINTER(StepParamsC), ctypes.c_float, ctypes.c_float,
                                            ctypes.c_uint64, ctypes.c_uint64, c_vp]),
@@ -359,15 +359,17 @@ def _twin(t, dtype, layout, rows, groups, cols, name, nullable=False):
 
 
 def bias_act_fwd(y, y_layout, bias, pre, out, out_layout, rows, groups, cols, act):
-    """pre = y + bias, out = act(pre) over a twin tensor (phc_bias_act_fwd)."""
+    """pre = y + bias, out = act(pre) over a twin tensor (phc_bias_act_fwd); out may be f16 / bf16
+    from an f32 y."""
     dt = y.dtype
-    if dt not in DTYPE_CODE:
-        raise ValueError(f"bias_act_fwd: unsupported dtype {dt}")
+    ot = out.dtype if out is not None else dt
+    if dt not in DTYPE_CODE or ot not in DTYPE_CODE:
+        raise ValueError(f"bias_act_fwd: unsupported dtypes {dt} -> {ot}")
     _check(lib().phc_bias_act_fwd(_twin(y, dt, y_layout, rows, groups, cols, "y"), y_layout,
                                   _ptr(bias, torch.float32, (groups * cols,), "bias", nullable=True),
                                   _twin(pre, dt, y_layout, rows, groups, cols, "pre", nullable=True),
-                                  _twin(out, dt, out_layout, rows, groups, cols, "out", nullable=True), out_layout,
-                                  rows, groups, cols, act, DTYPE_CODE[dt], _stream()),
+                                  _twin(out, ot, out_layout, rows, groups, cols, "out", nullable=True), out_layout,
+                                  rows, groups, cols, act, DTYPE_CODE[dt], DTYPE_CODE[ot], _stream()),
            "phc_bias_act_fwd")
 
 
@@ -414,19 +416,21 @@ def _workspace(nbytes, device):
 
 def act_bwd(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, bias_grad, rows, groups, cols, act,
             pre_bias=None):
-    """grad_pre = grad_out * act'(pre + pre_bias), bias_grad = column sums (phc_act_bwd)."""
+    """grad_pre = grad_out * act'(pre + pre_bias), bias_grad = column sums (phc_act_bwd); grad_pre
+    may be f16 / bf16 from an f32 grad_out / pre."""
     dt = grad_out.dtype
-    if dt not in DTYPE_CODE:
-        raise ValueError(f"act_bwd: unsupported dtype {dt}")
+    ot = grad_pre.dtype if grad_pre is not None else dt
+    if dt not in DTYPE_CODE or ot not in DTYPE_CODE:
+        raise ValueError(f"act_bwd: unsupported dtypes {dt} -> {ot}")
     ws = None
     if bias_grad is not None:
         ws = _workspace(lib().phc_act_bwd_workspace_bytes(rows, groups, cols), grad_out.device).data_ptr()
     _check(lib().phc_act_bwd(_twin(grad_out, dt, go_layout, rows, groups, cols, "grad_out"), go_layout,
                              _twin(pre, dt, pre_layout, rows, groups, cols, "pre", nullable=act == ACT_NONE),
                              pre_layout, _ptr(pre_bias, torch.float32, (groups * cols,), "pre_bias", nullable=True),
-                             _twin(grad_pre, dt, gp_layout, rows, groups, cols, "grad_pre", nullable=True),
+                             _twin(grad_pre, ot, gp_layout, rows, groups, cols, "grad_pre", nullable=True),
                              gp_layout, _ptr(bias_grad, torch.float32, (groups * cols,), "bias_grad", nullable=True),
-                             rows, groups, cols, act, DTYPE_CODE[dt], ws, _stream()),
+                             rows, groups, cols, act, DTYPE_CODE[dt], DTYPE_CODE[ot], ws, _stream()),
            "phc_act_bwd")
 
 

@@ -68,9 +68,9 @@ __device__ __forceinline__ float silu_grad(float dz, float a) {
   return dz * sg * (1.0f + a * (1.0f - sg));
 }
 
-template <typename T>
+template <typename T, typename To>
 __global__ __launch_bounds__(256) void k_bias_act_fwd(const T *y, int y_layout, const float *__restrict__ bias, T *pre,
-                                                      T *out, int out_layout, TwinShape s, int act) {
+                                                      To *out, int out_layout, TwinShape s, int act) {
   const int c = blockIdx.x * kColsPerBlock + (threadIdx.x & 63) * 4;
   if (c >= s.g * s.n) return;
   float b[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -96,9 +96,9 @@ __global__ __launch_bounds__(256) void k_bias_act_fwd(const T *y, int y_layout, 
   }
 }
 
-template <typename T>
+template <typename T, typename To>
 __global__ __launch_bounds__(256) void k_act_bwd(const T *dz, int dz_layout, const T *pre, int pre_layout,
-                                                 const float *__restrict__ pre_bias, T *g, int g_layout,
+                                                 const float *__restrict__ pre_bias, To *g, int g_layout,
                                                  float *__restrict__ partial, TwinShape s, int act) {
   __shared__ float red[4][kColsPerBlock];
   const int lane4 = (threadIdx.x & 63) * 4;
@@ -360,6 +360,8 @@ __global__ __launch_bounds__(256) void k_colsum_strided(const float *__restrict_
   }
 }
 
+static bool valid_dtype(int d) { return d == PHC_DT_F32 || d == PHC_DT_F16 || d == PHC_DT_BF16; }
+
 static int check_twin(const void *p, int layout, int dtype, const char *what) {
   PHC_REQUIRE(p, "%s: null tensor", what);
   PHC_REQUIRE(layout == PHC_LAYOUT_SPLIT || layout == PHC_LAYOUT_GROUPED, "%s: bad layout", what);
@@ -373,19 +375,31 @@ static dim3 twin_grid(const TwinShape &s) {
               (unsigned)((s.m + kRowsPerBlock - 1) / kRowsPerBlock));
 }
 
-template <typename T>
-static void launch_fwd(const void *y, int yl, const float *bias, void *pre, void *out, int ol, TwinShape s, int act,
-                       hipStream_t st) {
-  hipLaunchKernelGGL(k_bias_act_fwd<T>, twin_grid(s), dim3(256), 0, st, (const T *)y, yl, bias, (T *)pre, (T *)out,
-                     ol, s, act);
+// element-type pairs (input, output): equal types, or f32 GEMM outputs -> f16 / bf16 operands
+template <template <typename, typename> class K, typename F>
+static bool dispatch_twin(int dtype, int out_dtype, F &&launch) {
+  if (dtype == out_dtype) {
+    if (dtype == PHC_DT_F32) launch(K<float, float>{});
+    else if (dtype == PHC_DT_F16) launch(K<_Float16, _Float16>{});
+    else launch(K<__bf16, __bf16>{});
+    return true;
+  }
+  if (dtype != PHC_DT_F32) return false;
+  if (out_dtype == PHC_DT_F16) launch(K<float, _Float16>{});
+  else launch(K<float, __bf16>{});
+  return true;
 }
 
-template <typename T>
-static void launch_bwd(const void *dz, int dl, const void *pre, int pl, const float *pb, void *g, int gl,
-                       float *partial, TwinShape s, int act, hipStream_t st) {
-  hipLaunchKernelGGL(k_act_bwd<T>, twin_grid(s), dim3(256), 0, st, (const T *)dz, dl, (const T *)pre, pl, pb, (T *)g,
-                     gl, partial, s, act);
-}
+template <typename T, typename To> struct ActFwd {
+  using in = T;
+  using out = To;
+  static constexpr auto kernel = k_bias_act_fwd<T, To>;
+};
+template <typename T, typename To> struct ActBwd {
+  using in = T;
+  using out = To;
+  static constexpr auto kernel = k_act_bwd<T, To>;
+};
 
 }  // namespace phc
 
@@ -393,24 +407,28 @@ using namespace phc;
 
 extern "C" int phc_bias_act_fwd(const void *y, int32_t y_layout, const float *bias, void *pre, void *out,
                                 int32_t out_layout, int64_t rows, int32_t groups, int32_t cols, int32_t act,
-                                int32_t dtype, void *stream) {
+                                int32_t dtype, int32_t out_dtype, void *stream) {
   PHC_REQUIRE(rows >= 0 && groups >= 1 && cols > 0 && cols % 4 == 0, "bias_act_fwd: bad shape");
   PHC_REQUIRE(act == PHC_ACT_NONE || act == PHC_ACT_SILU, "bias_act_fwd: bad act");
-  PHC_REQUIRE(dtype == PHC_DT_F32 || dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "bias_act_fwd: bad dtype");
+  PHC_REQUIRE(valid_dtype(dtype) && valid_dtype(out_dtype) && (dtype == out_dtype || dtype == PHC_DT_F32),
+              "bias_act_fwd: bad dtype pair (%d, %d)", dtype, out_dtype);
   if (rows == 0) return PHC_OK;
   if (int rc = check_twin(y, y_layout, dtype, "bias_act_fwd y")) return rc;
   PHC_REQUIRE(pre || out, "bias_act_fwd: nothing to write");
   if (out)
-    if (int rc = check_twin(out, out_layout, dtype, "bias_act_fwd out")) return rc;
+    if (int rc = check_twin(out, out_layout, out_dtype, "bias_act_fwd out")) return rc;
   if (pre)
     if (int rc = check_twin(pre, y_layout, dtype, "bias_act_fwd pre")) return rc;
   PHC_REQUIRE(!bias || (reinterpret_cast<uintptr_t>(bias) & 15) == 0, "bias_act_fwd: misaligned bias");
-  PHC_REQUIRE(!(out && out == y && out_layout != y_layout), "bias_act_fwd: in-place output needs the input layout");
+  PHC_REQUIRE(!(out && out == y && (out_layout != y_layout || out_dtype != dtype)),
+              "bias_act_fwd: in-place output needs the input layout and type");
   const TwinShape s{rows, groups, cols};
   hipStream_t st = as_stream(stream);
-  if (dtype == PHC_DT_F32) launch_fwd<float>(y, y_layout, bias, pre, out, out_layout, s, act, st);
-  else if (dtype == PHC_DT_F16) launch_fwd<_Float16>(y, y_layout, bias, pre, out, out_layout, s, act, st);
-  else launch_fwd<__bf16>(y, y_layout, bias, pre, out, out_layout, s, act, st);
+  dispatch_twin<ActFwd>(dtype, out_dtype, [&](auto k) {
+    using K = decltype(k);
+    hipLaunchKernelGGL(K::kernel, twin_grid(s), dim3(256), 0, st, (const typename K::in *)y, y_layout, bias,
+                       (typename K::in *)pre, (typename K::out *)out, out_layout, s, act);
+  });
   return check_launch("bias_act_fwd");
 }
 
@@ -421,10 +439,12 @@ extern "C" size_t phc_act_bwd_workspace_bytes(int64_t rows, int32_t groups, int3
 
 extern "C" int phc_act_bwd(const void *grad_out, int32_t go_layout, const void *pre, int32_t pre_layout,
                            const float *pre_bias, void *grad_pre, int32_t gp_layout, float *bias_grad, int64_t rows,
-                           int32_t groups, int32_t cols, int32_t act, int32_t dtype, void *workspace, void *stream) {
+                           int32_t groups, int32_t cols, int32_t act, int32_t dtype, int32_t out_dtype,
+                           void *workspace, void *stream) {
   PHC_REQUIRE(rows >= 0 && groups >= 1 && cols > 0 && cols % 4 == 0, "act_bwd: bad shape");
   PHC_REQUIRE(act == PHC_ACT_NONE || act == PHC_ACT_SILU, "act_bwd: bad act");
-  PHC_REQUIRE(dtype == PHC_DT_F32 || dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "act_bwd: bad dtype");
+  PHC_REQUIRE(valid_dtype(dtype) && valid_dtype(out_dtype) && (dtype == out_dtype || dtype == PHC_DT_F32),
+              "act_bwd: bad dtype pair (%d, %d)", dtype, out_dtype);
   const TwinShape s{rows, groups, cols};
   hipStream_t st = as_stream(stream);
   if (rows == 0) {
@@ -435,7 +455,9 @@ extern "C" int phc_act_bwd(const void *grad_out, int32_t go_layout, const void *
   if (act == PHC_ACT_SILU)
     if (int rc = check_twin(pre, pre_layout, dtype, "act_bwd pre")) return rc;
   if (grad_pre)
-    if (int rc = check_twin(grad_pre, gp_layout, dtype, "act_bwd grad_pre")) return rc;
+    if (int rc = check_twin(grad_pre, gp_layout, out_dtype, "act_bwd grad_pre")) return rc;
+  PHC_REQUIRE(!(grad_pre && (grad_pre == grad_out || grad_pre == pre) && out_dtype != dtype),
+              "act_bwd: in-place grad needs the input type");
   PHC_REQUIRE(!(grad_pre && grad_pre == grad_out && gp_layout != go_layout),
               "act_bwd: in-place grad needs the grad_out layout");
   PHC_REQUIRE(grad_pre || bias_grad, "act_bwd: nothing to write");
@@ -447,11 +469,12 @@ extern "C" int phc_act_bwd(const void *grad_out, int32_t go_layout, const void *
     PHC_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "act_bwd: misaligned workspace");
     partial = static_cast<float *>(workspace);
   }
-  if (dtype == PHC_DT_F32)
-    launch_bwd<float>(grad_out, go_layout, pre, pre_layout, pre_bias, grad_pre, gp_layout, partial, s, act, st);
-  else if (dtype == PHC_DT_F16)
-    launch_bwd<_Float16>(grad_out, go_layout, pre, pre_layout, pre_bias, grad_pre, gp_layout, partial, s, act, st);
-  else launch_bwd<__bf16>(grad_out, go_layout, pre, pre_layout, pre_bias, grad_pre, gp_layout, partial, s, act, st);
+  dispatch_twin<ActBwd>(dtype, out_dtype, [&](auto k) {
+    using K = decltype(k);
+    hipLaunchKernelGGL(K::kernel, grid, dim3(256), 0, st, (const typename K::in *)grad_out, go_layout,
+                       (const typename K::in *)pre, pre_layout, pre_bias, (typename K::out *)grad_pre, gp_layout,
+                       partial, s, act);
+  });
   if (bias_grad) {
     const int c = groups * cols;
     hipLaunchKernelGGL(k_colsum, dim3((unsigned)((c + 63) / 64)), dim3(256), 0, st, partial, (int)grid.y, c,

@@ -9,7 +9,7 @@ from torch import nn
 
 from .discriminator_policy import DiscriminatorPolicy
 from .pufferl_policy import Linear, layer_init
-from .twin_mlp import TwinWeights, head_linear, twin_ln_silu, twin_trunks
+from .twin_mlp import TwinWeights, head_linear, twin_ln_silu, twin_ln_silu_supported, twin_trunks
 
 
 def mlp(layer_sizes, activation):
@@ -42,7 +42,7 @@ class PHCPolicy(DiscriminatorPolicy):
         if self.fused and obs.is_cuda:
             y = twin_trunks(self.obs_pointer, self._twin)  # [2, M, hidden]: actor, critic
             h = self._head
-            if self.fused_ln:
+            if self.fused_ln and twin_ln_silu_supported(y.shape[2]):
                 z = twin_ln_silu(y, self.actor_mlp[h], self.critic_mlp[h])  # LayerNorm + SiLU of both trunks
             else:
                 z = [self.critic_mlp[h + 1](m[h](y[i])) if i else self.actor_mlp[h + 1](m[h](y[i]))

@@ -10,9 +10,15 @@ stacked weights are a cache in the GEMM dtype, rebuilt when a parameter's versio
 (i.e. after each optimizer step).
 
 GEMM arithmetic follows the autocast context: fp32 storage with torch's "high" matmul
-precision (hipBLASLt xf32) outside autocast, fp16 / bf16 operands (fp32 accumulate, fp32
-weight gradients) inside.  The reference's unfused path (nn.Sequential of Linear/SiLU) is what
-the tests compare against.
+precision (hipBLASLt xf32) outside autocast, fp16 / bf16 operands inside.  In the half-precision
+modes only the GEMM OPERANDS are rounded: every GEMM accumulates and writes fp32, the epilogues
+compute in fp32 from those outputs and round once, when they write the next GEMM's operand
+(activations forward, activation gradients backward), and bias / weight gradients are fp32.
+With fp16 operands this is TF32's arithmetic (an 11-bit significand per operand, fp32 products
+and sums; the reference sets torch.set_float32_matmul_precision("high"),
+clean_pufferl/core.py:38) with fp16's exponent range, which dynamic loss scaling covers for the
+gradients.  The reference's unfused path (nn.Sequential of Linear/SiLU) is what the tests
+compare against.
 """
 
 import torch
@@ -37,7 +43,7 @@ def _bmm(a, b, out_fp32=False):
             if out_dt is None:
                 torch.mm(a[g], b[g], out=out[g])
             else:
-                out[g] = torch.mm(a[g], b[g], out_dtype=out_dt)
+                torch.mm(a[g], b[g], out_dtype=out_dt, out=out[g])
         return out
     if out_dt is not None:
         return torch.bmm(a, b, out_dtype=out_dt)
@@ -128,17 +134,18 @@ class TwinTrunkFn(torch.autograd.Function):
             M = x.shape[0]
             xc = x.to(dt).contiguous()
             n1 = W[0].shape[0] // 2
-            y = torch.mm(xc, W[0].t())  # [M, 2*n1], SPLIT
-            z = torch.empty((2, M, n1), dtype=dt, device=x.device)
+            # GEMM outputs are fp32 in every mode (see the module docstring)
+            y = torch.mm(xc, W[0].t()) if dt == torch.float32 else torch.mm(xc, W[0].t(), out_dtype=torch.float32)
+            z = torch.empty((2, M, n1), dtype=dt, device=x.device)  # [M, 2*n1] SPLIT -> GROUPED
             # the raw GEMM output y is kept for backward (pre-activation = y + b recomputed there)
             N.bias_act_fwd(y, N.SPLIT, B[0], None, z, N.GROUPED, M, 2, n1, N.ACT_SILU)
             pres, zs = [y], [z]
             L = len(W)
             for l in range(1, L):
                 n = W[l].shape[1]
-                y = _bmm(zs[-1], W[l].transpose(1, 2))  # [2, M, n]
+                y = _bmm(zs[-1], W[l].transpose(1, 2), True)  # [2, M, n] fp32
                 if l < L - 1:
-                    z = torch.empty_like(y)
+                    z = torch.empty(y.shape, dtype=dt, device=y.device)
                     N.bias_act_fwd(y, N.GROUPED, B[l], None, z, N.GROUPED, M, 2, n, N.ACT_SILU)
                     pres.append(y)
                     zs.append(z)
@@ -159,22 +166,28 @@ class TwinTrunkFn(torch.autograd.Function):
         M = xc.shape[0]
         grads = [None] * (2 * L)  # (dW, db) per layer, stacked over the two trunks
         with torch.autocast("cuda", enabled=False):
-            g = gy.to(dt).contiguous()
-            n = g.shape[2]
-            db = torch.empty(2 * n, dtype=torch.float32, device=g.device)
-            N.act_bwd(g, N.GROUPED, None, N.GROUPED, None, N.GROUPED, db, M, 2, n, N.ACT_NONE)
+            gy = gy.float().contiguous()
+            n = gy.shape[2]
+            db = torch.empty(2 * n, dtype=torch.float32, device=gy.device)
+            if dt == torch.float32:
+                g = gy
+                N.act_bwd(g, N.GROUPED, None, N.GROUPED, None, N.GROUPED, db, M, 2, n, N.ACT_NONE)
+            else:  # the fp32 gradient rounded once into the next GEMMs' operand; bias grad from fp32
+                g = torch.empty(gy.shape, dtype=dt, device=gy.device)
+                N.act_bwd(gy, N.GROUPED, None, N.GROUPED, g, N.GROUPED, db, M, 2, n, N.ACT_NONE)
             for l in range(L - 1, 0, -1):
                 dW = _weight_grad(g, zs[l - 1])  # [2, n_out, n_in] fp32
                 grads[2 * l], grads[2 * l + 1] = dW, db
-                dz = _bmm(g, W[l])  # [2, M, n_in]
+                dz = _bmm(g, W[l], True)  # [2, M, n_in] fp32
                 n = dz.shape[2]
                 db = torch.empty(2 * n, dtype=torch.float32, device=g.device)
                 if l > 1:
-                    N.act_bwd(dz, N.GROUPED, pres[l - 1], N.GROUPED, dz, N.GROUPED, db, M, 2, n, N.ACT_SILU,
+                    g = dz if dt == torch.float32 else torch.empty(dz.shape, dtype=dt, device=dz.device)
+                    N.act_bwd(dz, N.GROUPED, pres[l - 1], N.GROUPED, g, N.GROUPED, db, M, 2, n, N.ACT_SILU,
                               pre_bias=B[l - 1])
-                    g = dz
                 else:
-                    g1 = pres[0]  # SPLIT [M, 2n]: the layer-1 GEMM output buffer is reused for its grad
+                    # SPLIT [M, 2n]; fp32: the layer-1 GEMM output buffer is reused for its grad
+                    g1 = pres[0] if dt == torch.float32 else torch.empty(pres[0].shape, dtype=dt, device=dz.device)
                     N.act_bwd(dz, N.GROUPED, pres[0], N.SPLIT, g1, N.SPLIT, db, M, 2, n, N.ACT_SILU, pre_bias=B[0])
                     grads[0] = _weight_grad(g1[None], xc[None])[0]  # [2n, K]
                     grads[1] = db
@@ -259,6 +272,11 @@ class TwinLNSiLUFn(torch.autograd.Function):
         dy, dg, db = N.ln_silu_bwd(y, gamma, beta, mr, dz.float().contiguous())
         n = y.shape[2]
         return dy, dg[:n], db[:n], dg[n:], db[n:], None
+
+
+def twin_ln_silu_supported(width):
+    """phc_ln_silu_* handle row widths that are multiples of 256 up to 1024 (the reference's 512)."""
+    return width % 256 == 0 and width <= 1024
 
 
 def twin_ln_silu(y, ln_a, ln_c):

@@ -73,6 +73,31 @@ def test_bias_act_half_types(dtype):
     torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_bias_act_f32_to_half(dtype):
+    """fp32 GEMM output -> half-precision operand of the next GEMM: fp32 math, one rounding on the
+    write; the bias gradient sums the fp32 values (before that rounding)."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    M, G, C = 200, 2, 512
+    y = torch.randn((M, G * C), device=DEV, generator=g) * 2
+    b = torch.randn(G * C, device=DEV, generator=g)
+    out = torch.empty((G, M, C), dtype=dtype, device=DEV)
+    N.bias_act_fwd(y, N.SPLIT, b, None, out, N.GROUPED, M, G, C, N.ACT_SILU)
+    ref = torch.nn.functional.silu(y + b).view(M, G, C).permute(1, 0, 2)
+    ulp = 2.0 ** -10 if dtype == torch.float16 else 2.0 ** -7
+    torch.testing.assert_close(out.float(), ref, atol=1e-6, rtol=ulp)  # one rounding of the fp32 value
+    dz = torch.randn((G, M, C), device=DEV, generator=g)
+    gp = torch.empty((M, G * C), dtype=dtype, device=DEV)
+    db = torch.empty(G * C, device=DEV)
+    N.act_bwd(dz, N.GROUPED, y, N.SPLIT, gp, N.SPLIT, db, M, G, C, N.ACT_SILU, pre_bias=b)
+    p = (y + b).requires_grad_(True)
+    torch.nn.functional.silu(p).backward(dz.permute(1, 0, 2).reshape(M, G * C))
+    torch.testing.assert_close(gp.float(), p.grad, atol=1e-6, rtol=ulp)
+    torch.testing.assert_close(db, p.grad.sum(0), atol=1e-4, rtol=1e-5)
+
+
 class _Env:
     def __init__(self):
         from puffer_phc_amd.envs.humanoid_phc import Box
@@ -96,15 +121,15 @@ def _policy():
     return pol
 
 
-def _run(pol, obs, act, fused, precision):
+def _run(pol, obs, act, fused, precision, loss_scale=1.0):
     pol.policy.fused = fused
     pol.zero_grad(set_to_none=True)
     ctx = torch.autocast("cuda", dtype=precision) if precision is not None else torch.autocast("cuda", enabled=False)
     with ctx:
         _, logp, _, value = pol(obs, action=act)
     loss = logp.sum() * 1e-3 + (value.float() ** 2).sum()
-    loss.backward()
-    grads = {n: p.grad.detach().clone() for n, p in pol.named_parameters() if p.grad is not None}
+    (loss * loss_scale).backward()  # fp16 training scales the loss (GradScaler) the same way
+    grads = {n: p.grad.detach() / loss_scale for n, p in pol.named_parameters() if p.grad is not None}
     return logp.detach(), value.detach().float(), grads
 
 
@@ -170,3 +195,61 @@ def test_ln_silu_kernels_vs_torch(dtype):
     torch.testing.assert_close(dy.float(), yr.grad, atol=tol, rtol=tol)
     torch.testing.assert_close(dg, gr.grad.view(-1), atol=1e-3, rtol=1e-4)
     torch.testing.assert_close(db, br.grad.view(-1), atol=1e-3, rtol=1e-4)
+
+
+class _TF32Linear(torch.autograd.Function):
+    """nn.Linear under TF32 (the reference's matmul precision "high" on its GPUs): every GEMM
+    operand rounded to a 10-bit mantissa, exact fp32 products and sums, forward and backward."""
+
+    @staticmethod
+    def _r(t):
+        i = t.contiguous().view(torch.int32)
+        return ((i + 0x1000) & ~0x1FFF).view(torch.float32)  # round-to-nearest on the 13 dropped bits
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return _TF32Linear._r(x) @ _TF32Linear._r(w).t() + b
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        r = _TF32Linear._r
+        gx = r(gy.reshape(-1, gy.shape[-1])) @ r(w)
+        gw = r(gy.reshape(-1, gy.shape[-1])).t() @ r(x.reshape(-1, x.shape[-1]))
+        return gx.view(x.shape), gw, gy.reshape(-1, gy.shape[-1]).sum(0)
+
+
+def test_fp16_operands_match_tf32_error():
+    """The fp16 mode (fp16 GEMM operands, fp32 GEMM outputs and epilogues) is as precise as the
+    reference's TF32 GEMMs: its error against exact fp32 stays within 1.5x the error of an exact
+    TF32 emulation of the unfused policy (values, log-probs and every parameter gradient; both
+    are a few 1e-4 here, bf16 operands are ~8x worse).  The backward runs on a loss scaled by
+    2^12, as fp16 training does (GradScaler), so the deepest activation gradients stay fp16
+    normals: fp16's exponent range is the one difference from TF32."""
+    pol = _policy()
+    g = torch.Generator(device=DEV).manual_seed(2)
+    obs = torch.randn((1000, 934), device=DEV, generator=g) * 2
+    act = torch.randn((1000, 69), device=DEV, generator=g) * 0.3
+    from puffer_phc_amd.policies.pufferl_policy import Linear
+
+    prev = torch.get_float32_matmul_precision()
+    orig = Linear.forward
+    try:
+        torch.set_float32_matmul_precision("highest")
+        ref = _run(pol, obs, act, fused=False, precision=None)
+        Linear.forward = lambda self, x: _TF32Linear.apply(x, self.weight, self.bias)
+        tf32 = _run(pol, obs, act, fused=False, precision=None)
+        Linear.forward = orig
+        f16 = _run(pol, obs, act, fused=True, precision=torch.float16, loss_scale=2.0 ** 12)
+    finally:
+        Linear.forward = orig
+        torch.set_float32_matmul_precision(prev)
+    assert rel(tf32[1], ref[1]) > 0, "the TF32 emulation must be in effect"
+    errs = {}
+    for name, i in (("logp", 0), ("value", 1)):
+        errs[name] = (rel(f16[i], ref[i]), rel(tf32[i], ref[i]))
+    for k in ref[2]:
+        errs[k] = (rel(f16[2][k], ref[2][k]), rel(tf32[2][k], ref[2][k]))
+    bad = {k: v for k, v in errs.items() if v[0] > 1.5 * v[1] + 1e-7}
+    assert not bad, bad
