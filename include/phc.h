@@ -229,6 +229,38 @@ int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, 
                 int32_t groups, int32_t cols, int32_t act, int32_t dtype, int32_t out_dtype, void *workspace,
                 void *stream);
 
+/* R19/R21: the twin trunks' GEMMs with their epilogues fused (phc_gemm.hip).  For b < batch:
+ * C[b] = A[b] · B[b]^T with A[b] [m, k] (lda) and B[b] [n, k] (ldb) row-major f16 / bf16 (dtype),
+ * fp32 accumulation; k % 64 == 0 (zero-pad), lda / ldb multiples of 8, 16-byte aligned operands.
+ * Output column j of batch b is logical column c = b * n + j of a twin tensor of twin_groups x
+ * twin_cols columns (out_layout / aux_layout SPLIT or GROUPED, as phc_bias_act_fwd).  Epilogues
+ * (what nn.Linear + nn.SiLU and their autograd backward compute, policies/phc_policy.py:10-61):
+ *   STORE     out = C
+ *   BIAS      out = C + bias[c]
+ *   BIAS_SILU aux = C + bias[c] (fp32, nullable), out = silu(C + bias[c])
+ *   SILU_GRAD out = C * silu'(aux + bias[c]) (aux fp32; bias nullable, e.g. when aux is the
+ *             pre-activation BIAS_SILU wrote, bias included), and
+ *             bias_grad[c] = column sums of that product in fp32 (nullable; needs
+ *             phc_twin_gemm_workspace_bytes of workspace)
+ * out is fp32 or dtype (out_dtype). */
+enum { PHC_EPI_STORE = 0, PHC_EPI_BIAS = 1, PHC_EPI_BIAS_SILU = 2, PHC_EPI_SILU_GRAD = 3 };
+typedef struct phc_gemm_desc {
+  const void *a;
+  const void *b;
+  int64_t a_batch_stride, b_batch_stride; /* elements */
+  int64_t lda, ldb;                       /* elements */
+  int64_t m;
+  int32_t n, k, batch, dtype;
+  int32_t epilogue, out_dtype;
+  const float *bias; /* [batch * n] */
+  void *aux;         /* fp32 pre-activation (BIAS_SILU: written, SILU_GRAD: read) */
+  void *out;
+  int32_t aux_layout, out_layout;
+  int32_t twin_groups, twin_cols;
+} phc_gemm_desc;
+size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_t n);
+int phc_twin_gemm(const phc_gemm_desc *desc, float *bias_grad, void *workspace, void *stream);
+
 /* R19/R21: the twin trunks' LayerNorm(cols) + SiLU (policies/phc_policy.py:16-30) over a GROUPED
  * [groups, rows, cols] tensor y (dtype) with per-group gamma/beta [groups*cols] fp32:
  * z = silu((y - mean) * rstd * gamma + beta) in fp32, mean_rstd [groups*rows, 2] saved.

@@ -80,6 +80,18 @@ class AmpBuffersC(ctypes.Structure):
     _fields_ = [("amp_obs", c_vp), ("amp_obs_demo", c_vp), ("num_steps", ctypes.c_int32)]
 
 
+class GemmDescC(ctypes.Structure):
+    _fields_ = [("a", c_vp), ("b", c_vp), ("a_batch_stride", c_i64), ("b_batch_stride", c_i64), ("lda", c_i64),
+                ("ldb", c_i64), ("m", c_i64), ("n", ctypes.c_int32), ("k", ctypes.c_int32),
+                ("batch", ctypes.c_int32), ("dtype", ctypes.c_int32), ("epilogue", ctypes.c_int32),
+                ("out_dtype", ctypes.c_int32), ("bias", c_vp), ("aux", c_vp), ("out", c_vp),
+                ("aux_layout", ctypes.c_int32), ("out_layout", ctypes.c_int32), ("twin_groups", ctypes.c_int32),
+                ("twin_cols", ctypes.c_int32)]
+
+
+EPI_STORE, EPI_BIAS, EPI_BIAS_SILU, EPI_SILU_GRAD = 0, 1, 2, 3
+
+
 _EXPORTS = {
     "phc_version": (ctypes.c_int, []),
     "phc_last_error": (ctypes.c_char_p, []),
@@ -109,6 +121,8 @@ _EXPORTS = {
     "phc_ln_silu_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
     "phc_ln_silu_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
                                         ctypes.c_int32, ctypes.c_int32, c_vp, c_vp]),
+    "phc_twin_gemm_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
+    "phc_twin_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDescC), c_vp, c_vp, c_vp]),
     "phc_ppo_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_ppo_loss_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
                                          ctypes.POINTER(PpoCoefsC), c_vp, c_vp, c_vp, c_vp]),
@@ -400,6 +414,51 @@ def ln_silu_bwd(y, gamma, beta, mean_rstd, dz):
                                  M, G, N_, DTYPE_CODE[dt], ws.data_ptr(), _stream()),
            "phc_ln_silu_bwd")
     return dy, dg, db
+
+
+def _operand(t, name):
+    """(pointer, batch stride, leading dimension, batch, rows, cols) of a [rows, k] or
+    [batch, rows, k] half-precision GEMM operand with unit column stride."""
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype not in (torch.float16, torch.bfloat16):
+        raise ValueError(f"twin_gemm {name}: expected a f16 / bf16 device tensor")
+    if t.dim() == 2:
+        t3, bs = t[None], 0
+    elif t.dim() == 3:
+        t3, bs = t, t.stride(0)
+    else:
+        raise ValueError(f"twin_gemm {name}: expected 2-D or 3-D, got {tuple(t.shape)}")
+    if t3.stride(2) != 1:
+        raise ValueError(f"twin_gemm {name}: columns must be contiguous")
+    return t3.data_ptr(), bs, t3.stride(1), t3.shape[0], t3.shape[1], t3.shape[2]
+
+
+def twin_gemm(a, b, epilogue, out, twin, bias=None, aux=None, aux_layout=GROUPED, out_layout=GROUPED,
+              bias_grad=None):
+    """out = epilogue(a[b] @ b[b]^T) for a [batch?, m, k], b [batch?, n, k] (phc_twin_gemm).
+    twin = (groups, cols) of the output / aux tensors' logical columns."""
+    pa, abs_, lda, ba, m, k = _operand(a, "a")
+    pb, bbs, ldb, bb, n, kb = _operand(b, "b")
+    if kb != k or (ba != bb and ba != 1 and bb != 1):
+        raise ValueError(f"twin_gemm: operand shapes {tuple(a.shape)} x {tuple(b.shape)}^T do not match")
+    if a.dtype != b.dtype:
+        raise ValueError("twin_gemm: operands must share a dtype")
+    batch = max(ba, bb)
+    G, C = twin
+    if out.dtype not in (torch.float32, a.dtype) or not out.is_contiguous() or out.numel() != m * batch * n:
+        raise ValueError("twin_gemm: out must be contiguous f32 / operand-dtype with m * batch * n elements")
+    if aux is not None and (aux.dtype != torch.float32 or not aux.is_contiguous() or aux.numel() != out.numel()):
+        raise ValueError("twin_gemm: aux must be a contiguous f32 tensor shaped like out")
+    d = GemmDescC(pa, pb, abs_, bbs, lda, ldb, m, n, k, batch, DTYPE_CODE[a.dtype], epilogue, DTYPE_CODE[out.dtype],
+                  _ptr(bias, torch.float32, (batch * n,), "bias", nullable=True),
+                  aux.data_ptr() if aux is not None else None, out.data_ptr(), aux_layout, out_layout, G, C)
+    ws = None
+    if bias_grad is not None:
+        _ptr(bias_grad, torch.float32, (batch * n,), "bias_grad")
+        ws = _workspace(lib().phc_twin_gemm_workspace_bytes(m, batch, n), a.device).data_ptr()
+    _check(lib().phc_twin_gemm(ctypes.byref(d), bias_grad.data_ptr() if bias_grad is not None else None, ws,
+                               _stream()),
+           "phc_twin_gemm")
+    return out
 
 
 _WS = {}

@@ -20,6 +20,7 @@ import torch
 
 from .. import _native
 from .. import distributed as D
+from ..policies.twin_mlp import refresh_twin
 from .ppo_loss import ppo_objective
 from .structs import Experience, LossComponents, Profile, StatsData, TrainComponents, TrainInfo, Utilization
 from .utils import count_params, save_checkpoint, seed_everything
@@ -136,7 +137,7 @@ class RolloutStep:
 
     def run(self, use_graph=True):
         if self.twin is not None:
-            self.twin.get(_compute_dtype(self.cfg))  # in-place refresh after optimizer steps
+            refresh_twin(self.twin, _compute_dtype(self.cfg))  # in-place refresh after optimizer steps
         if self.graph is not None:
             self.graph.replay()
         elif not use_graph or self.eager_steps == 0:

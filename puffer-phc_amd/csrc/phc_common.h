@@ -199,4 +199,33 @@ __device__ __forceinline__ void write_obs_body(float *__restrict__ o, int b, con
   write_task_obs(o, b, s, root_p, hinv, hrot, ref);
 }
 
+// column sums of the [rows, cols] fp32 partials (bias gradients; a template so every
+// translation unit that launches it carries its own copy): 16 lanes x float4 = 64 columns per block, 16 row
+// slices reduced through LDS
+template <int = 0>
+__global__ __launch_bounds__(256) void k_colsum(const float *__restrict__ partial, int rows, int cols,
+                                                float *__restrict__ out) {
+  __shared__ float4 red[16][16];
+  const int cl = threadIdx.x & 15, rs = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + cl * 4;
+  float4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (c < cols) {
+#pragma unroll 4
+    for (int r = rs; r < rows; r += 16) {
+      const float4 v = *reinterpret_cast<const float4 *>(partial + (int64_t)r * cols + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[rs][cl] = acc;
+  __syncthreads();
+  if (rs == 0 && c < cols) {
+    float4 t = red[0][cl];
+    for (int k = 1; k < 16; ++k) {
+      const float4 v = red[k][cl];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    *reinterpret_cast<float4 *>(out + c) = t;
+  }
+}
+
 }  // namespace phc

@@ -1,0 +1,467 @@
+// phc_gemm.hip — half-precision MFMA GEMM with the twin-trunk epilogues fused (R19/R21).
+//
+// C[b] = A[b] · B[b]^T for b < batch, A [m, k] and B [n, k] row-major f16 / bf16 (both operands
+// k-contiguous: the forward's X · W^T, and the input-gradient G · W with W pre-transposed),
+// fp32 accumulation on v_mfma_f32_16x16x32_{f16,bf16}.  What the reference does between its GEMMs
+// (nn.Linear bias + nn.SiLU forward, their backward and the bias gradient; policies/phc_policy.py:
+// 10-61 under torch autograd) runs on the accumulator tile before it leaves the CU:
+//   PHC_EPI_STORE     : out = acc
+//   PHC_EPI_BIAS      : out = acc + bias
+//   PHC_EPI_BIAS_SILU : pre = acc + bias (aux, fp32, nullable), out = silu(pre)
+//   PHC_EPI_SILU_GRAD : out = acc * silu'(aux + bias) (bias nullable: aux is then the whole
+//                       pre-activation, as BIAS_SILU writes it); bias_grad = column sums of out
+// so no fp32 GEMM output makes an HBM round trip through a separate elementwise kernel.
+//
+// Tiling: 128 x 128 output tile per 256-thread block (4 waves as 2 x 2, 64 x 64 per wave =
+// 4 x 4 MFMA blocks), K in steps of 64.  Operand tiles move global -> LDS by global_load_lds
+// (16 B per lane, no VGPR staging) into two LDS buffers: tile t+1 streams in while the waves
+// compute on tile t, one barrier per K-step.  The LDS image of a tile is [row][8 chunks of 16 B]
+// with chunk c of row r stored at slot c ^ (r & 7) (the source address is pre-swizzled, the
+// DMA's LDS side stays lane-linear), so the 16 rows one ds_read_b128 touches hit 8 distinct
+// 16-B bank slots.  Blocks are renumbered XCD-major (bijective remap) so the blocks sharing an
+// XCD's L2 walk the column tiles of the same A row panel.  m and n may be ragged (loads clamp
+// to the last row, stores are masked); k must be a multiple of 64.
+#include "phc_common.h"
+
+#include <cstdlib>
+#include <type_traits>
+
+namespace phc {
+
+constexpr int kGBK = 64;
+using f4 = __attribute__((ext_vector_type(4))) float;
+using h8 = __attribute__((ext_vector_type(8))) _Float16;
+using b8 = __attribute__((ext_vector_type(8))) __bf16;
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct GemmArgs {
+  const char *a, *b;
+  int64_t a_bs, b_bs, lda, ldb;  // element strides
+  int64_t m;
+  int n, k, batch;
+  const float *bias;
+  void *aux;
+  int aux_layout;
+  void *out;
+  int out_layout;
+  int tg, tc;  // twin geometry of out / aux: logical column b * n + j -> group / column
+  float *partial;
+  int tiles_m, tiles_n;
+  int discard;
+};
+
+// element offset of (row, logical column c) in a twin tensor of tg groups x tc columns
+__device__ __forceinline__ int64_t gemm_twin_off(const GemmArgs &g, int layout, int64_t row, int c) {
+  const int grp = c / g.tc, j = c - grp * g.tc;
+  if (layout == PHC_LAYOUT_SPLIT) return row * (int64_t)(g.tg * g.tc) + c;
+  return ((int64_t)grp * g.m + row) * g.tc + j;
+}
+
+__device__ __forceinline__ float gemm_silu(float a) { return a / (1.0f + expf(-a)); }
+
+template <typename OutT> __device__ __forceinline__ void gemm_store(void *p, int64_t off, float v) {
+  static_cast<OutT *>(p)[off] = (OutT)v;
+}
+
+template <typename OutT> __device__ __forceinline__ void gemm_store4(void *p, int64_t off, const float v[4]) {
+  if constexpr (sizeof(OutT) == 4) {
+    *reinterpret_cast<float4 *>(static_cast<float *>(p) + off) = float4{v[0], v[1], v[2], v[3]};
+  } else {
+    OutT h[4] = {(OutT)v[0], (OutT)v[1], (OutT)v[2], (OutT)v[3]};
+    uint2 raw;
+    __builtin_memcpy(&raw, h, sizeof(raw));
+    *reinterpret_cast<uint2 *>(static_cast<OutT *>(p) + off) = raw;
+  }
+}
+
+// issue the global_load_lds of one R-row x 64-column operand tile (R / 8 wave-instructions over
+// the block's W waves)
+template <int R, int W>
+__device__ __forceinline__ void stage_tile(const char *base, int64_t ld, int64_t row0, int64_t rows, int k0,
+                                           char *lds_tile, int wave, int lane) {
+  static_assert((R / 8) % W == 0, "tile rows must split evenly over the waves");
+#pragma unroll
+  for (int i = 0; i < R / 8 / W; ++i) {
+    const int q0 = (i * W + wave) * 64;  // first 16-B chunk this wave-instruction fills
+    const int q = q0 + lane;
+    const int r = q >> 3, c = q & 7;
+    int64_t gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    const char *src = base + (gr * ld + k0 + ((c ^ (r & 7)) << 3)) * 2;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (lds_void *)(lds_tile + q0 * 16), 16, 0, 0);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void read_frag(const char *lds_tile, int row, int chunk, T &f) {
+  f = *reinterpret_cast<const T *>(lds_tile + row * 128 + ((chunk ^ (row & 7)) << 4));
+}
+
+// Tile geometry: BM x BN block tile, WGM x WGN waves, each owning a TM x TN = (BM / WGM) x
+// (BN / WGN) sub-tile of (TM / 16) x (TN / 16) MFMA blocks; STAGES operand buffers in LDS.
+template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_> struct Tile {
+  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, STAGES = STAGES_;
+  static constexpr int kWaves = WGM * WGN, kThreads = kWaves * 64;
+  static constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
+  static constexpr int kStageBytes = (BM + BN) * kGBK * 2;
+  static constexpr int kLoadsPerTile = (BM + BN) / 8 / kWaves;  // glds per thread per K-step
+  static constexpr int kOpBytes = STAGES * kStageBytes;
+  // epilogue: wave rows per pass through the fp32 LDS image (reusing the operand buffers)
+  static constexpr int kEpWaveRows = (kOpBytes / (TM * BN * 4)) >= WGM ? WGM : (kOpBytes / (TM * BN * 4));
+  static constexpr int kEpRows = kEpWaveRows * TM;
+  static constexpr int kLdsBytes = kOpBytes;
+  static_assert(kEpWaveRows >= 1 && WGM % kEpWaveRows == 0, "epilogue image must fit the operand buffers");
+  static_assert(MI >= 1 && NI >= 1 && TM % 16 == 0 && TN % 16 == 0, "bad wave tile");
+};
+
+template <typename T, typename OutT, int EPI, typename TL>
+__global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
+  constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
+  using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][A BM rows | B BN rows]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / TL::WGN, wn = wave % TL::WGN;
+
+  // XCD-major renumbering (bijective for any grid size), then n fastest within an A panel
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tn = wg % g.tiles_n;
+  const int tm = (wg / g.tiles_n) % g.tiles_m;
+  const int bt = wg / (g.tiles_n * g.tiles_m);
+  const int64_t m0 = (int64_t)tm * BM;
+  const int n0 = tn * BN;
+  const char *A = g.a + bt * g.a_bs * 2;
+  const char *B = g.b + bt * g.b_bs * 2;
+
+  f4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  auto stage = [&](int kt, int buf) {
+    char *st = smem + buf * TL::kStageBytes;
+    stage_tile<BM, TL::kWaves>(A, g.lda, m0, g.m, kt * kGBK, st, wave, lane);
+    stage_tile<BN, TL::kWaves>(B, g.ldb, n0, g.n, kt * kGBK, st + BM * 128, wave, lane);
+  };
+  // one K-step (64) = 2 MFMA sub-steps of 32; within it the (MI / 2) pairs of A fragments
+  // are walked as groups of 2 x NI MFMAs, the fragments of group q + 1 read from LDS while the
+  // MFMAs of group q run (two fragment register sets; B fragments re-read per sub-step)
+  auto compute = [&](int buf) {
+    const char *ta = smem + buf * TL::kStageBytes;
+    const char *tb = ta + BM * 128;
+    constexpr int GP = MI / 2, NG = 2 * GP;
+    static_assert(MI % 2 == 0, "A fragments are walked in pairs");
+    V8 fa[2][2], fb[2][NI];
+    auto load_b = [&](V8 *f, int s) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) read_frag(tb, wn * TL::TN + j * 16 + (lane & 15), s * 4 + (lane >> 4), f[j]);
+    };
+    auto load_a = [&](V8 *f, int s, int p) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+        read_frag(ta, wm * TL::TM + (2 * p + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), f[ii]);
+    };
+    load_b(fb[0], 0);
+    load_a(fa[0], 0, 0);
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const int s = q / GP, p = q % GP;
+      if (q + 1 < NG) {
+        const int s1 = (q + 1) / GP, p1 = (q + 1) % GP;
+        if (s1 != s) load_b(fb[s1 & 1], s1);
+        load_a(fa[(q + 1) & 1], s1, p1);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          f4 &c = acc[2 * p + ii][j];
+          if constexpr (std::is_same<T, _Float16>::value)
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
+          else
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
+        }
+    }
+  };
+
+  const int kt_n = g.k / kGBK;
+  if constexpr (TL::STAGES == 2) {
+    stage(0, 0);
+    for (int kt = 0; kt < kt_n; ++kt) {
+      __syncthreads();  // tile kt landed (vmcnt(0) + barrier); buffer (kt+1)&1 is no longer read
+      if (kt + 1 < kt_n) stage(kt + 1, (kt + 1) & 1);
+      compute(kt & 1);
+    }
+  } else {
+    static_assert(TL::STAGES == 3, "2 or 3 stages");
+    stage(0, 0);
+    if (kt_n > 1) stage(1, 1);
+    int buf = 0;
+    for (int kt = 0; kt < kt_n; ++kt) {
+      // this thread's part of tile kt has landed (tile kt + 1 may stay in flight); after the
+      // barrier every thread's part has, and every wave is done with tile kt - 1's buffer
+      if (kt + 1 < kt_n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TL::kLoadsPerTile) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + 2 < kt_n) stage(kt + 2, buf == 0 ? 2 : buf - 1);
+      compute(buf);
+      buf = buf == 2 ? 0 : buf + 1;
+    }
+  }
+
+  if (g.discard) {  // measurement aid: main loop only (keeps the accumulators alive)
+    float t = 0.0f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1234.5f) static_cast<float *>(g.out)[0] = t;
+    return;
+  }
+  // ---- epilogue.  The accumulators (lane: column lane & 15, rows 4 * (lane >> 4) + e of each
+  // 16 x 16 block) go through LDS as an fp32 [rows][BN] image, 16-column groups XOR-swizzled by
+  // (row >> 2) & 3 so both the scattered writes and the row reads are conflict-free (in passes of
+  // kEpRows rows when the whole tile does not fit); then each thread owns 4 consecutive columns
+  // of every kRowGroups-th row: 16-B loads / stores, BN * 4 contiguous bytes per row.
+  constexpr int kColThreads = BN / 4, kRowGroups = TL::kThreads / kColThreads;
+  float *ep = reinterpret_cast<float *>(smem);
+  const int c4 = (tid % kColThreads) * 4, rg = tid / kColThreads;
+  const int gcol = n0 + c4;
+  const bool vec = gcol + 3 < g.n && g.tc % 4 == 0;
+  float bias4[4] = {0.0f, 0.0f, 0.0f, 0.0f}, csum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (EPI != PHC_EPI_STORE && g.bias) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (gcol + q < g.n) bias4[q] = g.bias[bt * g.n + gcol + q];
+  }
+#pragma unroll 1
+  for (int pass = 0; pass < TL::WGM / TL::kEpWaveRows; ++pass) {
+    __syncthreads();  // operand tiles / the previous pass's image are no longer read
+    if (wm / TL::kEpWaveRows == pass) {
+      const int rbase = (wm % TL::kEpWaveRows) * TL::TM;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = rbase + i * 16 + 4 * (lane >> 4) + e;
+            const int c = wn * TL::TN + j * 16 + (lane & 15);
+            ep[r * BN + (c ^ (((r >> 2) & 3) << 4))] = acc[i][j][e];
+          }
+    }
+    __syncthreads();
+    for (int it = 0; it < TL::kEpRows / kRowGroups; ++it) {
+      const int r = rg + kRowGroups * it;
+      const int64_t row = m0 + (int64_t)pass * TL::kEpRows + r;
+      if (row >= g.m) break;
+      const float4 t = *reinterpret_cast<const float4 *>(&ep[r * BN + (c4 ^ (((r >> 2) & 3) << 4))]);
+      float v[4] = {t.x, t.y, t.z, t.w};
+      float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      const int lc = bt * g.n + gcol;
+      if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+        const float *aux = static_cast<const float *>(g.aux);
+        if (vec) {
+          const float4 av = *reinterpret_cast<const float4 *>(aux + gemm_twin_off(g, g.aux_layout, row, lc));
+          a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
+        } else {
+          for (int q = 0; q < 4; ++q)
+            if (gcol + q < g.n) a[q] = aux[gemm_twin_off(g, g.aux_layout, row, lc + q)];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU) {
+          v[q] += bias4[q];
+          a[q] = v[q];
+          if constexpr (EPI == PHC_EPI_BIAS_SILU) v[q] = gemm_silu(v[q]);
+        } else if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+          const float x = a[q] + bias4[q];
+          const float sg = 1.0f / (1.0f + expf(-x));
+          v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
+          csum[q] += gcol + q < g.n ? v[q] : 0.0f;
+        }
+      }
+      if (vec) {
+        if constexpr (EPI == PHC_EPI_BIAS_SILU) {
+          if (g.aux)
+            *reinterpret_cast<float4 *>(static_cast<float *>(g.aux) + gemm_twin_off(g, g.aux_layout, row, lc)) =
+                float4{a[0], a[1], a[2], a[3]};
+        }
+        gemm_store4<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, lc), v);
+      } else {
+        for (int q = 0; q < 4; ++q) {
+          if (gcol + q >= g.n) break;
+          if constexpr (EPI == PHC_EPI_BIAS_SILU) {
+            if (g.aux) static_cast<float *>(g.aux)[gemm_twin_off(g, g.aux_layout, row, lc + q)] = a[q];
+          }
+          gemm_store<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, lc + q), v[q]);
+        }
+      }
+    }
+  }
+  if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+    if (!g.partial) return;
+    // column sums over the tile's rows: row groups inside a wave by shuffle, the waves by LDS
+    if constexpr (kColThreads == 32) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) csum[q] += __shfl_xor(csum[q], 32, 64);
+    }
+    constexpr int kWaveRows = kColThreads >= 64 ? 1 : 64 / kColThreads;  // rows one wave spans
+    __syncthreads();  // the epilogue image is no longer read
+    if (lane < 64 / kWaveRows) {
+      const int wc = (kColThreads >= 64 ? (tid % kColThreads) : lane) * 4;
+      const int slot = kColThreads >= 64 ? (tid / kColThreads) : wave;
+      *reinterpret_cast<float4 *>(&ep[slot * BN + wc]) = float4{csum[0], csum[1], csum[2], csum[3]};
+    }
+    __syncthreads();
+    constexpr int kSlots = kColThreads >= 64 ? kRowGroups : TL::kWaves;
+    if (tid < kColThreads) {
+      float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int w = 0; w < kSlots; ++w)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] += ep[w * BN + c4 + q];
+      float *pr = g.partial + (int64_t)tm * (g.batch * g.n) + bt * g.n;
+      for (int q = 0; q < 4; ++q)
+        if (gcol + q < g.n) pr[gcol + q] = o[q];
+    }
+  }
+}
+
+// tile configurations
+using Tile128x2 = Tile<128, 128, 2, 2, 2>;
+using Tile256x3 = Tile<256, 128, 4, 2, 3>;
+using Tile256sq = Tile<256, 256, 2, 4, 2>;
+enum { kCfg128 = 0, kCfg256x128 = 1, kCfg256sq = 2 };
+
+// 256 x 256 tiles when they still give every CU two or more tiles, else 128 x 128 (the
+// rollout's 4096-row GEMMs)
+static int gemm_config(int64_t m, int n, int batch) {
+  static const int forced = [] {
+    const char *e = getenv("PHC_GEMM_CFG");  // tuning aid (tools/twin_gemm_probe.py)
+    return e ? atoi(e) : -1;
+  }();
+  if (forced >= 0) return forced;
+  const int64_t big = ((m + 255) / 256) * ((n + 255) / 256) * batch;
+  return big >= 512 ? kCfg256sq : kCfg128;
+}
+
+static void gemm_tile_dims(int cfg, int *bm, int *bn) {
+  *bm = cfg == kCfg128 ? 128 : 256;
+  *bn = cfg == kCfg256sq ? 256 : 128;
+}
+
+template <typename T, typename OutT, int EPI, typename TL>
+static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
+  auto kernel = k_twin_gemm<T, OutT, EPI, TL>;
+  static bool attr = [&] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              TL::kLdsBytes);
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
+}
+
+template <typename T, typename OutT, int EPI>
+static void launch_cfg(int cfg, const GemmArgs &g, int64_t blocks, hipStream_t st) {
+  switch (cfg) {
+    case kCfg128: launch_one<T, OutT, EPI, Tile128x2>(g, blocks, st); break;
+    case kCfg256x128: launch_one<T, OutT, EPI, Tile256x3>(g, blocks, st); break;
+    default: launch_one<T, OutT, EPI, Tile256sq>(g, blocks, st); break;
+  }
+}
+
+template <typename T, typename OutT>
+static void launch_epi(int epi, int cfg, const GemmArgs &g, int64_t blocks, hipStream_t st) {
+  switch (epi) {
+    case PHC_EPI_STORE: launch_cfg<T, OutT, PHC_EPI_STORE>(cfg, g, blocks, st); break;
+    case PHC_EPI_BIAS: launch_cfg<T, OutT, PHC_EPI_BIAS>(cfg, g, blocks, st); break;
+    case PHC_EPI_BIAS_SILU: launch_cfg<T, OutT, PHC_EPI_BIAS_SILU>(cfg, g, blocks, st); break;
+    default: launch_cfg<T, OutT, PHC_EPI_SILU_GRAD>(cfg, g, blocks, st); break;
+  }
+}
+
+static void launch_gemm(int dtype, int out_dtype, int epi, int cfg, const GemmArgs &g, int64_t blocks,
+                        hipStream_t st) {
+  if (dtype == PHC_DT_F16) {
+    if (out_dtype == PHC_DT_F32) launch_epi<_Float16, float>(epi, cfg, g, blocks, st);
+    else launch_epi<_Float16, _Float16>(epi, cfg, g, blocks, st);
+  } else {
+    if (out_dtype == PHC_DT_F32) launch_epi<__bf16, float>(epi, cfg, g, blocks, st);
+    else launch_epi<__bf16, __bf16>(epi, cfg, g, blocks, st);
+  }
+}
+
+}  // namespace phc
+
+using namespace phc;
+
+extern "C" size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_t n) {
+  if (m <= 0 || batch <= 0 || n <= 0) return 0;
+  return (size_t)((m + 127) / 128) * batch * n * sizeof(float);  // one partial row per m tile (BM >= 128)
+}
+
+extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *workspace, void *stream) {
+  PHC_REQUIRE(d, "twin_gemm: null descriptor");
+  PHC_REQUIRE(d->a && d->b && d->out, "twin_gemm: null operand");
+  PHC_REQUIRE(d->m > 0 && d->n > 0 && d->k > 0 && d->batch >= 1, "twin_gemm: bad shape");
+  PHC_REQUIRE(d->k % kGBK == 0, "twin_gemm: k (%d) must be a multiple of %d (zero-pad the operands)", d->k, kGBK);
+  PHC_REQUIRE(d->lda >= d->k && d->ldb >= d->k && d->lda % 8 == 0 && d->ldb % 8 == 0,
+              "twin_gemm: leading dimensions must cover k and be multiples of 8");
+  PHC_REQUIRE((reinterpret_cast<uintptr_t>(d->a) & 15) == 0 && (reinterpret_cast<uintptr_t>(d->b) & 15) == 0,
+              "twin_gemm: operands must be 16-byte aligned");
+  PHC_REQUIRE(d->dtype == PHC_DT_F16 || d->dtype == PHC_DT_BF16, "twin_gemm: operands must be f16 or bf16");
+  PHC_REQUIRE(d->out_dtype == PHC_DT_F32 || d->out_dtype == d->dtype, "twin_gemm: out must be f32 or the operand type");
+  PHC_REQUIRE(d->epilogue >= PHC_EPI_STORE && d->epilogue <= PHC_EPI_SILU_GRAD, "twin_gemm: bad epilogue");
+  PHC_REQUIRE(d->twin_groups >= 1 && d->twin_cols >= 1 && d->twin_groups * d->twin_cols == d->batch * d->n,
+              "twin_gemm: twin geometry must cover batch * n columns");
+  PHC_REQUIRE(!(d->epilogue == PHC_EPI_BIAS || d->epilogue == PHC_EPI_BIAS_SILU) || d->bias,
+              "twin_gemm: epilogue needs the bias");
+  PHC_REQUIRE(d->epilogue != PHC_EPI_SILU_GRAD || d->aux, "twin_gemm: SILU_GRAD needs the pre-activation (aux)");
+  PHC_REQUIRE(!bias_grad || (d->epilogue == PHC_EPI_SILU_GRAD && workspace),
+              "twin_gemm: bias_grad needs the SILU_GRAD epilogue and a workspace");
+  const int cfg = gemm_config(d->m, d->n, d->batch);
+  int bm, bn;
+  gemm_tile_dims(cfg, &bm, &bn);
+  const int64_t tiles_m = (d->m + bm - 1) / bm;
+  const int64_t tiles_n = (d->n + bn - 1) / bn;
+  const int64_t blocks = tiles_m * tiles_n * d->batch;
+  PHC_REQUIRE(blocks < (1ll << 31), "twin_gemm: grid too large");
+  GemmArgs g{};
+  g.a = static_cast<const char *>(d->a);
+  g.b = static_cast<const char *>(d->b);
+  g.a_bs = d->a_batch_stride;
+  g.b_bs = d->b_batch_stride;
+  g.lda = d->lda;
+  g.ldb = d->ldb;
+  g.m = d->m;
+  g.n = d->n;
+  g.k = d->k;
+  g.batch = d->batch;
+  g.bias = d->bias;
+  g.aux = d->aux;
+  g.aux_layout = d->aux_layout;
+  g.out = d->out;
+  g.out_layout = d->out_layout;
+  g.tg = d->twin_groups;
+  g.tc = d->twin_cols;
+  g.partial = bias_grad ? static_cast<float *>(workspace) : nullptr;
+  g.tiles_m = (int)tiles_m;
+  g.tiles_n = (int)tiles_n;
+  static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
+  g.discard = discard ? 1 : 0;
+  hipStream_t st = as_stream(stream);
+  launch_gemm(d->dtype, d->out_dtype, d->epilogue, cfg, g, blocks, st);
+  if (bias_grad) {
+    const int c = d->batch * d->n;
+    hipLaunchKernelGGL(k_colsum<>, dim3((unsigned)((c + 63) / 64)), dim3(256), 0, st,
+                       static_cast<const float *>(workspace), (int)tiles_m, c, bias_grad);
+  }
+  return check_launch("twin_gemm");
+}

@@ -141,33 +141,6 @@ __global__ __launch_bounds__(256) void k_act_bwd(const T *dz, int dz_layout, con
   }
 }
 
-// column sums of the [rows, cols] partials: 16 lanes x float4 = 64 columns per block, 16 row
-// slices reduced through LDS
-__global__ __launch_bounds__(256) void k_colsum(const float *__restrict__ partial, int rows, int cols,
-                                                float *__restrict__ out) {
-  __shared__ float4 red[16][16];
-  const int cl = threadIdx.x & 15, rs = threadIdx.x >> 4;
-  const int c = blockIdx.x * 64 + cl * 4;
-  float4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (c < cols) {
-#pragma unroll 4
-    for (int r = rs; r < rows; r += 16) {
-      const float4 v = *reinterpret_cast<const float4 *>(partial + (int64_t)r * cols + c);
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
-  }
-  red[rs][cl] = acc;
-  __syncthreads();
-  if (rs == 0 && c < cols) {
-    float4 t = red[0][cl];
-    for (int k = 1; k < 16; ++k) {
-      const float4 v = red[k][cl];
-      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-    }
-    *reinterpret_cast<float4 *>(out + c) = t;
-  }
-}
-
 // ------------------------------------------------ LayerNorm + SiLU (twin head) --
 // z = silu(LayerNorm(y) * gamma + beta) per row of a GROUPED [G, M, N] tensor with per-group
 // affine parameters (the actor's and the critic's nn.LayerNorm(512) + nn.SiLU(),
@@ -477,7 +450,7 @@ extern "C" int phc_act_bwd(const void *grad_out, int32_t go_layout, const void *
   });
   if (bias_grad) {
     const int c = groups * cols;
-    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((c + 63) / 64)), dim3(256), 0, st, partial, (int)grid.y, c,
+    hipLaunchKernelGGL(k_colsum<>, dim3((unsigned)((c + 63) / 64)), dim3(256), 0, st, partial, (int)grid.y, c,
                        bias_grad);
   }
   return check_launch("act_bwd");

@@ -123,6 +123,142 @@ class TwinWeights:
         return self.w, self.b
 
 
+def _pad64(k):
+    return -(-k // 64) * 64
+
+
+class MfmaOperands:
+    """Operands of the hand-written MFMA GEMM path (phc_twin_gemm) in a half-precision dtype:
+    the first layer's stacked weight zero-padded to K % 64 == 0, the stacked [2, N, K] weights
+    of layers 2..L (forward B operands) and their transposes [2, K, N] (input-gradient B
+    operands).  Refreshed in place, like TwinWeights.get."""
+
+    def __init__(self):
+        self.key = None
+        self.w0 = None
+        self.w, self.wt, self.b = [], [], []
+
+
+def mfma_supported(weights):
+    """The MFMA path needs every reduction and output width (but the input's) % 64 == 0."""
+    for i, (a, _) in enumerate(weights.pairs):
+        n, k = a.weight.shape
+        if n % 64 or (i > 0 and k % 64):
+            return False
+    return True
+
+
+def mfma_operands(weights, dtype):
+    ps = weights.params()
+    key = (dtype,) + tuple((p._version, p.data_ptr()) for p in ps)
+    ops = weights.__dict__.setdefault("_mfma", MfmaOperands())
+    if ops.key == key:
+        return ops
+    with torch.no_grad():
+        a0, c0 = weights.pairs[0]
+        n0, k0 = a0.weight.shape
+        fresh = ops.w0 is None or ops.w0.dtype != dtype
+        if fresh:
+            ops.w0 = torch.zeros((2 * n0, _pad64(k0)), dtype=dtype, device=a0.weight.device)
+            ops.w = [torch.empty((2,) + a.weight.shape, dtype=dtype, device=a.weight.device)
+                     for a, _ in weights.pairs[1:]]
+            ops.wt = [torch.empty((2, a.weight.shape[1], a.weight.shape[0]), dtype=dtype, device=a.weight.device)
+                      for a, _ in weights.pairs[1:]]
+            ops.b = [torch.empty(2 * a.bias.shape[0], dtype=torch.float32, device=a.bias.device)
+                     for a, _ in weights.pairs]
+        ops.w0[:n0, :k0].copy_(a0.weight)
+        ops.w0[n0:, :k0].copy_(c0.weight)
+        for i, (a, c) in enumerate(weights.pairs):
+            ops.b[i][:a.bias.shape[0]].copy_(a.bias)
+            ops.b[i][a.bias.shape[0]:].copy_(c.bias)
+        for i, (a, c) in enumerate(weights.pairs[1:]):
+            ops.w[i][0].copy_(a.weight)
+            ops.w[i][1].copy_(c.weight)
+            ops.wt[i][0].copy_(a.weight.t())
+            ops.wt[i][1].copy_(c.weight.t())
+    ops.key = key
+    return ops
+
+
+class TwinTrunkMfmaFn(torch.autograd.Function):
+    """TwinTrunkFn on the hand-written MFMA GEMM (phc_gemm.hip) for f16 / bf16 operands: every
+    forward GEMM carries its bias + SiLU epilogue (pre-activation kept in fp32 for backward),
+    every input-gradient GEMM its SiLU-backward + bias-gradient epilogue, so no activation
+    makes a separate elementwise round trip.  Weight gradients stay split-K library GEMMs
+    (their reduction runs over the 32768 rows)."""
+
+    @staticmethod
+    def forward(ctx, x, weights, need_grad, *params):
+        dt = _compute_dtype()
+        with torch.autocast("cuda", enabled=False):
+            ops = mfma_operands(weights, dt)
+            B = ops.b
+            M, K0 = x.shape
+            Kp = ops.w0.shape[1]
+            xc = torch.zeros((M, Kp), dtype=dt, device=x.device) if Kp != K0 else torch.empty((M, Kp), dtype=dt,
+                                                                                               device=x.device)
+            xc[:, :K0].copy_(x)
+            n1 = ops.w0.shape[0] // 2
+            z = torch.empty((2, M, n1), dtype=dt, device=x.device)
+            pre = torch.empty((M, 2 * n1), dtype=torch.float32, device=x.device) if need_grad else None
+            N.twin_gemm(xc, ops.w0, N.EPI_BIAS_SILU, z, (2, n1), bias=B[0], aux=pre, aux_layout=N.SPLIT,
+                        out_layout=N.GROUPED)
+            pres, zs = [pre], [z]
+            L = len(ops.w) + 1
+            for l in range(1, L):
+                n = ops.w[l - 1].shape[1]
+                if l < L - 1:
+                    z = torch.empty((2, M, n), dtype=dt, device=x.device)
+                    pre = torch.empty((2, M, n), dtype=torch.float32, device=x.device) if need_grad else None
+                    N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS_SILU, z, (2, n), bias=B[l], aux=pre)
+                    pres.append(pre)
+                    zs.append(z)
+                else:
+                    y = torch.empty((2, M, n), dtype=torch.float32, device=x.device)
+                    N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS, y, (2, n), bias=B[l])
+        if need_grad:
+            ctx.save_for_backward(xc, *ops.wt, *pres, *zs)  # pres: pre-activations, biases included
+            ctx.L, ctx.K0 = L, K0
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        L, K0 = ctx.L, ctx.K0
+        saved = ctx.saved_tensors
+        xc, WT = saved[0], saved[1:L]
+        pres, zs = saved[L:2 * L - 1], saved[2 * L - 1:3 * L - 2]
+        dt = xc.dtype
+        M = xc.shape[0]
+        grads = [None] * (2 * L)
+        with torch.autocast("cuda", enabled=False):
+            gy = gy.float().contiguous()
+            n = gy.shape[2]
+            db = torch.empty(2 * n, dtype=torch.float32, device=gy.device)
+            g = torch.empty(gy.shape, dtype=dt, device=gy.device)
+            N.act_bwd(gy, N.GROUPED, None, N.GROUPED, g, N.GROUPED, db, M, 2, n, N.ACT_NONE)
+            for l in range(L - 1, 0, -1):
+                grads[2 * l], grads[2 * l + 1] = _weight_grad(g, zs[l - 1]), db
+                k = WT[l - 1].shape[1]
+                db = torch.empty(2 * k, dtype=torch.float32, device=g.device)
+                if l > 1:
+                    gp = torch.empty((2, M, k), dtype=dt, device=g.device)
+                    N.twin_gemm(g, WT[l - 1], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[l - 1], bias_grad=db)
+                else:  # into the first layer's SPLIT [M, 2k] layout, the operand of its weight gradient
+                    gp = torch.empty((M, 2 * k), dtype=dt, device=g.device)
+                    N.twin_gemm(g, WT[0], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[0], aux_layout=N.SPLIT,
+                                out_layout=N.SPLIT, bias_grad=db)
+                    grads[0] = _weight_grad(gp[None], xc[None])[0][:, :K0]
+                    grads[1] = db
+                g = gp
+        out = []
+        for l in range(L):
+            dW, db = grads[2 * l], grads[2 * l + 1]
+            n = db.shape[0] // 2
+            dWa, dWc = (dW[:n], dW[n:]) if l == 0 else (dW[0], dW[1])
+            out += [dWa, db[:n], dWc, db[n:]]
+        return (None, None, None, *out)
+
+
 class TwinTrunkFn(torch.autograd.Function):
     """y[2, M, H] = the two trunks' last Linear outputs (before LayerNorm)."""
 
@@ -203,11 +339,29 @@ class TwinTrunkFn(torch.autograd.Function):
         return (None, None, None, *out)
 
 
+USE_MFMA_GEMM = True  # half-precision trunks on phc_twin_gemm (False: hipBLASLt + epilogue kernels)
+
+
+def _use_mfma(weights, dtype):
+    return USE_MFMA_GEMM and dtype != torch.float32 and mfma_supported(weights)
+
+
+def refresh_twin(weights, dtype):
+    """Refresh, in place, the weight copies the trunk path for `dtype` reads (a captured
+    rollout graph replays on these buffers)."""
+    if _use_mfma(weights, dtype):
+        mfma_operands(weights, dtype)
+    else:
+        weights.get(dtype)
+
+
 def twin_trunks(x, weights):
     """Both trunks' pre-LayerNorm outputs, [2, M, H] (index 0 = actor, 1 = critic)."""
     if not x.is_cuda:
         raise RuntimeError("twin_trunks runs on the HIP path only (no CPU fallback)")
     need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in weights.params())
+    if _use_mfma(weights, _compute_dtype()):
+        return TwinTrunkMfmaFn.apply(x, weights, need_grad, *weights.params())
     return TwinTrunkFn.apply(x, weights, need_grad, *weights.params())
 
 

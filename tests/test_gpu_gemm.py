@@ -1,0 +1,120 @@
+"""phc_twin_gemm (phc_gemm.hip): the half-precision MFMA GEMM with fused twin-trunk epilogues vs
+plain PyTorch fp32 (needs an MI355X).
+
+Tolerances: the STORE epilogue on small-integer operands is bit-exact (every product and partial
+sum is an integer below 2^24, so fp32 accumulation in any order gives the same value; asymmetric
+operands catch a transposed output).  The fused epilogues on random data are compared with the
+fp32 product of the same half-precision operands followed by the torch ops: GEMM sums differ only
+in fp32 summation order (rel. 2e-5), a half-precision output by one rounding (rel. 2^-10 f16).
+"""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _ints(shape, g, dtype, lo=-4, hi=5):
+    return torch.randint(lo, hi, shape, device=DEV, generator=g).to(dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("m,n,k,batch", [(300, 200, 192, 2), (256, 128, 64, 1), (1000, 69, 960, 1)])
+def test_store_exact_integer_operands(dtype, m, n, k, batch):
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(0)
+    a = _ints((batch, m, k), g, dtype)
+    b = _ints((batch, n, k), g, dtype, lo=-3, hi=7)  # asymmetric range
+    out = torch.empty((batch, m, n), device=DEV)
+    N.twin_gemm(a, b, N.EPI_STORE, out, (batch, n))
+    ref = torch.bmm(a.float(), b.float().transpose(1, 2))
+    assert torch.equal(out, ref)
+
+
+def test_strided_operand_and_shared_a():
+    """A row-strided view (lda > k, the zero-padded first layer) and an A shared by both batches."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(1)
+    base = _ints((200, 256), g, torch.float16)
+    a = base[:, :192]
+    b = _ints((2, 96, 192), g, torch.float16)
+    out = torch.empty((2, 200, 96), device=DEV)
+    N.twin_gemm(a, b, N.EPI_STORE, out, (2, 96))
+    ref = torch.einsum("mk,bnk->bmn", a.float(), b.float())
+    assert torch.equal(out, ref)
+
+
+def test_bias_silu_split_to_grouped():
+    """Layer 1: one [m, k] x [2n, k]^T GEMM, pre kept SPLIT [m, 2n] (fp32), silu written GROUPED
+    [2, m, n] in f16 — the twin layout conversion of phc_bias_act_fwd, fused."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(2)
+    m, n, k = 333, 256, 128
+    a = torch.randn((m, k), device=DEV, generator=g).half()
+    w = (torch.randn((2 * n, k), device=DEV, generator=g) / k ** 0.5).half()
+    bias = torch.randn(2 * n, device=DEV, generator=g)
+    pre = torch.empty((m, 2 * n), device=DEV)
+    z = torch.empty((2, m, n), dtype=torch.float16, device=DEV)
+    N.twin_gemm(a, w, N.EPI_BIAS_SILU, z, (2, n), bias=bias, aux=pre, aux_layout=N.SPLIT, out_layout=N.GROUPED)
+    ref_pre = a.float() @ w.float().t() + bias
+    torch.testing.assert_close(pre, ref_pre, rtol=2e-5, atol=2e-5)
+    ref_z = torch.nn.functional.silu(ref_pre).view(m, 2, n).permute(1, 0, 2)
+    torch.testing.assert_close(z.float(), ref_z, rtol=2.0 ** -10, atol=2e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_bias_fp32_out_batched(dtype):
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    m, n, k = 500, 192, 256
+    a = torch.randn((2, m, k), device=DEV, generator=g).to(dtype)
+    w = (torch.randn((2, n, k), device=DEV, generator=g) / k ** 0.5).to(dtype)
+    bias = torch.randn(2 * n, device=DEV, generator=g)
+    y = torch.empty((2, m, n), device=DEV)
+    N.twin_gemm(a, w, N.EPI_BIAS, y, (2, n), bias=bias)
+    ref = torch.bmm(a.float(), w.float().transpose(1, 2)) + bias.view(2, 1, n)
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("out_layout", [0, 1])
+def test_silu_grad_and_bias_grad(out_layout):
+    """Input gradient of a SiLU layer: dz = g @ W (W pre-transposed to [k_in, n_out]), then
+    dz * silu'(pre + b) rounded to f16, and the bias gradient from the fp32 products."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(4)
+    m, n_out, k_in = 777, 192, 256
+    gr = torch.randn((2, m, n_out), device=DEV, generator=g).half()
+    w = (torch.randn((2, n_out, k_in), device=DEV, generator=g) / n_out ** 0.5).half()
+    wt = w.transpose(1, 2).contiguous()  # [2, k_in, n_out]
+    pre_shape = (m, 2 * k_in) if out_layout == N.SPLIT else (2, m, k_in)
+    pre = torch.randn(pre_shape, device=DEV, generator=g) * 2
+    pb = torch.randn(2 * k_in, device=DEV, generator=g)
+    gout = torch.empty(pre_shape, dtype=torch.float16, device=DEV)
+    db = torch.empty(2 * k_in, device=DEV)
+    N.twin_gemm(gr, wt, N.EPI_SILU_GRAD, gout, (2, k_in), bias=pb, aux=pre, aux_layout=out_layout,
+                out_layout=out_layout, bias_grad=db)
+
+    def grouped(t):
+        return t.view(m, 2, k_in).permute(1, 0, 2) if out_layout == N.SPLIT else t
+
+    dz = torch.bmm(gr.float(), w.float())  # [2, m, k_in]
+    p = (grouped(pre) + pb.view(2, 1, k_in)).clone().requires_grad_(True)
+    torch.nn.functional.silu(p).backward(dz)
+    torch.testing.assert_close(grouped(gout).float(), p.grad, rtol=2.0 ** -10, atol=1e-4)
+    torch.testing.assert_close(db, p.grad.sum(1).reshape(-1), rtol=1e-4, atol=1e-3)
+
+
+def test_rejects_unpadded_k():
+    from puffer_phc_amd import _native as N
+
+    a = torch.zeros((64, 934), dtype=torch.float16, device=DEV)
+    b = torch.zeros((64, 934), dtype=torch.float16, device=DEV)
+    out = torch.empty((64, 64), device=DEV)
+    with pytest.raises(RuntimeError, match="multiple of 64"):
+        N.twin_gemm(a, b, N.EPI_STORE, out, (1, 64))

@@ -253,3 +253,30 @@ def test_fp16_operands_match_tf32_error():
         errs[k] = (rel(f16[2][k], ref[2][k]), rel(tf32[2][k], ref[2][k]))
     bad = {k: v for k, v in errs.items() if v[0] > 1.5 * v[1] + 1e-7}
     assert not bad, bad
+
+
+@pytest.mark.parametrize("precision", [torch.float16, torch.bfloat16])
+def test_mfma_trunks_match_library_path(precision):
+    """The hand-written MFMA GEMM path (phc_twin_gemm with fused epilogues) against the
+    hipBLASLt + epilogue-kernel path on the same half-precision operands: the same rounding
+    points, so only fp32 summation order differs (rel. L2 <= 1e-3 f16 / 1e-2 bf16 incl. the
+    log-prob's amplification of mu)."""
+    from puffer_phc_amd.policies import twin_mlp
+
+    pol = _policy()
+    g = torch.Generator(device=DEV).manual_seed(6)
+    obs = torch.randn((1000, 934), device=DEV, generator=g) * 2
+    act = torch.randn((1000, 69), device=DEV, generator=g) * 0.3
+    assert twin_mlp.mfma_supported(pol.policy._twin)
+    try:
+        twin_mlp.USE_MFMA_GEMM = False
+        lib = _run(pol, obs, act, fused=True, precision=precision, loss_scale=2.0 ** 12)
+        twin_mlp.USE_MFMA_GEMM = True
+        mf = _run(pol, obs, act, fused=True, precision=precision, loss_scale=2.0 ** 12)
+    finally:
+        twin_mlp.USE_MFMA_GEMM = True
+    tol = 1e-3 if precision == torch.float16 else 1e-2
+    assert rel(mf[1], lib[1]) <= tol
+    assert rel(mf[0], lib[0]) <= tol
+    worst = max(rel(mf[2][k], lib[2][k]) for k in lib[2])
+    assert worst <= tol, worst
