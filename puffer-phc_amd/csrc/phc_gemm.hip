@@ -256,6 +256,62 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
           }
     }
     __syncthreads();
+    const int64_t prow0 = m0 + (int64_t)pass * TL::kEpRows;  // first row of this pass
+    if (vec && prow0 + TL::kEpRows <= g.m) {
+      // full pass, 4 whole columns per thread: offsets are base + row * stride, and the rows go
+      // in batches of 4 with their aux loads issued together
+      const int lc = bt * g.n + gcol;
+      const int grp = lc / g.tc, jc = lc - grp * g.tc;
+      auto lin = [&](int layout, int64_t &base, int64_t &stride) {
+        if (layout == PHC_LAYOUT_SPLIT) { base = lc; stride = (int64_t)g.tg * g.tc; }
+        else { base = (int64_t)grp * g.m * g.tc + jc; stride = g.tc; }
+      };
+      int64_t ob, os, ab = 0, as = 0;
+      lin(g.out_layout, ob, os);
+      lin(g.aux_layout, ab, as);
+      constexpr int IT = TL::kEpRows / kRowGroups, U = EPI == PHC_EPI_SILU_GRAD ? 2 : 4;
+      static_assert(IT % U == 0, "row batches");
+#pragma unroll 1
+      for (int i0 = 0; i0 < IT; i0 += U) {
+        float4 av[U];
+        if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int64_t row = prow0 + rg + kRowGroups * (i0 + u);
+            av[u] = *reinterpret_cast<const float4 *>(static_cast<const float *>(g.aux) + ab + row * as);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int r = rg + kRowGroups * (i0 + u);
+          const int64_t row = prow0 + r;
+          const float4 t = *reinterpret_cast<const float4 *>(&ep[r * BN + (c4 ^ (((r >> 2) & 3) << 4))]);
+          float v[4] = {t.x, t.y, t.z, t.w};
+          if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+            const float a[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float x = a[q] + bias4[q];
+              const float sg = 1.0f / (1.0f + expf(-x));
+              v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
+              csum[q] += v[q];
+            }
+          } else if constexpr (EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] += bias4[q];
+            if constexpr (EPI == PHC_EPI_BIAS_SILU) {
+              if (g.aux)
+                *reinterpret_cast<float4 *>(static_cast<float *>(g.aux) + ab + row * as) =
+                    float4{v[0], v[1], v[2], v[3]};
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = gemm_silu(v[q]);
+            }
+          }
+          gemm_store4<OutT>(g.out, ob + row * os, v);
+        }
+      }
+      continue;
+    }
     for (int it = 0; it < TL::kEpRows / kRowGroups; ++it) {
       const int r = rg + kRowGroups * it;
       const int64_t row = m0 + (int64_t)pass * TL::kEpRows + r;

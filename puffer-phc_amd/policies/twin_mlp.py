@@ -21,6 +21,8 @@ gradients.  The reference's unfused path (nn.Sequential of Linear/SiLU) is what 
 compare against.
 """
 
+import os
+
 import torch
 
 from .. import _native as N
@@ -339,7 +341,8 @@ class TwinTrunkFn(torch.autograd.Function):
         return (None, None, None, *out)
 
 
-USE_MFMA_GEMM = True  # half-precision trunks on phc_twin_gemm (False: hipBLASLt + epilogue kernels)
+# half-precision trunks on phc_twin_gemm (PHC_MFMA_GEMM=0: hipBLASLt GEMMs + epilogue kernels)
+USE_MFMA_GEMM = os.environ.get("PHC_MFMA_GEMM", "1") == "1"
 
 
 def _use_mfma(weights, dtype):
