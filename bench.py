@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--minibatch-size", type=int, default=32768)
     ap.add_argument("--min-len", type=int, default=60)
     ap.add_argument("--max-len", type=int, default=300)
-    ap.add_argument("--precision", default="xf32", choices=["xf32", "fp16", "bf16"],
+    ap.add_argument("--precision", default="fp16", choices=["xf32", "fp16", "bf16"],
                     help="policy GEMM arithmetic (TrainConfig.precision)")
     ap.add_argument("--amp", action="store_true",
                     help="AMP discriminator obs + discriminator loss (BASELINE config C5, with --precision bf16)")
@@ -159,7 +159,15 @@ class Runner:
         p = self.info.profile
         return {k: (getattr(p, k).elapsed - self._p0[k]) / steps * 1e3 for k in self._p0}
 
+    def skipped(self):
+        """Optimizer steps the fp16 loss scaler skipped so far (None outside fp16 PPO)."""
+        c = getattr(self, "components", None)
+        if c is None or c.skipped_steps is None:
+            return None
+        return int(c.skipped_steps)
+
     def mark(self):
+        self._skip0 = self.skipped()
         if self.args.mode == "ppo":
             p = self.info.profile
             self._p0 = {k: getattr(p, k).elapsed for k in ("evaluate", "env", "eval_forward", "train",
@@ -219,6 +227,8 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    skipped = runner.skipped()
+    skipped = None if skipped is None else skipped - runner._skip0
     env_steps = timer.count  # phc_env_step launches in the timed region, each timed by its dispatch events
     kern_s = timer.total_ms() / max(env_steps, 1) * 1e-3
     env.env.kernel_timer = None
@@ -267,9 +277,13 @@ def main():
                        "parallelism": f"dp{world} (env shards, RCCL grad all-reduce)",
                        "amp_obs": bool(args.amp),
                        "policy_gemm": {"xf32": "fp32 storage, hipBLASLt xf32 (torch 'high', as the reference)",
-                                       "fp16": "autocast fp16 MFMA + dynamic loss scaling",
-                                       "bf16": "autocast bf16 MFMA"}[args.precision] if args.mode != "env"
-                       else None,
+                                       "fp16": "fp16 operands (TF32's 11-bit significand; the reference runs "
+                                               "TF32) on hand-written MFMA GEMMs with fused bias/SiLU epilogues, "
+                                               "fp32 accumulate + outputs, dynamic loss scaling",
+                                       "bf16": "bf16 operands on hand-written MFMA GEMMs with fused epilogues, "
+                                               "fp32 accumulate + outputs"}[args.precision]
+                       if args.mode != "env" else None,
+                       "optimizer_steps_skipped_by_loss_scaler": skipped,
                        "phase_ms_per_step": runner.phase_ms(args.steps)},
             "roofline": {"bound": "hbm", "kernel": "phc_env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

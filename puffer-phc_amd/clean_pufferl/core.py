@@ -92,6 +92,7 @@ def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=Non
     if train_cfg.precision == "fp16":
         # fp16 keeps TF32's mantissa but not its exponent range: dynamic loss scaling for the grads
         components.scaler = torch.amp.GradScaler("cuda")
+        components.skipped_steps = torch.zeros((), dtype=torch.int64, device=train_cfg.device)
     components.flat_grads = D.FlatGrads(uncompiled_policy.parameters())
     components.gae = _native.GAE()
     info = TrainInfo(config=train_cfg, exp_id=exp_id, env_name=env_cfg.name, stats=StatsData(), msg=msg,
@@ -348,6 +349,8 @@ def train(components, info, utilization=None):
                         scaler.unscale_(components.optimizer)
                         gnorm = flat.clip_(cfg.max_grad_norm)
                         scaler.step(components.optimizer)  # skipped when a grad is inf/nan
+                        for found in scaler._found_inf_per_device(components.optimizer).values():
+                            components.skipped_steps += (found > 0).long()  # device-side count, no sync
                         scaler.update()
                 with profile.train_misc, torch.no_grad():
                     acc += torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,

@@ -259,6 +259,8 @@ class TrainComponents:
     experience: Experience
     optimizer: torch.optim.Optimizer
     scaler: Any = None
+    # fp16: optimizer steps the loss scaler skipped (inf/nan gradients), a device counter
+    skipped_steps: Any = None
 
 
 @dataclass

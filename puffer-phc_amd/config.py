@@ -173,11 +173,14 @@ class TrainConfig(DeviceConfig):
     disc_coef: float = 5.0
     bound_coef: float = 10.0
     l2_reg_coef: float = 0.0
-    # policy GEMM arithmetic: "xf32" = float32 storage with hipBLASLt's xf32 emulation (what
-    # torch "high" precision gives on gfx950, at least TF32-accurate as the reference);
-    # "fp16" = autocast fp16 MFMA (TF32's 10-bit mantissa) with dynamic loss scaling;
-    # "bf16" = autocast bf16 MFMA (BASELINE config C5).
-    precision: str = "xf32"
+    # policy GEMM arithmetic.  "fp16" (default) = fp16 GEMM operands on the hand-written MFMA
+    # GEMM (phc_gemm.hip), fp32 accumulation and outputs, epilogues in fp32: TF32's arithmetic
+    # (the reference sets torch.set_float32_matmul_precision("high"), clean_pufferl/core.py:38)
+    # with dynamic loss scaling for fp16's narrower exponent range (tests/test_gpu_twin_mlp.py
+    # test_fp16_operands_match_tf32_error); "xf32" = float32 storage with hipBLASLt's xf32
+    # emulation (torch "high" on gfx950, bf16x3: more accurate than TF32, 2.3x slower);
+    # "bf16" = bf16 operands (BASELINE config C5).
+    precision: str = "fp16"
     # replay policy inference + experience store of each rollout step from a captured hipGraph
     # (the env step itself stays eager); False = the reference's eager loop
     rollout_graph: bool = True

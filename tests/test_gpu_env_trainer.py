@@ -144,10 +144,10 @@ def test_ppo_iteration_trains(small_env):
     assert float(policy.policy.obs_norm.count) == 2.0
 
 
-@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+@pytest.mark.parametrize("precision", ["fp16", "bf16", "xf32"])
 def test_ppo_iteration_reduced_precision(small_env, precision):
-    """TrainConfig.precision fp16 (dynamic loss scaling) / bf16 (autocast): one full PPO
-    iteration stays finite, updates the weights and keeps fp32 master parameters."""
+    """TrainConfig.precision fp16 (default; dynamic loss scaling) / bf16 / xf32 (fp32 storage):
+    one full PPO iteration stays finite, updates the weights and keeps fp32 master parameters."""
     from puffer_phc_amd import clean_pufferl
     from puffer_phc_amd.config import TrainConfig
     from puffer_phc_amd.policies import PHCPolicy, Policy
@@ -168,6 +168,8 @@ def test_ppo_iteration_reduced_precision(small_env, precision):
     assert all(v.dtype == torch.float32 for v in policy.parameters())
     changed = sum(not torch.equal(before[k], v) for k, v in policy.named_parameters() if v.requires_grad)
     assert changed > 0
+    if precision == "fp16":
+        assert int(comps.skipped_steps) >= 0
 
 
 @pytest.mark.parametrize("use_amp", [False, True])
