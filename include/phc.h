@@ -291,6 +291,38 @@ size_t phc_compact_workspace_bytes(int64_t n);
 int phc_compact_rows(const phc_row_field *fields, int32_t num_fields, const uint8_t *mask, int64_t n,
                      int64_t *cursor, int64_t capacity, int64_t *counts, void *workspace, void *stream);
 
+/* R21: the update tail of a PPO minibatch (clean_pufferl/core.py:360-372: clip_grad_norm_ +
+ * torch.optim.Adam(eps=1e-5), under torch.amp.GradScaler when use_loss_scale) on FLAT fp32
+ * buffers param / grad / exp_avg / exp_avg_sq of n elements (16-byte aligned).  The gradient
+ * is cut into nblk blocks of at most phc_opt_block_elems() elements that never straddle a
+ * parameter: blk_range [nblk, 2] = (start, end), seg_blk [nseg + 1] = first block of each
+ * parameter (device int64 / int32 tables).  One call: per-parameter norms of the unscaled
+ * gradients, clip coefficient max_norm / (total + 1e-6) (<= 1), loss-scale update and skip
+ * on inf / nan (GradScaler: backoff, growth after growth_interval clean steps), Adam step with
+ * bias corrections.  state lives in device memory (a captured graph can replay the call);
+ * norm_out (device, nullable) = [sum of per-parameter norms, total norm]. */
+typedef struct phc_adam_params {
+  float lr, beta1, beta2, eps;
+  float max_norm;
+  int32_t use_loss_scale;
+  float growth_factor, backoff_factor;
+  int32_t growth_interval;
+  int32_t reserved;
+} phc_adam_params;
+typedef struct phc_opt_state {
+  float loss_scale;
+  int32_t growth_tracker;
+  int32_t step;    /* Adam steps taken */
+  int32_t skipped; /* steps skipped for inf / nan gradients */
+  float grad_mul, step_size, bc2_sqrt; /* this step's coefficients (written by the call) */
+  int32_t skip;
+} phc_opt_state;
+int64_t phc_opt_block_elems(void);
+size_t phc_opt_workspace_bytes(int32_t nblk);
+int phc_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const int64_t *blk_range,
+                 int32_t nblk, const int32_t *seg_blk, int32_t nseg, const phc_adam_params *hp, phc_opt_state *state,
+                 float *norm_out, void *workspace, void *stream);
+
 /* R21: the PPO minibatch objective (clean_pufferl/core.py:298-352 with the fixed-sigma Normal
  * log-prob / entropy of pufferlib.sample_logits and PHCPolicy.bound_loss).  Forward: stats[0] =
  * loss = pg - ent_coef*ent + vf_coef*v + bound_coef*bound, stats[1..7] = pg, v, ent,

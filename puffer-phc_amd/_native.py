@@ -92,6 +92,18 @@ class GemmDescC(ctypes.Structure):
 EPI_STORE, EPI_BIAS, EPI_BIAS_SILU, EPI_SILU_GRAD = 0, 1, 2, 3
 
 
+class AdamParamsC(ctypes.Structure):
+    _fields_ = [("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("max_norm", ctypes.c_float), ("use_loss_scale", ctypes.c_int32), ("growth_factor", ctypes.c_float),
+                ("backoff_factor", ctypes.c_float), ("growth_interval", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class OptStateC(ctypes.Structure):
+    _fields_ = [("loss_scale", ctypes.c_float), ("growth_tracker", ctypes.c_int32), ("step", ctypes.c_int32),
+                ("skipped", ctypes.c_int32), ("grad_mul", ctypes.c_float), ("step_size", ctypes.c_float),
+                ("bc2_sqrt", ctypes.c_float), ("skip", ctypes.c_int32)]
+
+
 _EXPORTS = {
     "phc_version": (ctypes.c_int, []),
     "phc_last_error": (ctypes.c_char_p, []),
@@ -123,6 +135,10 @@ _EXPORTS = {
                                         ctypes.c_int32, ctypes.c_int32, c_vp, c_vp]),
     "phc_twin_gemm_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
     "phc_twin_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDescC), c_vp, c_vp, c_vp]),
+    "phc_opt_block_elems": (c_i64, []),
+    "phc_opt_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
+    "phc_opt_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, ctypes.c_int32, c_vp, ctypes.c_int32,
+                                     ctypes.POINTER(AdamParamsC), c_vp, c_vp, c_vp, c_vp]),
     "phc_ppo_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_ppo_loss_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
                                          ctypes.POINTER(PpoCoefsC), c_vp, c_vp, c_vp, c_vp]),

@@ -20,6 +20,7 @@ import torch
 
 from .. import _native
 from .. import distributed as D
+from ..optim import FlatAdam
 from ..policies.twin_mlp import refresh_twin
 from .ppo_loss import ppo_objective
 from .structs import Experience, LossComponents, Profile, StatsData, TrainComponents, TrainInfo, Utilization
@@ -81,19 +82,27 @@ def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=Non
     uncompiled_policy = policy
     if train_cfg.compile:
         policy = torch.compile(policy)
+    autocast(train_cfg)  # validates the precision name
+    flat_grads = D.FlatGrads(uncompiled_policy.parameters())
+    fp16 = train_cfg.precision == "fp16"
     if optimizer is None:
-        # one fused kernel for the whole parameter set on the device (same Adam update)
-        fused = next(policy.parameters()).is_cuda
-        optimizer = torch.optim.Adam(policy.parameters(), lr=train_cfg.learning_rate, eps=1e-5, fused=fused)
+        if next(policy.parameters()).is_cuda:
+            # flat parameter / gradient / moment buffers, the clip + loss-scale + Adam tail in one
+            # HIP call (optim.FlatAdam); fp16 keeps TF32's mantissa but not its exponent range:
+            # dynamic loss scaling (torch.amp.GradScaler's policy) for the gradients
+            optimizer = FlatAdam(flat_grads, lr=train_cfg.learning_rate, eps=1e-5, use_loss_scale=fp16)
+        else:
+            optimizer = torch.optim.Adam(policy.parameters(), lr=train_cfg.learning_rate, eps=1e-5)
     initial_params = {name: p.detach().clone() for name, p in policy.named_parameters()}
     components = TrainComponents(vecenv=vecenv, policy=policy, uncompiled_policy=uncompiled_policy,
                                  experience=experience, optimizer=optimizer)
-    autocast(train_cfg)  # validates the precision name
-    if train_cfg.precision == "fp16":
-        # fp16 keeps TF32's mantissa but not its exponent range: dynamic loss scaling for the grads
+    if isinstance(optimizer, FlatAdam):
+        components.scaler = optimizer if fp16 else None
+        components.skipped_steps = optimizer.skipped_steps if fp16 else None
+    elif fp16:
         components.scaler = torch.amp.GradScaler("cuda")
         components.skipped_steps = torch.zeros((), dtype=torch.int64, device=train_cfg.device)
-    components.flat_grads = D.FlatGrads(uncompiled_policy.parameters())
+    components.flat_grads = flat_grads
     components.gae = _native.GAE()
     info = TrainInfo(config=train_cfg, exp_id=exp_id, env_name=env_cfg.name, stats=StatsData(), msg=msg,
                      last_log_time=0, use_amp_obs=env_cfg.use_amp_obs, initial_params=initial_params,
@@ -337,19 +346,23 @@ def train(components, info, utilization=None):
                         loss = loss + l2 * cfg.l2_reg_coef
                 with profile.learn:
                     flat.zero()
-                    scaler = components.scaler
-                    if scaler is None:
+                    opt, scaler = components.optimizer, components.scaler
+                    if isinstance(opt, FlatAdam):
+                        opt.scale(loss).backward()  # loss * S under fp16 loss scaling
+                        flat.allreduce_mean()
+                        gnorm = opt.fused_step(cfg.max_grad_norm)[0]  # unscale, clip, skip-on-inf, Adam
+                    elif scaler is None:
                         loss.backward()
                         flat.allreduce_mean()
                         gnorm = flat.clip_(cfg.max_grad_norm)  # clip_grad_norm_ (core.py:366-370)
-                        components.optimizer.step()
+                        opt.step()
                     else:
                         scaler.scale(loss).backward()
                         flat.allreduce_mean()
-                        scaler.unscale_(components.optimizer)
+                        scaler.unscale_(opt)
                         gnorm = flat.clip_(cfg.max_grad_norm)
-                        scaler.step(components.optimizer)  # skipped when a grad is inf/nan
-                        for found in scaler._found_inf_per_device(components.optimizer).values():
+                        scaler.step(opt)  # skipped when a grad is inf/nan
+                        for found in scaler._found_inf_per_device(opt).values():
                             components.skipped_steps += (found > 0).long()  # device-side count, no sync
                         scaler.update()
                 with profile.train_misc, torch.no_grad():

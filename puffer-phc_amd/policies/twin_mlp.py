@@ -197,9 +197,10 @@ class TwinTrunkMfmaFn(torch.autograd.Function):
             B = ops.b
             M, K0 = x.shape
             Kp = ops.w0.shape[1]
-            xc = torch.zeros((M, Kp), dtype=dt, device=x.device) if Kp != K0 else torch.empty((M, Kp), dtype=dt,
-                                                                                               device=x.device)
+            xc = torch.empty((M, Kp), dtype=dt, device=x.device)
             xc[:, :K0].copy_(x)
+            if Kp != K0:
+                xc[:, K0:].zero_()  # K padding (the padded weight columns are zero too)
             n1 = ops.w0.shape[0] // 2
             z = torch.empty((2, M, n1), dtype=dt, device=x.device)
             pre = torch.empty((M, 2 * n1), dtype=torch.float32, device=x.device) if need_grad else None

@@ -1,0 +1,121 @@
+"""optim.FlatAdam (phc_opt_step, phc_optim.hip) vs the reference's update tail
+(clean_pufferl/core.py:360-372: clip_grad_norm_ + torch.optim.Adam(eps=1e-5), and
+torch.amp.GradScaler for the fp16 path) on the same parameters and gradients (needs an MI355X).
+
+Tolerance: parameters within rel 2e-6 / abs 1e-8 after several steps (Adam's update is
+lr * m / (sqrt(v) + eps) in fp32 in both; torch's moment updates use lerp / addcmul, a different
+rounding order; the clip coefficient here comes from a double-precision norm).  The logged norm
+(sum of per-parameter norms) within rel 1e-5.  Skip / scale decisions are exact.
+"""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+SHAPES = [(256, 96), (256,), (69, 256), (69,), (1, 256), (1,), (3000,)]
+
+
+def _params(seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return [torch.nn.Parameter(torch.randn(s, device=DEV, generator=g) * 0.1) for s in SHAPES]
+
+
+def _grads(step, scale=1.0):
+    g = torch.Generator(device=DEV).manual_seed(100 + step)
+    return [torch.randn(s, device=DEV, generator=g) * (0.5 + step) * scale for s in SHAPES]
+
+
+def _flat(params, **kw):
+    from puffer_phc_amd.distributed import FlatGrads
+    from puffer_phc_amd.optim import FlatAdam
+
+    fg = FlatGrads(params)
+    return fg, FlatAdam(fg, lr=3e-4, eps=1e-5, **kw)
+
+
+@pytest.mark.parametrize("max_norm", [1.0, 1e9])
+def test_clip_adam_matches_torch(max_norm):
+    ref = _params(0)
+    ours = _params(0)
+    opt_ref = torch.optim.Adam(ref, lr=3e-4, eps=1e-5)
+    fg, opt = _flat(ours)
+    for step in range(4):
+        for p, g in zip(ref, _grads(step)):
+            p.grad = g.clone()
+        norms = torch.stack([p.grad.norm() for p in ref])
+        torch.nn.utils.clip_grad_norm_(ref, max_norm)
+        opt_ref.step()
+        fg.zero()
+        for p, g in zip(ours, _grads(step)):
+            p.grad.copy_(g)
+        out = opt.fused_step(max_norm)
+        torch.testing.assert_close(out[0], norms.sum(), rtol=1e-5, atol=0)
+        for a, b in zip(ours, ref):
+            torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-6, atol=1e-8)
+    # the module parameters are views of the flat buffer
+    off = 0
+    for p in ours:
+        assert p.data_ptr() == opt.param_flat[off:].data_ptr()
+        off += p.numel()
+    assert int(opt._i[2]) == 4
+
+
+def test_loss_scale_skip_and_growth():
+    """GradScaler semantics: gradients of a scaled loss are unscaled; an inf gradient skips the
+    step (parameters and moments untouched) and halves the scale; growth after the interval."""
+    ref = _params(1)
+    ours = _params(1)
+    opt_ref = torch.optim.Adam(ref, lr=3e-4, eps=1e-5)
+    fg, opt = _flat(ours, use_loss_scale=True, init_scale=1024.0, growth_interval=2)
+    scales = []
+    for step in range(5):
+        S = float(opt.loss_scale)
+        scales.append(S)
+        grads = _grads(step)
+        fg.zero()
+        for p, g in zip(ours, grads):
+            p.grad.copy_(g * S)
+        if step == 2:
+            ours[3].grad[0] = float("inf")
+        before = [p.detach().clone() for p in ours]
+        opt.fused_step(1.0)
+        if step == 2:
+            for a, b in zip(ours, before):
+                assert torch.equal(a.detach(), b)
+            continue
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        opt_ref.step()
+        for a, b in zip(ours, ref):
+            torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-6, atol=1e-8)
+    # 1024 -> (2 clean steps) 2048 -> inf: 1024 -> 1024 -> (2 clean) 2048
+    assert scales == [1024.0, 1024.0, 2048.0, 1024.0, 1024.0]
+    assert float(opt.loss_scale) == 2048.0
+    assert int(opt.skipped_steps) == 1
+    assert int(opt._i[2]) == 4
+
+
+def test_state_dict_round_trip():
+    a = _params(2)
+    fg, opt = _flat(a, use_loss_scale=True)
+    for step in range(3):
+        fg.zero()
+        for p, g in zip(a, _grads(step, float(opt.loss_scale))):
+            p.grad.copy_(g)
+        opt.fused_step(5.0)
+    sd = opt.state_dict()
+    assert all(float(st["step"]) == 3.0 for st in sd["state"].values())
+    b = [torch.nn.Parameter(p.detach().clone()) for p in a]
+    fg2, opt2 = _flat(b, use_loss_scale=True)
+    opt2.load_state_dict(sd)
+    assert torch.equal(opt2.exp_avg, opt.exp_avg) and torch.equal(opt2.exp_avg_sq, opt.exp_avg_sq)
+    assert float(opt2.loss_scale) == float(opt.loss_scale)
+    for o, f, P in ((opt, fg, a), (opt2, fg2, b)):
+        f.zero()
+        for p, g in zip(P, _grads(7, float(o.loss_scale))):
+            p.grad.copy_(g)
+        o.fused_step(5.0)
+    for x, y in zip(a, b):
+        assert torch.equal(x.detach(), y.detach())
