@@ -237,8 +237,8 @@ int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, 
  * (what nn.Linear + nn.SiLU and their autograd backward compute, policies/phc_policy.py:10-61):
  *   STORE     out = C
  *   BIAS      out = C + bias[c]
- *   BIAS_SILU aux = C + bias[c] (fp32, nullable), out = silu(C + bias[c])
- *   SILU_GRAD out = C * silu'(aux + bias[c]) (aux fp32; bias nullable, e.g. when aux is the
+ *   BIAS_SILU aux = C + bias[c] (fp32 or dtype, nullable), out = silu(C + bias[c])
+ *   SILU_GRAD out = C * silu'(aux + bias[c]) (aux fp32 or dtype; bias nullable, e.g. when aux is the
  *             pre-activation BIAS_SILU wrote, bias included), and
  *             bias_grad[c] = column sums of that product in fp32 (nullable; needs
  *             phc_twin_gemm_workspace_bytes of workspace)
@@ -253,13 +253,47 @@ typedef struct phc_gemm_desc {
   int32_t n, k, batch, dtype;
   int32_t epilogue, out_dtype;
   const float *bias; /* [batch * n] */
-  void *aux;         /* fp32 pre-activation (BIAS_SILU: written, SILU_GRAD: read) */
+  void *aux;         /* pre-activation (BIAS_SILU: written, SILU_GRAD: read), aux_dtype */
   void *out;
   int32_t aux_layout, out_layout;
   int32_t twin_groups, twin_cols;
+  int32_t aux_dtype; /* PHC_DT_F32, or dtype: the pre-activation kept in the operand type, as
+                        torch.autocast's Linear output and SiLU's saved input are */
+  int32_t reserved;
 } phc_gemm_desc;
 size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_t n);
 int phc_twin_gemm(const phc_gemm_desc *desc, float *bias_grad, void *workspace, void *stream);
+
+/* R17 + R19: RunningNorm forward (policies/running_norm.py:15-20) of float32 observations
+ * obs [*, d], rows gathered through `rows` (int64 [m], nullable = identity), rounded into the
+ * first trunk GEMM's f16 / bf16 operand out [m, ld_out] (columns d..ld_out-1 zero; ld_out % 8
+ * == 0, out 16-byte aligned).  Same arithmetic as phc_rms_normalize before the rounding. */
+int phc_obs_half(const float *obs, const int64_t *rows, int64_t m, int32_t d, const float *mean,
+                 const float *var, float eps, float clip, void *out, int32_t ld_out, int32_t dtype,
+                 void *stream);
+
+/* R19 rollout tail (policies/phc_policy.py:40-61, discriminator_policy.py:55-67, pufferlib
+ * sample_logits): per row of the twin-trunk output trunk_out [2, rows, hidden] fp32 (actor rows,
+ * then critic rows, last Linear bias included): h_g = silu(LayerNorm_g(trunk_out[g])),
+ * mu = w_mu h_0 + b_mu, value = w_value . h_1 + b_value, std_j = min(exp(log_sigma_j), std_max),
+ * actions = mu + std * noise, logprob = sum_j Normal(mu, std).log_prob(actions).
+ * hidden in {256, 512, 768, 1024}; num_actions <= PHC_NUM_DOF + 3; mu nullable; trunk_out
+ * 16-byte aligned (the parameters may be 4-byte aligned views into a flat buffer). */
+typedef struct phc_policy_act_args {
+  const float *trunk_out;             /* [2, rows, hidden] */
+  const float *ln_gamma[2];           /* [hidden] each: actor, critic LayerNorm weight */
+  const float *ln_beta[2];            /* [hidden] each: actor, critic LayerNorm bias */
+  const float *w_mu, *b_mu;           /* [num_actions, hidden], [num_actions] */
+  const float *w_value, *b_value;     /* [hidden], [1] */
+  const float *log_sigma;             /* [num_actions] */
+  const float *noise;                 /* [rows, num_actions] standard normal draws */
+  float *actions, *logprob, *value;   /* [rows, num_actions], [rows], [rows] */
+  float *mu;                          /* [rows, num_actions], nullable */
+  int64_t rows;
+  int32_t hidden, num_actions;
+  float ln_eps, std_max;
+} phc_policy_act_args;
+int phc_policy_act(const phc_policy_act_args *args, void *stream);
 
 /* R19/R21: the twin trunks' LayerNorm(cols) + SiLU (policies/phc_policy.py:16-30) over a GROUPED
  * [groups, rows, cols] tensor y (dtype) with per-group gamma/beta [groups*cols] fp32:
@@ -276,7 +310,8 @@ int phc_ln_silu_bwd(const void *y, const float *gamma, const float *beta, const 
 /* R18: Experience.store (clean_pufferl/structs.py:113-131) on the device.  Each field copies
  * row r of src [n, row_elems] to row (*cursor + rank(r)) of dst [capacity, row_elems] for the
  * rows whose mask byte is set (mask NULL = all rows), in row order, while rows remain;
- * counts[0] = mask-true rows (n_valid), counts[1] = rows taken, *cursor += taken.  cursor and
+ * counts[0] = mask-true rows (n_valid), counts[1] = rows taken, counts[2] += n_valid,
+ * counts[3] += taken (running sums, zeroed by the caller), *cursor += taken.  cursor and
  * counts are device int64 so a captured hipGraph can replay the call. */
 #define PHC_MAX_ROW_FIELDS 12
 enum { PHC_ROW_COPY32 = 0, PHC_ROW_COPY64 = 1, PHC_ROW_U8_TO_F32 = 2 };
@@ -300,7 +335,9 @@ int phc_compact_rows(const phc_row_field *fields, int32_t num_fields, const uint
  * gradients, clip coefficient max_norm / (total + 1e-6) (<= 1), loss-scale update and skip
  * on inf / nan (GradScaler: backoff, growth after growth_interval clean steps), Adam step with
  * bias corrections.  state lives in device memory (a captured graph can replay the call);
- * norm_out (device, nullable) = [sum of per-parameter norms, total norm]. */
+ * norm_out (device, nullable) = [sum of per-parameter norms, total norm, l2]; with param_init
+ * (the flat initial parameters, nullable) l2 = sum over parameters of mean((p - p0)^2) before
+ * this step's update (the L2-init regulariser the reference logs, core.py:352-359). */
 typedef struct phc_adam_params {
   float lr, beta1, beta2, eps;
   float max_norm;
@@ -321,7 +358,21 @@ int64_t phc_opt_block_elems(void);
 size_t phc_opt_workspace_bytes(int32_t nblk);
 int phc_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const int64_t *blk_range,
                  int32_t nblk, const int32_t *seg_blk, int32_t nseg, const phc_adam_params *hp, phc_opt_state *state,
-                 float *norm_out, void *workspace, void *stream);
+                 float *norm_out, const float *param_init, void *workspace, void *stream);
+
+/* R21 gradient plumbing: for each job, dst[r, c] (+= when accumulate) = sum over s < parts of
+ * src[s * part_stride + r * src_ld + c] (parts summed in order; dst dense [rows, cols]).  Writes
+ * split-K weight-gradient partials and bias gradients of both trunks straight into the flat
+ * gradient buffer's per-parameter views (what autograd's per-parameter accumulation did), up to
+ * PHC_MAX_REDUCE_JOBS jobs per launch. */
+#define PHC_MAX_REDUCE_JOBS 32
+typedef struct phc_reduce_job {
+  const float *src;
+  float *dst;
+  int64_t rows, cols, src_ld, part_stride;
+  int32_t parts, accumulate;
+} phc_reduce_job;
+int phc_reduce_into(const phc_reduce_job *jobs, int32_t num_jobs, void *stream);
 
 /* R21: the PPO minibatch objective (clean_pufferl/core.py:298-352 with the fixed-sigma Normal
  * log-prob / entropy of pufferlib.sample_logits and PHCPolicy.bound_loss).  Forward: stats[0] =

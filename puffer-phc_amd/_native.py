@@ -86,10 +86,25 @@ class GemmDescC(ctypes.Structure):
                 ("batch", ctypes.c_int32), ("dtype", ctypes.c_int32), ("epilogue", ctypes.c_int32),
                 ("out_dtype", ctypes.c_int32), ("bias", c_vp), ("aux", c_vp), ("out", c_vp),
                 ("aux_layout", ctypes.c_int32), ("out_layout", ctypes.c_int32), ("twin_groups", ctypes.c_int32),
-                ("twin_cols", ctypes.c_int32)]
+                ("twin_cols", ctypes.c_int32), ("aux_dtype", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_SILU, EPI_SILU_GRAD = 0, 1, 2, 3
+
+
+class ReduceJobC(ctypes.Structure):
+    _fields_ = [("src", c_vp), ("dst", c_vp), ("rows", c_i64), ("cols", c_i64), ("src_ld", c_i64),
+                ("part_stride", c_i64), ("parts", ctypes.c_int32), ("accumulate", ctypes.c_int32)]
+
+
+MAX_REDUCE_JOBS = 32
+
+
+class PolicyActArgsC(ctypes.Structure):
+    _fields_ = [("trunk_out", c_vp), ("ln_gamma", c_vp * 2), ("ln_beta", c_vp * 2), ("w_mu", c_vp), ("b_mu", c_vp),
+                ("w_value", c_vp), ("b_value", c_vp), ("log_sigma", c_vp), ("noise", c_vp), ("actions", c_vp),
+                ("logprob", c_vp), ("value", c_vp), ("mu", c_vp), ("rows", c_i64), ("hidden", ctypes.c_int32),
+                ("num_actions", ctypes.c_int32), ("ln_eps", ctypes.c_float), ("std_max", ctypes.c_float)]
 
 
 class AdamParamsC(ctypes.Structure):
@@ -135,10 +150,14 @@ _EXPORTS = {
                                         ctypes.c_int32, ctypes.c_int32, c_vp, c_vp]),
     "phc_twin_gemm_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
     "phc_twin_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDescC), c_vp, c_vp, c_vp]),
+    "phc_reduce_into": (ctypes.c_int, [ctypes.POINTER(ReduceJobC), ctypes.c_int32, c_vp]),
+    "phc_obs_half": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int32, c_vp, c_vp, ctypes.c_float, ctypes.c_float,
+                                     c_vp, ctypes.c_int32, ctypes.c_int32, c_vp]),
+    "phc_policy_act": (ctypes.c_int, [ctypes.POINTER(PolicyActArgsC), c_vp]),
     "phc_opt_block_elems": (c_i64, []),
     "phc_opt_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
     "phc_opt_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, ctypes.c_int32, c_vp, ctypes.c_int32,
-                                     ctypes.POINTER(AdamParamsC), c_vp, c_vp, c_vp, c_vp]),
+                                     ctypes.POINTER(AdamParamsC), c_vp, c_vp, c_vp, c_vp, c_vp]),
     "phc_ppo_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_ppo_loss_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
                                          ctypes.POINTER(PpoCoefsC), c_vp, c_vp, c_vp, c_vp]),
@@ -462,11 +481,13 @@ def twin_gemm(a, b, epilogue, out, twin, bias=None, aux=None, aux_layout=GROUPED
     G, C = twin
     if out.dtype not in (torch.float32, a.dtype) or not out.is_contiguous() or out.numel() != m * batch * n:
         raise ValueError("twin_gemm: out must be contiguous f32 / operand-dtype with m * batch * n elements")
-    if aux is not None and (aux.dtype != torch.float32 or not aux.is_contiguous() or aux.numel() != out.numel()):
-        raise ValueError("twin_gemm: aux must be a contiguous f32 tensor shaped like out")
+    if aux is not None and (aux.dtype not in (torch.float32, a.dtype) or not aux.is_contiguous()
+                            or aux.numel() != out.numel()):
+        raise ValueError("twin_gemm: aux must be a contiguous f32 / operand-dtype tensor shaped like out")
     d = GemmDescC(pa, pb, abs_, bbs, lda, ldb, m, n, k, batch, DTYPE_CODE[a.dtype], epilogue, DTYPE_CODE[out.dtype],
                   _ptr(bias, torch.float32, (batch * n,), "bias", nullable=True),
-                  aux.data_ptr() if aux is not None else None, out.data_ptr(), aux_layout, out_layout, G, C)
+                  aux.data_ptr() if aux is not None else None, out.data_ptr(), aux_layout, out_layout, G, C,
+                  DTYPE_CODE[aux.dtype] if aux is not None else 0, 0)
     ws = None
     if bias_grad is not None:
         _ptr(bias_grad, torch.float32, (batch * n,), "bias_grad")
@@ -475,6 +496,70 @@ def twin_gemm(a, b, epilogue, out, twin, bias=None, aux=None, aux_layout=GROUPED
                                _stream()),
            "phc_twin_gemm")
     return out
+
+
+def reduce_into(jobs, accumulate=True):
+    """jobs: (src, dst) pairs; src [parts, rows, cols] (any row stride, unit column stride) or
+    [rows, cols]; dst a dense fp32 tensor of rows * cols elements: dst (+)= src.sum(0) in one
+    launch (phc_reduce_into).  The sources must stay alive until the launch has run (stream
+    order: the caching allocator guarantees it for tensors freed after this call)."""
+    for i in range(0, len(jobs), MAX_REDUCE_JOBS):
+        chunk = jobs[i:i + MAX_REDUCE_JOBS]
+        arr = (ReduceJobC * len(chunk))()
+        for q, (src, dst) in enumerate(chunk):
+            if src.dim() == 2:
+                src = src[None]
+            P, R, C = src.shape
+            if src.dtype != torch.float32 or dst.dtype != torch.float32 or not src.is_cuda or not dst.is_cuda:
+                raise ValueError("reduce_into: fp32 device tensors only")
+            if src.stride(2) != 1 or not dst.is_contiguous() or dst.numel() != R * C:
+                raise ValueError(f"reduce_into: job {q}: src {tuple(src.shape)} / dst {tuple(dst.shape)} mismatch")
+            arr[q] = ReduceJobC(src.data_ptr(), dst.data_ptr(), R, C, src.stride(1) if R > 1 else C,
+                                src.stride(0) if P > 1 else 0, P, int(accumulate))
+        _check(lib().phc_reduce_into(arr, len(chunk), _stream()), "phc_reduce_into")
+
+
+def obs_half(obs, mean, var, eps, clip, out, rows=None):
+    """out [m, ld] (f16 / bf16) = RunningNorm(obs[rows]) rounded once, zero-padded (phc_obs_half)."""
+    d = obs.shape[1]
+    m, ld = out.shape
+    _ptr(obs, torch.float32, None, "obs")
+    if obs.dim() != 2:
+        raise ValueError("obs_half: obs must be [rows, features]")
+    if out.dtype not in (torch.float16, torch.bfloat16) or not out.is_cuda or not out.is_contiguous():
+        raise ValueError("obs_half: out must be a contiguous f16 / bf16 device tensor")
+    if rows is None and obs.shape[0] != m:
+        raise ValueError(f"obs_half: {obs.shape[0]} obs rows for {m} output rows")
+    _check(lib().phc_obs_half(obs.data_ptr(), _ptr(rows, torch.int64, (m,), "rows", nullable=True), m, d,
+                              _ptr(mean.reshape(-1), torch.float32, (d,), "mean"),
+                              _ptr(var.reshape(-1), torch.float32, (d,), "var"), float(eps), float(clip),
+                              out.data_ptr(), ld, DTYPE_CODE[out.dtype], _stream()),
+           "phc_obs_half")
+    return out
+
+
+def policy_act(trunk_out, ln_actor, ln_critic, eps, w_mu, b_mu, w_value, b_value, log_sigma, noise, actions, logprob, value,
+               mu=None, std_max=float("inf")):
+    """Rollout tail after the trunks: LayerNorm+SiLU of both trunks (ln_* = (weight, bias)),
+    mu / value heads, Normal sample and log-prob (phc_policy_act)."""
+    G, M, H = trunk_out.shape
+    A = w_mu.shape[0]
+    if G != 2:
+        raise ValueError("policy_act: trunk_out must be [2, rows, hidden]")
+    args = PolicyActArgsC(_ptr(trunk_out, torch.float32, (2, M, H), "trunk_out"),
+                          (c_vp * 2)(_ptr(ln_actor[0], torch.float32, (H,), "actor ln weight"),
+                                     _ptr(ln_critic[0], torch.float32, (H,), "critic ln weight")),
+                          (c_vp * 2)(_ptr(ln_actor[1], torch.float32, (H,), "actor ln bias"),
+                                     _ptr(ln_critic[1], torch.float32, (H,), "critic ln bias")),
+                          _ptr(w_mu, torch.float32, (A, H), "w_mu"), _ptr(b_mu, torch.float32, (A,), "b_mu"),
+                          _ptr(w_value.reshape(-1), torch.float32, (H,), "w_value"),
+                          _ptr(b_value.reshape(-1), torch.float32, (1,), "b_value"),
+                          _ptr(log_sigma.reshape(-1), torch.float32, (A,), "log_sigma"),
+                          _ptr(noise, torch.float32, (M, A), "noise"), _ptr(actions, torch.float32, (M, A), "actions"),
+                          _ptr(logprob, torch.float32, (M,), "logprob"), _ptr(value, torch.float32, (M,), "value"),
+                          _ptr(mu, torch.float32, (M, A), "mu", nullable=True), M, H, A, float(eps),
+                          min(float(std_max), 3.0e38))
+    _check(lib().phc_policy_act(ctypes.byref(args), _stream()), "phc_policy_act")
 
 
 _WS = {}
@@ -557,7 +642,8 @@ class RowCompactor:
             raise ValueError(f"RowCompactor: 1..{MAX_ROW_FIELDS} fields")
         self.n, self.capacity = n, capacity
         self.cursor = torch.zeros(1, dtype=torch.int64, device=device)
-        self.counts = torch.zeros(2, dtype=torch.int64, device=device)
+        # {n_valid, taken} of the last call, then their running sums since reset()
+        self.counts = torch.zeros(4, dtype=torch.int64, device=device)
         self.workspace = torch.empty(lib().phc_compact_workspace_bytes(n), dtype=torch.uint8, device=device)
         self._keep = []
         arr = (RowFieldC * len(pairs))()
@@ -589,6 +675,7 @@ class RowCompactor:
 
     def reset(self, ptr=0):
         self.cursor.fill_(ptr)
+        self.counts.zero_()
 
 
 def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):

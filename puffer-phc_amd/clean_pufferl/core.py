@@ -91,6 +91,8 @@ def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=Non
             # HIP call (optim.FlatAdam); fp16 keeps TF32's mantissa but not its exponent range:
             # dynamic loss scaling (torch.amp.GradScaler's policy) for the gradients
             optimizer = FlatAdam(flat_grads, lr=train_cfg.learning_rate, eps=1e-5, use_loss_scale=fp16)
+            if train_cfg.l2_reg_coef == 0:
+                optimizer.track_init_distance()  # the logged L2-init term comes from the update pass
         else:
             optimizer = torch.optim.Adam(policy.parameters(), lr=train_cfg.learning_rate, eps=1e-5)
     initial_params = {name: p.detach().clone() for name, p in policy.named_parameters()}
@@ -126,6 +128,8 @@ class RolloutStep:
         self.value = torch.zeros(n, device=dev)
         self.actions = torch.zeros((n, *env.single_action_space.shape), device=dev)
         self.logprob = torch.zeros(n, device=dev)
+        self.noise = torch.zeros((n, *env.single_action_space.shape), device=dev)
+        self.fused_act = getattr(info.config, "fused_act", True)
         pairs = [(env.observations, exp.obs), (self.value, exp.values), (self.actions, exp.actions),
                  (self.logprob, exp.logprobs), (env.rewards, exp.rewards), (env.terminals, exp.dones),
                  (env.truncations, exp.truncateds), (env.env_ids, exp.env_ids)]
@@ -138,11 +142,18 @@ class RolloutStep:
         self.twin = getattr(pol, "_twin", None)
 
     def _body(self):
+        pol = self.policy.policy if hasattr(self.policy, "policy") else self.policy
         with torch.no_grad(), autocast(self.cfg):
-            actions, logprob, _, value = self.policy(self.env.observations)
-        self.value.copy_(value.flatten())
-        self.actions.copy_(actions)
-        self.logprob.copy_(logprob)
+            fused = False
+            if self.fused_act and hasattr(pol, "act_rollout"):
+                # sample_logits' Normal draw, then the fused policy tail writes the staging buffers
+                self.noise.normal_()
+                fused = pol.act_rollout(self.env.observations, self.noise, self.actions, self.logprob, self.value)
+            if not fused:
+                actions, logprob, _, value = self.policy(self.env.observations)
+                self.value.copy_(value.flatten())
+                self.actions.copy_(actions)
+                self.logprob.copy_(logprob)
         self.store(self.env.masks)
 
     def run(self, use_graph=True):
@@ -174,8 +185,16 @@ def _evaluate_graph(components, info):
     env_infos = defaultdict(list)
     vecenv = components.vecenv
     with profile.evaluate:
-        rs.store.reset(experience.ptr)
-        while not experience.full:
+        start = experience.ptr
+        rs.store.reset(start)
+        # a step stores at most num_agents rows, so the buffer cannot fill before `min_steps`:
+        # those steps run without a host read; after them the device cursor is read once per
+        # step (the reference's per-step mask.sum().item(), core.py:136, becomes the running
+        # sums counts[2:4] read once per evaluate)
+        n = max(1, rs.store.n)
+        min_steps = max(1, -(-(experience.batch_size - start) // n))
+        steps = 0
+        while True:
             with profile.env:
                 _, _, _, _, env_info, _, _ = vecenv.recv()
             for i in env_info:
@@ -185,11 +204,16 @@ def _evaluate_graph(components, info):
                 rs.run(train_cfg.rollout_graph)
             with profile.env:
                 vecenv.send(rs.actions)
-            with profile.eval_misc:
-                n_valid, taken = rs.store.counts.tolist()  # the reference's mask.sum().item()
-                info.global_step += n_valid
-                experience.ptr += taken
-                experience.step += 1
+            steps += 1
+            if steps >= min_steps:
+                with profile.eval_misc:
+                    if int(rs.store.cursor.item()) >= experience.batch_size:
+                        break
+        with profile.eval_misc:
+            n_valid, taken = rs.store.counts[2:4].tolist()
+            info.global_step += n_valid
+            experience.ptr = start + taken
+            experience.step += steps
         for k, v in env_infos.items():
             info.stats.extend(k, list(np.atleast_1d(v)))
     experience.ptr = 0
@@ -236,7 +260,14 @@ def compute_advantages(components, info):
     dones = experience.dones[idxs].contiguous()
     values = experience.values[idxs].contiguous()
     rewards = experience.rewards[idxs].contiguous()
-    experience.flatten_batch()
+    pol = components.policy.policy if hasattr(components.policy, "policy") else components.policy
+    experience.b_obs_half = None
+    if cfg.fused_obs and cfg.fused_loss and hasattr(pol, "obs_half_input") and experience.lstm_h is None:
+        # RunningNorm + rounding into the first GEMM operand for the whole batch, in minibatch
+        # order, once (the statistics are fixed during train(), scripts/train.py:337-346)
+        with autocast(cfg):
+            experience.b_obs_half = pol.obs_half_input(experience.obs, experience.b_idxs_obs.reshape(-1))
+    experience.flatten_batch(skip_obs=experience.b_obs_half is not None)
     adv_rew = torch.zeros((experience.num_minibatches, cfg.minibatch_size), device=cfg.device)
     discriminate = getattr(components.policy.policy, "discriminate", None) if hasattr(components.policy, "policy") \
         else None
@@ -265,6 +296,11 @@ def train(components, info, utilization=None):
     pol = components.policy.policy if hasattr(components.policy, "policy") else components.policy
     flat = components.flat_grads
     acc = torch.zeros(12, dtype=torch.float64, device=cfg.device)  # device-side loss accumulators
+    # fused path: the PPO kernel's 7 logged means and the optimizer's [norm sum, norm, l2]
+    acc_ppo = torch.zeros(7, dtype=torch.float64, device=cfg.device)
+    acc_opt = torch.zeros(3, dtype=torch.float64, device=cfg.device)
+    opt_l2 = isinstance(components.optimizer, FlatAdam) and components.optimizer.param_init is not None \
+        and cfg.l2_reg_coef == 0
     with profile.train:
         with profile.train_misc:
             compute_advantages(components, info)
@@ -272,13 +308,18 @@ def train(components, info, utilization=None):
                 amp_obs_demo = components.vecenv.fetch_amp_obs_demo()
                 amp_mb = amp_obs_demo.shape[0]
         total_minibatches = experience.num_minibatches * cfg.update_epochs
+        adv_ms = None
         fused_loss = (cfg.fused_loss and hasattr(pol, "forward_train") and getattr(pol, "fused", False)
                       and experience.lstm_h is None)
         obs_dim = components.vecenv.single_observation_space.shape[0]
         for _epoch in range(cfg.update_epochs):
             for mb in range(experience.num_minibatches):
                 with profile.train_misc:
-                    obs = experience.b_obs[mb].reshape(-1, obs_dim)
+                    if experience.b_obs_half is not None:
+                        mbs = experience.minibatch_size
+                        obs = experience.b_obs_half[mb * mbs:(mb + 1) * mbs]
+                    else:
+                        obs = experience.b_obs[mb].reshape(-1, obs_dim)
                     atn = experience.b_actions[mb].reshape(-1, experience.b_actions.shape[-1])
                     log_probs = experience.b_logprobs[mb].reshape(-1)
                     val = experience.b_values[mb]
@@ -293,9 +334,12 @@ def train(components, info, utilization=None):
                 with profile.train_misc:
                     adv = adv.reshape(-1)
                     if fused_obj:
-                        # PPO objective in two HIP kernels (clean_pufferl/ppo_loss.py)
+                        # PPO objective in two HIP kernels (clean_pufferl/ppo_loss.py); the
+                        # per-minibatch advantage mean / std of every minibatch at once
                         if cfg.norm_adv:
-                            mean, std = D.global_mean_std(adv)
+                            if adv_ms is None:
+                                adv_ms = D.global_mean_std_rows(experience.b_advantages)
+                            mean, std = adv_ms[mb], None
                         else:
                             mean, std = 0.0, 1.0
                         loss, st = ppo_objective(mu, newvalue, pol.sigma, atn, log_probs, adv, mean, std, val, ret,
@@ -340,8 +384,8 @@ def train(components, info, utilization=None):
                         mbl = getattr(pol, "mean_bound_loss", None)
                         if cfg.bound_coef > 0 and mbl is not None:
                             loss = loss + mbl * cfg.bound_coef
-                    l2 = _l2_init_reg(list(components.policy.named_parameters()), info.initial_params,
-                                      cfg.l2_reg_coef > 0)
+                    l2 = None if opt_l2 else _l2_init_reg(list(components.policy.named_parameters()),
+                                                          info.initial_params, cfg.l2_reg_coef > 0)
                     if cfg.l2_reg_coef > 0:
                         loss = loss + l2 * cfg.l2_reg_coef
                 with profile.learn:
@@ -366,6 +410,12 @@ def train(components, info, utilization=None):
                             components.skipped_steps += (found > 0).long()  # device-side count, no sync
                         scaler.update()
                 with profile.train_misc, torch.no_grad():
+                    if fused_obj and opt_l2 and not info.use_amp_obs:
+                        acc_ppo += st  # pg, v, ent, old_kl, kl, clipfrac, bound (ppo_loss.py)
+                        acc_opt += components.optimizer.norms  # norm sum, total norm, l2
+                        continue
+                    if l2 is None:
+                        l2 = components.optimizer.norms[2]
                     acc += torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,
                                         approx_kl, clipfrac, gnorm, l2.detach(), disc_loss.detach(),
                                         (mbl.detach() if mbl is not None else torch.zeros((), device=cfg.device)),
@@ -374,6 +424,9 @@ def train(components, info, utilization=None):
             if cfg.target_kl is not None and float(approx_kl) > cfg.target_kl:
                 break
         with profile.train_misc:
+            p7, o3 = acc_ppo / total_minibatches, acc_opt / total_minibatches
+            acc[[0, 1, 2, 3, 4, 5, 9]] += p7
+            acc[[6, 7]] += o3[[0, 2]]
             a = acc.cpu().numpy()
             losses = LossComponents(policy_loss=a[0], value_loss=a[1], entropy=a[2], old_approx_kl=a[3],
                                     approx_kl=a[4], clipfrac=a[5], before_clip_grad_norm=a[6],

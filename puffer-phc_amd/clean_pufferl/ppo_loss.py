@@ -35,8 +35,11 @@ def ppo_objective(mu, value, log_sigma, actions, old_logprob, adv, adv_mean, adv
                   soft_bound):
     coefs = _native.ppo_coefs(cfg.clip_coef, cfg.vf_clip_coef, cfg.vf_coef, cfg.ent_coef,
                               cfg.bound_coef if cfg.bound_coef > 0 else 0.0, soft_bound, cfg.clip_vloss)
-    ms = torch.stack([torch.as_tensor(adv_mean, dtype=torch.float32, device=mu.device).reshape(()),
-                      torch.as_tensor(adv_std, dtype=torch.float32, device=mu.device).reshape(())])
+    if adv_std is None:  # adv_mean is already the device [2] (mean, std) pair
+        ms = adv_mean
+    else:
+        ms = torch.stack([torch.as_tensor(adv_mean, dtype=torch.float32, device=mu.device).reshape(()),
+                          torch.as_tensor(adv_std, dtype=torch.float32, device=mu.device).reshape(())])
     f = lambda t: t.detach().float().contiguous().reshape(-1)  # noqa: E731
     return _PPOObjective.apply(mu.float().contiguous(), value.float().reshape(-1), log_sigma.detach().float(),
                                actions.detach().float().contiguous(), f(old_logprob), f(adv), ms, f(old_value),

@@ -106,9 +106,11 @@ class Experience:
         self.b_idxs_flat = self.b_idxs.reshape(self.num_minibatches, self.minibatch_size)
         return idxs
 
-    def flatten_batch(self):
+    def flatten_batch(self, skip_obs=False):
+        """Gather the training tensors in minibatch order (structs.py:146-160); skip_obs when the
+        trainer reads the observations through its own normalised copy instead."""
         b_idxs, b_flat = self.b_idxs, self.b_idxs_flat
-        self.b_obs = self.obs[self.b_idxs_obs]
+        self.b_obs = None if skip_obs else self.obs[self.b_idxs_obs]
         self.b_actions = self.actions[b_idxs].contiguous()
         self.b_logprobs = self.logprobs[b_idxs]
         self.b_dones = self.dones[b_idxs]

@@ -187,3 +187,9 @@ class TrainConfig(DeviceConfig):
     # PPO objective (ratio / clipping / value / bound losses and their gradients) in two HIP
     # kernels (clean_pufferl/ppo_loss.py); False = the reference's eager expression
     fused_loss: bool = True
+    # rollout inference tail (LayerNorm+SiLU, mu / value heads, Normal sample, log_prob) in one
+    # HIP kernel (phc_policy_act) on the half-precision MFMA path; False = the policy module
+    fused_act: bool = True
+    # train(): normalise + round the whole batch's observations into the first GEMM's half
+    # operand once per call, in minibatch order (phc_obs_half); False = per minibatch, fp32
+    fused_obs: bool = True

@@ -7,7 +7,7 @@
 // 10-61 under torch autograd) runs on the accumulator tile before it leaves the CU:
 //   PHC_EPI_STORE     : out = acc
 //   PHC_EPI_BIAS      : out = acc + bias
-//   PHC_EPI_BIAS_SILU : pre = acc + bias (aux, fp32, nullable), out = silu(pre)
+//   PHC_EPI_BIAS_SILU : pre = acc + bias (aux, fp32 or the operand type, nullable), out = silu(pre)
 //   PHC_EPI_SILU_GRAD : out = acc * silu'(aux + bias) (bias nullable: aux is then the whole
 //                       pre-activation, as BIAS_SILU writes it); bias_grad = column sums of out
 // so no fp32 GEMM output makes an HBM round trip through a separate elementwise kernel.
@@ -48,7 +48,36 @@ struct GemmArgs {
   float *partial;
   int tiles_m, tiles_n;
   int discard;
+  int aux_half;  // aux in the operand type T instead of fp32
 };
+
+// 4 consecutive aux values (fp32, or the operand type T when g.aux_half) at element offset off
+template <typename T> __device__ __forceinline__ float4 aux_load4(const GemmArgs &g, int64_t off) {
+  if (g.aux_half) {
+    const uint2 raw = *reinterpret_cast<const uint2 *>(static_cast<const T *>(g.aux) + off);
+    T h[4];
+    __builtin_memcpy(h, &raw, sizeof(raw));
+    return float4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  }
+  return *reinterpret_cast<const float4 *>(static_cast<const float *>(g.aux) + off);
+}
+template <typename T> __device__ __forceinline__ float aux_load1(const GemmArgs &g, int64_t off) {
+  return g.aux_half ? (float)static_cast<const T *>(g.aux)[off] : static_cast<const float *>(g.aux)[off];
+}
+template <typename T> __device__ __forceinline__ void aux_store4(const GemmArgs &g, int64_t off, const float v[4]) {
+  if (g.aux_half) {
+    const T h[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+    uint2 raw;
+    __builtin_memcpy(&raw, h, sizeof(raw));
+    *reinterpret_cast<uint2 *>(static_cast<T *>(g.aux) + off) = raw;
+  } else {
+    *reinterpret_cast<float4 *>(static_cast<float *>(g.aux) + off) = float4{v[0], v[1], v[2], v[3]};
+  }
+}
+template <typename T> __device__ __forceinline__ void aux_store1(const GemmArgs &g, int64_t off, float v) {
+  if (g.aux_half) static_cast<T *>(g.aux)[off] = (T)v;
+  else static_cast<float *>(g.aux)[off] = v;
+}
 
 // element offset of (row, logical column c) in a twin tensor of tg groups x tc columns
 __device__ __forceinline__ int64_t gemm_twin_off(const GemmArgs &g, int layout, int64_t row, int c) {
@@ -278,7 +307,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int64_t row = prow0 + rg + kRowGroups * (i0 + u);
-            av[u] = *reinterpret_cast<const float4 *>(static_cast<const float *>(g.aux) + ab + row * as);
+            av[u] = aux_load4<T>(g, ab + row * as);
           }
         }
 #pragma unroll
@@ -300,9 +329,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] += bias4[q];
             if constexpr (EPI == PHC_EPI_BIAS_SILU) {
-              if (g.aux)
-                *reinterpret_cast<float4 *>(static_cast<float *>(g.aux) + ab + row * as) =
-                    float4{v[0], v[1], v[2], v[3]};
+              if (g.aux) aux_store4<T>(g, ab + row * as, v);
 #pragma unroll
               for (int q = 0; q < 4; ++q) v[q] = gemm_silu(v[q]);
             }
@@ -321,13 +348,12 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
       float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       const int lc = bt * g.n + gcol;
       if constexpr (EPI == PHC_EPI_SILU_GRAD) {
-        const float *aux = static_cast<const float *>(g.aux);
         if (vec) {
-          const float4 av = *reinterpret_cast<const float4 *>(aux + gemm_twin_off(g, g.aux_layout, row, lc));
+          const float4 av = aux_load4<T>(g, gemm_twin_off(g, g.aux_layout, row, lc));
           a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
         } else {
           for (int q = 0; q < 4; ++q)
-            if (gcol + q < g.n) a[q] = aux[gemm_twin_off(g, g.aux_layout, row, lc + q)];
+            if (gcol + q < g.n) a[q] = aux_load1<T>(g, gemm_twin_off(g, g.aux_layout, row, lc + q));
         }
       }
 #pragma unroll
@@ -345,16 +371,14 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
       }
       if (vec) {
         if constexpr (EPI == PHC_EPI_BIAS_SILU) {
-          if (g.aux)
-            *reinterpret_cast<float4 *>(static_cast<float *>(g.aux) + gemm_twin_off(g, g.aux_layout, row, lc)) =
-                float4{a[0], a[1], a[2], a[3]};
+          if (g.aux) aux_store4<T>(g, gemm_twin_off(g, g.aux_layout, row, lc), a);
         }
         gemm_store4<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, lc), v);
       } else {
         for (int q = 0; q < 4; ++q) {
           if (gcol + q >= g.n) break;
           if constexpr (EPI == PHC_EPI_BIAS_SILU) {
-            if (g.aux) static_cast<float *>(g.aux)[gemm_twin_off(g, g.aux_layout, row, lc + q)] = a[q];
+            if (g.aux) aux_store1<T>(g, gemm_twin_off(g, g.aux_layout, row, lc + q), a[q]);
           }
           gemm_store<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, lc + q), v[q]);
         }
@@ -480,6 +504,7 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   PHC_REQUIRE(!(d->epilogue == PHC_EPI_BIAS || d->epilogue == PHC_EPI_BIAS_SILU) || d->bias,
               "twin_gemm: epilogue needs the bias");
   PHC_REQUIRE(d->epilogue != PHC_EPI_SILU_GRAD || d->aux, "twin_gemm: SILU_GRAD needs the pre-activation (aux)");
+  PHC_REQUIRE(d->aux_dtype == PHC_DT_F32 || d->aux_dtype == d->dtype, "twin_gemm: aux must be f32 or the operand type");
   PHC_REQUIRE(!bias_grad || (d->epilogue == PHC_EPI_SILU_GRAD && workspace),
               "twin_gemm: bias_grad needs the SILU_GRAD epilogue and a workspace");
   const int cfg = gemm_config(d->m, d->n, d->batch);
@@ -503,6 +528,7 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   g.bias = d->bias;
   g.aux = d->aux;
   g.aux_layout = d->aux_layout;
+  g.aux_half = d->aux_dtype == d->dtype ? 1 : 0;
   g.out = d->out;
   g.out_layout = d->out_layout;
   g.tg = d->twin_groups;

@@ -18,60 +18,81 @@ constexpr int kOptBlock = 256;
 
 // partial sums of squares (double) and a non-finite flag per block of the flat gradient; the
 // block table maps block i -> [start, end) inside one parameter segment
+// With p0 (the initial parameters) the block also sums (p - p0)^2 for the L2-init
+// regulariser the reference logs every minibatch (core.py:352-359), on the parameters before
+// this step's update, as the reference evaluates it.
 __global__ __launch_bounds__(kOptBlock) void k_grad_partials(const float *__restrict__ g,
                                                              const int64_t *__restrict__ blk_range,
                                                              double *__restrict__ part_sq,
-                                                             int *__restrict__ part_bad) {
-  __shared__ double red[kOptBlock / 64];
+                                                             int *__restrict__ part_bad,
+                                                             const float *__restrict__ p,
+                                                             const float *__restrict__ p0,
+                                                             double *__restrict__ part_l2) {
+  __shared__ double red[kOptBlock / 64], red_l2[kOptBlock / 64];
   __shared__ int bad_s[kOptBlock / 64];
   const int64_t s = blk_range[2 * blockIdx.x], e = blk_range[2 * blockIdx.x + 1];
-  double acc = 0.0;
+  double acc = 0.0, l2 = 0.0;
   int bad = 0;
   for (int64_t i = s + threadIdx.x; i < e; i += kOptBlock) {
     const float v = g[i];
     bad |= !__builtin_isfinite(v);
     acc += (double)v * (double)v;
+    if (p0) {
+      const double d = (double)p[i] - (double)p0[i];
+      l2 += d * d;
+    }
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     acc += __shfl_xor(acc, o, 64);
+    l2 += __shfl_xor(l2, o, 64);
     bad |= __shfl_xor(bad, o, 64);
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) {
     red[w] = acc;
+    red_l2[w] = l2;
     bad_s[w] = bad;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     part_sq[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
     part_bad[blockIdx.x] = bad_s[0] | bad_s[1] | bad_s[2] | bad_s[3];
+    if (p0) part_l2[blockIdx.x] = ((red_l2[0] + red_l2[1]) + red_l2[2]) + red_l2[3];
   }
 }
 
 // one wave: per-segment norms (segment j owns blocks [seg_blk[j], seg_blk[j+1])), clip
 // coefficient, skip decision, loss-scale update, Adam step / bias corrections -> st
 __global__ __launch_bounds__(64) void k_opt_finish(const double *__restrict__ part_sq, const int *__restrict__ part_bad,
+                                                   const double *__restrict__ part_l2,
+                                                   const int64_t *__restrict__ blk_range,
                                                    const int32_t *__restrict__ seg_blk, int nseg,
                                                    phc_adam_params hp, phc_opt_state *__restrict__ st,
                                                    float *__restrict__ norm_out) {
   const int lane = threadIdx.x;
   const float inv = hp.use_loss_scale ? 1.0f / st->loss_scale : 1.0f;
-  double tot = 0.0, norm_sum = 0.0;
+  double tot = 0.0, norm_sum = 0.0, l2 = 0.0;
   int bad = 0;
   for (int j = lane; j < nseg; j += 64) {  // segment sums in block order
-    double sq = 0.0;
+    double sq = 0.0, dl = 0.0;
     for (int b = seg_blk[j]; b < seg_blk[j + 1]; ++b) {
       sq += part_sq[b];
       bad |= part_bad[b];
+      if (part_l2) dl += part_l2[b];
     }
     tot += sq;
     norm_sum += sqrt(sq) * (double)inv;
+    if (part_l2 && seg_blk[j + 1] > seg_blk[j]) {  // mean over the parameter's elements
+      const int64_t n = blk_range[2 * (seg_blk[j + 1] - 1) + 1] - blk_range[2 * seg_blk[j]];
+      l2 += dl / (double)n;
+    }
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     tot += __shfl_xor(tot, o, 64);
     norm_sum += __shfl_xor(norm_sum, o, 64);
+    l2 += __shfl_xor(l2, o, 64);
     bad |= __shfl_xor(bad, o, 64);
   }
   if (lane != 0) return;
@@ -101,6 +122,7 @@ __global__ __launch_bounds__(64) void k_opt_finish(const double *__restrict__ pa
   if (norm_out) {
     norm_out[0] = (float)norm_sum;
     norm_out[1] = total_norm;
+    if (part_l2) norm_out[2] = (float)l2;
   }
 }
 
@@ -142,16 +164,70 @@ __global__ __launch_bounds__(kOptBlock) void k_adam(float *__restrict__ p, const
   }
 }
 
+// ---------------------------------------------------------------- reduce_into --
+// dst[r, c] (+)= sum_{s < parts} src[s * part_stride + r * src_ld + c], parts summed in order:
+// split-K weight-gradient partials (and plain strided copies) written straight into a flat
+// gradient buffer's per-parameter views, many jobs per launch.
+struct ReduceJobs {
+  phc_reduce_job j[PHC_MAX_REDUCE_JOBS];
+  int64_t first_block[PHC_MAX_REDUCE_JOBS + 1];
+  int n;
+};
+constexpr int kRedThreads = 256, kRedPerThread = 4;
+
+__global__ __launch_bounds__(kRedThreads) void k_reduce_into(ReduceJobs js) {
+  int q = 0;
+  while (q + 1 < js.n && (int64_t)blockIdx.x >= js.first_block[q + 1]) ++q;
+  const phc_reduce_job &job = js.j[q];
+  const int64_t total = job.rows * job.cols;
+  const int64_t base = ((int64_t)blockIdx.x - js.first_block[q]) * kRedThreads * kRedPerThread + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < kRedPerThread; ++u) {
+    const int64_t i = base + (int64_t)u * kRedThreads;
+    if (i >= total) break;
+    const int64_t r = i / job.cols, c = i - r * job.cols;
+    const float *src = job.src + r * job.src_ld + c;
+    float acc = src[0];
+    for (int s = 1; s < job.parts; ++s) acc += src[s * job.part_stride];
+    if (job.accumulate) job.dst[i] += acc;
+    else job.dst[i] = acc;
+  }
+}
+
 }  // namespace phc
 
 using namespace phc;
+
+extern "C" int phc_reduce_into(const phc_reduce_job *jobs, int32_t num_jobs, void *stream) {
+  PHC_REQUIRE(jobs && num_jobs >= 0 && num_jobs <= PHC_MAX_REDUCE_JOBS, "reduce_into: 0..%d jobs",
+              PHC_MAX_REDUCE_JOBS);
+  ReduceJobs js{};
+  int64_t blocks = 0;
+  int n = 0;
+  for (int q = 0; q < num_jobs; ++q) {
+    const phc_reduce_job &j = jobs[q];
+    PHC_REQUIRE(j.rows >= 0 && j.cols >= 0 && j.parts >= 1 && j.src_ld >= j.cols, "reduce_into: job %d bad shape", q);
+    if (j.rows * j.cols == 0) continue;
+    PHC_REQUIRE(j.src && j.dst, "reduce_into: job %d null pointer", q);
+    js.j[n] = j;
+    js.first_block[n] = blocks;
+    blocks += (j.rows * j.cols + kRedThreads * kRedPerThread - 1) / (kRedThreads * kRedPerThread);
+    ++n;
+  }
+  if (n == 0) return PHC_OK;
+  js.first_block[n] = blocks;
+  js.n = n;
+  PHC_REQUIRE(blocks < (1ll << 31), "reduce_into: too large");
+  hipLaunchKernelGGL(k_reduce_into, dim3((unsigned)blocks), dim3(kRedThreads), 0, as_stream(stream), js);
+  return check_launch("reduce_into");
+}
 
 extern "C" int64_t phc_opt_block_elems(void) { return 16384; }
 
 extern "C" int phc_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                             const int64_t *blk_range, int32_t nblk, const int32_t *seg_blk, int32_t nseg,
-                            const phc_adam_params *hp, phc_opt_state *state, float *norm_out, void *workspace,
-                            void *stream) {
+                            const phc_adam_params *hp, phc_opt_state *state, float *norm_out,
+                            const float *param_init, void *workspace, void *stream) {
   PHC_REQUIRE(param && grad && exp_avg && exp_avg_sq && blk_range && seg_blk && hp && state && workspace,
               "opt_step: null argument");
   PHC_REQUIRE(n > 0 && nblk > 0 && nseg > 0, "opt_step: empty parameter set");
@@ -161,11 +237,12 @@ extern "C" int phc_opt_step(float *param, const float *grad, float *exp_avg, flo
   PHC_REQUIRE(!hp->use_loss_scale || hp->growth_interval > 0, "opt_step: bad loss-scale growth interval");
   hipStream_t st = as_stream(stream);
   double *part_sq = static_cast<double *>(workspace);
-  int *part_bad = reinterpret_cast<int *>(part_sq + nblk);
+  double *part_l2 = param_init ? part_sq + nblk : nullptr;
+  int *part_bad = reinterpret_cast<int *>(part_sq + 2 * (int64_t)nblk);
   hipLaunchKernelGGL(k_grad_partials, dim3((unsigned)nblk), dim3(kOptBlock), 0, st, grad, blk_range, part_sq,
-                     part_bad);
-  hipLaunchKernelGGL(k_opt_finish, dim3(1), dim3(64), 0, st, part_sq, part_bad, seg_blk, (int)nseg, *hp, state,
-                     norm_out);
+                     part_bad, param, param_init, part_l2);
+  hipLaunchKernelGGL(k_opt_finish, dim3(1), dim3(64), 0, st, part_sq, part_bad, part_l2, blk_range, seg_blk,
+                     (int)nseg, *hp, state, norm_out);
   const int64_t quads = (n + 3) / 4;
   const int64_t blocks = std::min<int64_t>((quads + kOptBlock - 1) / kOptBlock, 4096);
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptBlock), 0, st, param, grad, exp_avg, exp_avg_sq, n,
@@ -174,5 +251,5 @@ extern "C" int phc_opt_step(float *param, const float *grad, float *exp_avg, flo
 }
 
 extern "C" size_t phc_opt_workspace_bytes(int32_t nblk) {
-  return nblk <= 0 ? 0 : (size_t)nblk * (sizeof(double) + sizeof(int)) + 16;
+  return nblk <= 0 ? 0 : (size_t)nblk * (2 * sizeof(double) + sizeof(int)) + 16;
 }

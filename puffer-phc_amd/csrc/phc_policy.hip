@@ -1,0 +1,244 @@
+// phc_policy.hip — the PHCPolicy pieces around the twin-trunk GEMMs (R17, R19).
+//
+// phc_obs_half: RunningNorm forward (policies/running_norm.py:15-20: clamp((x - mean) /
+//   sqrt(var + eps), -clip, clip)) of float32 observation rows — optionally gathered through a
+//   row index (the trainer's env-major minibatch order, clean_pufferl/structs.py:146-160) —
+//   rounded once into the f16 / bf16 operand of the first trunk GEMM, zero-padded to its
+//   K % 64 == 0 width.  One pass replaces normalize + cast + pad (+ gather).
+//
+// phc_policy_act: the rollout's inference tail after the trunks (policies/phc_policy.py:40-61,
+//   discriminator_policy.py:55-67, pufferlib sample_logits): per row, LayerNorm + SiLU of both
+//   trunks' last Linear outputs, mu = W_mu h_actor + b_mu (512 -> 69), value = w_v h_critic + b_v,
+//   action = mu + std * noise (std = exp(sigma), clamped to 1e-6 in deterministic mode),
+//   logprob = sum_j Normal(mu, std).log_prob(action) — one launch instead of a LayerNorm kernel,
+//   two GEMMs and ~20 elementwise / reduction launches.  Rows are independent; a 320-thread
+//   block owns kActRows rows: LayerNorm one row per wave at a time (64 lanes x H/64 values), the
+//   actor's h rows kept in LDS, W_mu streamed through LDS in 64-deep k chunks, each thread
+//   accumulating 4 rows x 1 action of mu in fp32 (float4 LDS reads, 16 FMAs per 4-deep step).
+#include "phc_common.h"
+
+namespace phc {
+
+// ----------------------------------------------------------------- obs_half --
+template <typename T>
+__global__ __launch_bounds__(256) void k_obs_half(const float *__restrict__ obs, const int64_t *__restrict__ rows,
+                                                  int64_t m, int d, int ldo, const float *__restrict__ mean,
+                                                  const float *__restrict__ var, float eps, float clip,
+                                                  T *__restrict__ out) {
+  const int chunks = ldo / 8;  // 8 outputs (16 B) per thread; m * chunks < 2^31 (host check)
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int)m * chunks) return;
+  const int r = i / chunks;
+  const int c0 = (i - r * chunks) * 8;
+  const int64_t src = rows ? rows[r] : r;
+  const float *x = obs + src * d;
+  T o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e;
+    float v = 0.0f;
+    if (c < d) {
+      v = (x[c] - mean[c]) / sqrtf(var[c] + eps);  // same expression as k_rms_normalize
+      v = v < -clip ? -clip : (v > clip ? clip : v);
+    }
+    o[e] = (T)v;
+  }
+  uint4 raw;
+  __builtin_memcpy(&raw, o, sizeof(raw));
+  *reinterpret_cast<uint4 *>(out + (int64_t)r * ldo + c0) = raw;
+}
+
+// --------------------------------------------------------------- policy_act --
+constexpr int kActRows = 16;     // rows per block
+constexpr int kActK = 64;        // k chunk of W_mu staged in LDS
+constexpr int kActMaxA = 72;     // actions supported (PHC_NUM_DOF + 3)
+constexpr int kActThreads = 320; // (kActRows / 4) row groups x up to 72 actions, 5 waves
+static_assert((kActRows / 4) * kActMaxA <= kActThreads, "one (row group, action) per thread");
+static_assert(kActMaxA * (kActK + 4) >= kActRows * kActMaxA, "log_prob terms reuse wts");
+
+__device__ __forceinline__ float wave_sum(float s) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  return s;
+}
+
+// LayerNorm + SiLU of one H-wide row held as C x 4 values per lane (lane-strided float4 chunks),
+// the same arithmetic as k_ln_silu_fwd
+template <int C>
+__device__ __forceinline__ void ln_silu_row(float x[C][4], const float *__restrict__ gamma,
+                                            const float *__restrict__ beta, int lane, float eps) {
+  constexpr int H = C * 256;
+  float s = 0.0f;
+#pragma unroll
+  for (int k = 0; k < C; ++k) s += (x[k][0] + x[k][1]) + (x[k][2] + x[k][3]);
+  const float mean = wave_sum(s) / (float)H;
+  float v = 0.0f;
+#pragma unroll
+  for (int k = 0; k < C; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float dd = x[k][e] - mean;
+      v += dd * dd;
+    }
+  const float rstd = rsqrtf(wave_sum(v) / (float)H + eps);
+#pragma unroll
+  for (int k = 0; k < C; ++k) {
+    const int c = 4 * (lane + 64 * k);
+    // gamma / beta may be views into a flat parameter buffer: 4-byte alignment only
+    const float g4[4] = {gamma[c], gamma[c + 1], gamma[c + 2], gamma[c + 3]};
+    const float b4[4] = {beta[c], beta[c + 1], beta[c + 2], beta[c + 3]};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float ln = (x[k][e] - mean) * rstd * g4[e] + b4[e];
+      x[k][e] = ln / (1.0f + expf(-ln));
+    }
+  }
+}
+
+template <int C>
+__global__ __launch_bounds__(kActThreads) void k_policy_act(phc_policy_act_args a) {
+  constexpr int H = C * 256;
+  constexpr int kWs = kActK + 4;  // padded row of the staged W_mu chunk ([j][k]: float4 reads conflict-free)
+  __shared__ __attribute__((aligned(16))) float hs[kActRows][H];
+  __shared__ __attribute__((aligned(16))) float wts[kActMaxA][kWs];
+  __shared__ float red[kActRows];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * kActRows;
+  const int A = a.num_actions;
+  const float *y = a.trunk_out;
+
+  // LayerNorm + SiLU: rows of both trunks, one wave per row
+  for (int q = wave; q < 2 * kActRows; q += kActThreads / 64) {
+    const int grp = q / kActRows, rr = q % kActRows;
+    const int64_t row = r0 + rr;
+    if (row >= a.rows) continue;
+    float x[C][4];
+    const float *src = y + ((int64_t)grp * a.rows + row) * H;
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const float4 t = *reinterpret_cast<const float4 *>(src + 4 * (lane + 64 * k));
+      x[k][0] = t.x; x[k][1] = t.y; x[k][2] = t.z; x[k][3] = t.w;
+    }
+    ln_silu_row<C>(x, a.ln_gamma[grp], a.ln_beta[grp], lane, a.ln_eps);
+    if (grp == 0) {
+#pragma unroll
+      for (int k = 0; k < C; ++k)
+        *reinterpret_cast<float4 *>(&hs[rr][4 * (lane + 64 * k)]) = float4{x[k][0], x[k][1], x[k][2], x[k][3]};
+    } else {
+      float s = 0.0f;
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        const float *w = a.w_value + 4 * (lane + 64 * k);
+        s += x[k][0] * w[0] + x[k][1] * w[1] + x[k][2] * w[2] + x[k][3] * w[3];
+      }
+      s = wave_sum(s);
+      if (lane == 0) red[rr] = s + a.b_value[0];
+    }
+  }
+  __syncthreads();
+  if (tid < kActRows && r0 + tid < a.rows) a.value[r0 + tid] = red[tid];
+
+  // mu head: thread (g, j) owns rows 4g..4g+3 of action j; per 4-deep k step one float4 of its
+  // W_mu row and one broadcast float4 of each h row, 16 FMAs
+  const int g = tid / A, j = tid - g * A;
+  const bool active = g < kActRows / 4;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int k0 = 0; k0 < H; k0 += kActK) {
+    __syncthreads();  // previous chunk no longer read
+    for (int e = tid; e < kActK * A; e += kActThreads) {
+      const int jj = e / kActK, kk = e - jj * kActK;
+      wts[jj][kk] = a.w_mu[(int64_t)jj * H + k0 + kk];  // coalesced along k
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll 4
+      for (int kk = 0; kk < kActK; kk += 4) {
+        const float4 w = *reinterpret_cast<const float4 *>(&wts[j][kk]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float4 h = *reinterpret_cast<const float4 *>(&hs[4 * g + r][k0 + kk]);
+          acc[r] += h.x * w.x;
+          acc[r] += h.y * w.y;
+          acc[r] += h.z * w.z;
+          acc[r] += h.w * w.w;
+        }
+      }
+    }
+  }
+  // action / logprob: the Normal's log_prob terms per (row, action), summed per row in a fixed
+  // order (deterministic: a captured rollout graph and the eager step give identical bits)
+  __syncthreads();  // wts no longer read: reused as the [kActRows][A] log_prob terms
+  float *lps = &wts[0][0];
+  const float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+  if (active) {
+    float sd = expf(a.log_sigma[j]);
+    sd = sd > a.std_max ? a.std_max : sd;
+    const float bj = a.b_mu[j];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = 4 * g + r;
+      const int64_t row = r0 + rr;
+      if (row >= a.rows) break;
+      const float mu = acc[r] + bj;
+      const float act = mu + sd * a.noise[row * A + j];
+      const float d = act - mu;
+      lps[rr * A + j] = -(d * d) / (2.0f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
+      a.actions[row * A + j] = act;
+      if (a.mu) a.mu[row * A + j] = mu;
+    }
+  }
+  __syncthreads();
+  if (tid < kActRows && r0 + tid < a.rows) {
+    float s = 0.0f;
+    for (int jj = 0; jj < A; ++jj) s += lps[tid * A + jj];
+    a.logprob[r0 + tid] = s;
+  }
+}
+
+}  // namespace phc
+
+using namespace phc;
+
+extern "C" int phc_obs_half(const float *obs, const int64_t *rows, int64_t m, int32_t d, const float *mean,
+                            const float *var, float eps, float clip, void *out, int32_t ld_out, int32_t dtype,
+                            void *stream) {
+  PHC_REQUIRE(m >= 0 && d > 0 && ld_out >= d && ld_out % 8 == 0, "obs_half: bad shape (ld_out >= d, ld_out %% 8 == 0)");
+  if (m == 0) return PHC_OK;
+  PHC_REQUIRE(obs && mean && var && out, "obs_half: null argument");
+  PHC_REQUIRE((reinterpret_cast<uintptr_t>(out) & 15) == 0, "obs_half: out must be 16-byte aligned");
+  PHC_REQUIRE(dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "obs_half: dtype must be f16 or bf16");
+  const int64_t threads = m * (ld_out / 8);
+  PHC_REQUIRE(threads < (1ll << 31) - 256, "obs_half: too many rows");
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  hipStream_t st = as_stream(stream);
+  if (dtype == PHC_DT_F16)
+    hipLaunchKernelGGL(k_obs_half<_Float16>, grid, dim3(256), 0, st, obs, rows, m, (int)d, (int)ld_out, mean, var,
+                       eps, clip, static_cast<_Float16 *>(out));
+  else
+    hipLaunchKernelGGL(k_obs_half<__bf16>, grid, dim3(256), 0, st, obs, rows, m, (int)d, (int)ld_out, mean, var,
+                       eps, clip, static_cast<__bf16 *>(out));
+  return check_launch("obs_half");
+}
+
+extern "C" int phc_policy_act(const phc_policy_act_args *args, void *stream) {
+  PHC_REQUIRE(args, "policy_act: null args");
+  const phc_policy_act_args &a = *args;
+  PHC_REQUIRE(a.trunk_out && a.ln_gamma[0] && a.ln_beta[0] && a.ln_gamma[1] && a.ln_beta[1] && a.w_mu && a.b_mu && a.w_value && a.b_value && a.log_sigma &&
+                  a.noise && a.actions && a.logprob && a.value,
+              "policy_act: null argument");
+  PHC_REQUIRE(a.rows >= 0, "policy_act: bad rows");
+  PHC_REQUIRE(a.hidden == 256 || a.hidden == 512 || a.hidden == 768 || a.hidden == 1024,
+              "policy_act: hidden must be 256, 512, 768 or 1024");
+  PHC_REQUIRE(a.num_actions >= 1 && a.num_actions <= kActMaxA, "policy_act: 1..%d actions", kActMaxA);
+  PHC_REQUIRE((reinterpret_cast<uintptr_t>(a.trunk_out) & 15) == 0, "policy_act: trunk_out must be 16-byte aligned");
+  if (a.rows == 0) return PHC_OK;
+  const dim3 grid((unsigned)((a.rows + kActRows - 1) / kActRows));
+  hipStream_t st = as_stream(stream);
+  switch (a.hidden / 256) {
+    case 1: hipLaunchKernelGGL(k_policy_act<1>, grid, dim3(kActThreads), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(k_policy_act<2>, grid, dim3(kActThreads), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(k_policy_act<3>, grid, dim3(kActThreads), 0, st, a); break;
+    default: hipLaunchKernelGGL(k_policy_act<4>, grid, dim3(kActThreads), 0, st, a); break;
+  }
+  return check_launch("policy_act");
+}

@@ -4,7 +4,7 @@
 // (`idx = nonzero(mask)`, CPU copies, a host-side ptr).  Here one scan block ranks the mask,
 // clamps to the remaining capacity and advances a DEVICE cursor; a copy kernel moves every
 // field of every taken row.  No host value enters the launch, so the whole rollout step can be
-// replayed from a hipGraph; the host reads back {n_valid, taken} once per step.
+// replayed from a hipGraph; running sums of {n_valid, taken} let the host read back once per rollout.
 #include "phc_common.h"
 
 namespace phc {
@@ -53,6 +53,8 @@ __global__ __launch_bounds__(kScanThreads) void k_rank_mask(const uint8_t *__res
     const int64_t take = total < room ? total : room;
     counts[0] = total;
     counts[1] = take;
+    counts[2] += total;  // running sums since the caller last zeroed them: the rollout loop
+    counts[3] += take;   // reads these once per evaluate() instead of {n_valid, taken} per step
     ws[0] = start;
     *cursor = start + take;
   }

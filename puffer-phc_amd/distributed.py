@@ -111,6 +111,22 @@ def global_mean_std(x):
     return mean.float(), var.clamp_min(0).sqrt().float()
 
 
+def global_mean_std_rows(x):
+    """[rows, 2] (mean, unbiased std) of each row of x over all ranks' copies of that row — the
+    per-minibatch advantage statistics of a whole train() call in one reduction (and one
+    all-reduce), instead of two reductions (and an all-reduce) per minibatch."""
+    if not is_dist():
+        return torch.stack([x.mean(1), x.std(1)], 1).contiguous()
+    xd = x.double()
+    buf = torch.stack([xd.sum(1), (xd * xd).sum(1),
+                       torch.full((x.shape[0],), float(x.shape[1]), dtype=torch.float64, device=x.device)], 1)
+    dist.all_reduce(buf)
+    n = buf[:, 2]
+    mean = buf[:, 0] / n
+    var = (buf[:, 1] - n * mean * mean) / (n - 1)
+    return torch.stack([mean, var.clamp_min(0).sqrt()], 1).float().contiguous()
+
+
 def allreduce_sum_(t):
     if is_dist():
         dist.all_reduce(t)

@@ -58,7 +58,9 @@ class FlatAdam(torch.optim.Adam):
         self._f = self._state.view(torch.float32)
         self._i = self._state.view(torch.int32)
         self._f[0] = init_scale
-        self.norms = torch.zeros(2, dtype=torch.float32, device=dev)  # [sum of per-param norms, total]
+        # [sum of per-param norms, total norm, L2-init regulariser]
+        self.norms = torch.zeros(3, dtype=torch.float32, device=dev)
+        self.param_init = None
         self.use_loss_scale = bool(use_loss_scale)
         self._hp_scale = (growth_factor, backoff_factor, growth_interval)
         self._bind_state()
@@ -123,9 +125,16 @@ class FlatAdam(torch.optim.Adam):
         """Device int32: steps skipped for inf / nan gradients."""
         return self._i[3]
 
+    def track_init_distance(self):
+        """Keep a flat copy of the current parameters; every fused_step then also reports
+        sum_p mean((p - p0)^2) over them (norms[2]), the L2-init regulariser the reference logs
+        each minibatch (clean_pufferl/core.py:352-359), from the same pass over the buffers."""
+        self.param_init = self.param_flat.detach().clone()
+
     def fused_step(self, max_norm):
-        """clip_grad_norm_(max_norm) + Adam (+ loss-scale update); returns the device [2] tensor
-        (sum of per-parameter gradient norms as the reference logs, global norm)."""
+        """clip_grad_norm_(max_norm) + Adam (+ loss-scale update); returns the device [3] tensor
+        (sum of per-parameter gradient norms as the reference logs, global norm, L2-init
+        distance of the parameters before the update when tracked)."""
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         gf, bf, gi = self._hp_scale
@@ -136,6 +145,7 @@ class FlatAdam(torch.optim.Adam):
                                       self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), n, self._blk.data_ptr(),
                                       self._blk.shape[0], self._seg.data_ptr(), self._seg.numel() - 1,
                                       ctypes.byref(hp), self._state.data_ptr(), self.norms.data_ptr(),
+                                      self.param_init.data_ptr() if self.param_init is not None else None,
                                       self._ws.data_ptr(), N._stream()),
                  "phc_opt_step")
         return self.norms

@@ -9,7 +9,9 @@ from torch import nn
 
 from .discriminator_policy import DiscriminatorPolicy
 from .pufferl_policy import Linear, layer_init
-from .twin_mlp import TwinWeights, head_linear, twin_ln_silu, twin_ln_silu_supported, twin_trunks
+from .. import _native as N
+from .twin_mlp import (TwinWeights, half_input_width, head_linear, twin_ln_silu, twin_ln_silu_supported,
+                       twin_trunks)
 
 
 def mlp(layer_sizes, activation):
@@ -37,8 +39,50 @@ class PHCPolicy(DiscriminatorPolicy):
         self.fused_ln = True  # LayerNorm + SiLU of both trunks in one kernel (False: torch modules)
         self._critic_trunk = None
 
+    def _compute_dtype(self):
+        return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else torch.float32
+
+    def obs_half_input(self, obs, rows=None):
+        """RunningNorm(obs[rows]) as the padded f16 / bf16 operand of the first trunk GEMM in one
+        pass (phc_obs_half), or None when the current precision does not run the MFMA trunks.
+        The trainer builds it once per train() call: the statistics only change between
+        iterations (scripts/train.py:337-346)."""
+        if not (self.fused and obs.is_cuda):
+            return None
+        dt = self._compute_dtype()
+        width = half_input_width(self._twin, dt)
+        if width is None:
+            return None
+        m = obs.shape[0] if rows is None else rows.shape[0]
+        out = torch.empty((m, width), dtype=dt, device=obs.device)
+        n = self.obs_norm
+        return N.obs_half(obs, n.running_mean, n.running_var, n.epsilon, n.clip, out, rows)
+
+    def act_rollout(self, obs, noise, actions, logprob, value):
+        """Rollout inference (encode_observations + decode_actions + sample_logits) writing the
+        sampled actions, their log-probability and the value into the given buffers: half input
+        (phc_obs_half), MFMA trunks, then LayerNorm+SiLU, both heads, the Normal sample and
+        log_prob in one kernel (phc_policy_act).  False when this precision / shape has no fused
+        path (the caller then runs the module)."""
+        h = self._head
+        if not (self.fused and self.fused_ln and twin_ln_silu_supported(self._twin.pairs[-1][0].weight.shape[0])):
+            return False
+        xc = self.obs_half_input(obs)
+        if xc is None:
+            return False
+        y = twin_trunks(xc, self._twin)
+        la, lc = self.actor_mlp[h], self.critic_mlp[h]
+        vh, mh = self.critic_mlp[h + 2], self.mu[0]
+        N.policy_act(y, (la.weight, la.bias), (lc.weight, lc.bias), la.eps, mh.weight, mh.bias, vh.weight, vh.bias,
+                     self.sigma, noise, actions, logprob, value,
+                     std_max=1e-6 if self._deterministic_action is True else float("inf"))
+        return True
+
     def encode_observations(self, obs):
-        self.obs_pointer = self.obs_norm(obs)
+        if obs.dtype in (torch.float16, torch.bfloat16):
+            self.obs_pointer = obs  # obs_half_input's output: normalised, padded GEMM operand
+        else:
+            self.obs_pointer = self.obs_norm(obs)
         if self.fused and obs.is_cuda:
             y = twin_trunks(self.obs_pointer, self._twin)  # [2, M, hidden]: actor, critic
             h = self._head

@@ -14,6 +14,8 @@ precision (hipBLASLt xf32) outside autocast, fp16 / bf16 operands inside.  In th
 modes only the GEMM OPERANDS are rounded: every GEMM accumulates and writes fp32, the epilogues
 compute in fp32 from those outputs and round once, when they write the next GEMM's operand
 (activations forward, activation gradients backward), and bias / weight gradients are fp32.
+The pre-activations saved for the SiLU backward are kept in the operand type on the MFMA path,
+as torch.autocast keeps them (PRE_HALF).
 With fp16 operands this is TF32's arithmetic (an 11-bit significand per operand, fp32 products
 and sums; the reference sets torch.set_float32_matmul_precision("high"),
 clean_pufferl/core.py:38) with fp16's exponent range, which dynamic loss scaling covers for the
@@ -62,6 +64,18 @@ def _split_k(m, n, k, groups):
     while s * 2 * tiles <= 256 and s < 32 and m % (s * 2) == 0 and m // (s * 2) >= 1024:
         s *= 2
     return s
+
+
+def _weight_grad_parts(g, z):
+    """The split-K partials of dW[b] = g[b]^T z[b]: [B, S, n, k] fp32 (S = 1: no split), summed
+    by the caller (phc_reduce_into, straight into the gradient views)."""
+    B, M, n = g.shape
+    k = z.shape[2]
+    S = 1 if g.dtype == torch.bfloat16 else _split_k(M, n, k, B)
+    if S == 1:
+        return _bmm(g.transpose(1, 2), z, True).view(B, 1, n, k)
+    part = _bmm(g.reshape(B * S, M // S, n).transpose(1, 2), z.reshape(B * S, M // S, k), True)
+    return part.view(B, S, n, k)
 
 
 def _weight_grad(g, z):
@@ -184,7 +198,8 @@ def mfma_operands(weights, dtype):
 
 class TwinTrunkMfmaFn(torch.autograd.Function):
     """TwinTrunkFn on the hand-written MFMA GEMM (phc_gemm.hip) for f16 / bf16 operands: every
-    forward GEMM carries its bias + SiLU epilogue (pre-activation kept in fp32 for backward),
+    forward GEMM carries its bias + SiLU epilogue (pre-activation kept for backward in the
+    operand type, see PRE_HALF),
     every input-gradient GEMM its SiLU-backward + bias-gradient epilogue, so no activation
     makes a separate elementwise round trip.  Weight gradients stay split-K library GEMMs
     (their reduction runs over the 32768 rows)."""
@@ -195,15 +210,20 @@ class TwinTrunkMfmaFn(torch.autograd.Function):
         with torch.autocast("cuda", enabled=False):
             ops = mfma_operands(weights, dt)
             B = ops.b
-            M, K0 = x.shape
+            M = x.shape[0]
+            K0 = weights.pairs[0][0].weight.shape[1]
             Kp = ops.w0.shape[1]
-            xc = torch.empty((M, Kp), dtype=dt, device=x.device)
-            xc[:, :K0].copy_(x)
-            if Kp != K0:
-                xc[:, K0:].zero_()  # K padding (the padded weight columns are zero too)
+            if x.dtype == dt and x.shape[1] == Kp and x.is_contiguous():
+                xc = x  # already the padded GEMM operand (obs_half_input)
+            else:
+                xc = torch.empty((M, Kp), dtype=dt, device=x.device)
+                xc[:, :K0].copy_(x)
+                if Kp != K0:
+                    xc[:, K0:].zero_()  # K padding (the padded weight columns are zero too)
             n1 = ops.w0.shape[0] // 2
             z = torch.empty((2, M, n1), dtype=dt, device=x.device)
-            pre = torch.empty((M, 2 * n1), dtype=torch.float32, device=x.device) if need_grad else None
+            pdt = dt if PRE_HALF else torch.float32
+            pre = torch.empty((M, 2 * n1), dtype=pdt, device=x.device) if need_grad else None
             N.twin_gemm(xc, ops.w0, N.EPI_BIAS_SILU, z, (2, n1), bias=B[0], aux=pre, aux_layout=N.SPLIT,
                         out_layout=N.GROUPED)
             pres, zs = [pre], [z]
@@ -212,7 +232,7 @@ class TwinTrunkMfmaFn(torch.autograd.Function):
                 n = ops.w[l - 1].shape[1]
                 if l < L - 1:
                     z = torch.empty((2, M, n), dtype=dt, device=x.device)
-                    pre = torch.empty((2, M, n), dtype=torch.float32, device=x.device) if need_grad else None
+                    pre = torch.empty((2, M, n), dtype=pdt, device=x.device) if need_grad else None
                     N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS_SILU, z, (2, n), bias=B[l], aux=pre)
                     pres.append(pre)
                     zs.append(z)
@@ -222,6 +242,7 @@ class TwinTrunkMfmaFn(torch.autograd.Function):
         if need_grad:
             ctx.save_for_backward(xc, *ops.wt, *pres, *zs)  # pres: pre-activations, biases included
             ctx.L, ctx.K0 = L, K0
+            ctx.params = params
         return y
 
     @staticmethod
@@ -232,7 +253,28 @@ class TwinTrunkMfmaFn(torch.autograd.Function):
         pres, zs = saved[L:2 * L - 1], saved[2 * L - 1:3 * L - 2]
         dt = xc.dtype
         M = xc.shape[0]
+        params = ctx.params
+        # with gradient views already bound (FlatGrads), the weight / bias gradients go straight
+        # into them (phc_reduce_into sums the split-K partials there): no per-parameter
+        # accumulation launches
+        direct = DIRECT_GRADS and all(p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+                                      for p in params)
         grads = [None] * (2 * L)
+        jobs = []
+
+        def put(l, dW_parts, db):
+            """dW_parts: ([parts, 2n, k] or [2, parts, n, k] partials, layer-1 flag), db [2n]."""
+            if not direct:
+                grads[2 * l], grads[2 * l + 1] = dW_parts, db
+                return
+            wa, ba, wc, bc = params[4 * l:4 * l + 4]
+            n, k = wa.shape
+            if l == 0:
+                jobs.extend([(dW_parts[:, :n, :k], wa.grad), (dW_parts[:, n:, :k], wc.grad)])
+            else:
+                jobs.extend([(dW_parts[0], wa.grad), (dW_parts[1], wc.grad)])
+            jobs.extend([(db[:n].view(1, n), ba.grad), (db[n:].view(1, n), bc.grad)])
+
         with torch.autocast("cuda", enabled=False):
             gy = gy.float().contiguous()
             n = gy.shape[2]
@@ -240,7 +282,7 @@ class TwinTrunkMfmaFn(torch.autograd.Function):
             g = torch.empty(gy.shape, dtype=dt, device=gy.device)
             N.act_bwd(gy, N.GROUPED, None, N.GROUPED, g, N.GROUPED, db, M, 2, n, N.ACT_NONE)
             for l in range(L - 1, 0, -1):
-                grads[2 * l], grads[2 * l + 1] = _weight_grad(g, zs[l - 1]), db
+                put(l, _weight_grad_parts(g, zs[l - 1]) if direct else _weight_grad(g, zs[l - 1]), db)
                 k = WT[l - 1].shape[1]
                 db = torch.empty(2 * k, dtype=torch.float32, device=g.device)
                 if l > 1:
@@ -250,9 +292,14 @@ class TwinTrunkMfmaFn(torch.autograd.Function):
                     gp = torch.empty((M, 2 * k), dtype=dt, device=g.device)
                     N.twin_gemm(g, WT[0], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[0], aux_layout=N.SPLIT,
                                 out_layout=N.SPLIT, bias_grad=db)
-                    grads[0] = _weight_grad(gp[None], xc[None])[0][:, :K0]
-                    grads[1] = db
+                    if direct:
+                        put(0, _weight_grad_parts(gp[None], xc[None])[0], db)
+                    else:
+                        put(0, _weight_grad(gp[None], xc[None])[0][:, :K0], db)
                 g = gp
+            if direct:
+                N.reduce_into(jobs, accumulate=True)
+                return (None, None, None) + (None,) * (4 * L)
         out = []
         for l in range(L):
             dW, db = grads[2 * l], grads[2 * l + 1]
@@ -344,6 +391,13 @@ class TwinTrunkFn(torch.autograd.Function):
 
 # half-precision trunks on phc_twin_gemm (PHC_MFMA_GEMM=0: hipBLASLt GEMMs + epilogue kernels)
 USE_MFMA_GEMM = os.environ.get("PHC_MFMA_GEMM", "1") == "1"
+# trunk weight / bias gradients written straight into bound gradient views (FlatGrads) by one
+# phc_reduce_into launch per backward (PHC_DIRECT_GRADS=0: returned to autograd)
+DIRECT_GRADS = os.environ.get("PHC_DIRECT_GRADS", "1") == "1"
+# the pre-activations saved for backward in the operand type (what torch.autocast keeps: its
+# Linear returns f16 / bf16 and SiLU saves that input), not fp32: a third less epilogue traffic
+# (PHC_PRE_HALF=0: fp32)
+PRE_HALF = os.environ.get("PHC_PRE_HALF", "1") == "1"
 
 
 def _use_mfma(weights, dtype):
@@ -359,8 +413,17 @@ def refresh_twin(weights, dtype):
         weights.get(dtype)
 
 
+def half_input_width(weights, dtype):
+    """Width of the first trunk GEMM's padded operand for `dtype` on the MFMA path (None when
+    that path does not serve `dtype`)."""
+    if not _use_mfma(weights, dtype):
+        return None
+    return _pad64(weights.pairs[0][0].weight.shape[1])
+
+
 def twin_trunks(x, weights):
-    """Both trunks' pre-LayerNorm outputs, [2, M, H] (index 0 = actor, 1 = critic)."""
+    """Both trunks' pre-LayerNorm outputs, [2, M, H] (index 0 = actor, 1 = critic).  x is the
+    normalised observation (fp32), or on the MFMA path already its padded half operand."""
     if not x.is_cuda:
         raise RuntimeError("twin_trunks runs on the HIP path only (no CPU fallback)")
     need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in weights.params())

@@ -47,9 +47,11 @@ def test_strided_operand_and_shared_a():
     assert torch.equal(out, ref)
 
 
-def test_bias_silu_split_to_grouped():
-    """Layer 1: one [m, k] x [2n, k]^T GEMM, pre kept SPLIT [m, 2n] (fp32), silu written GROUPED
-    [2, m, n] in f16 — the twin layout conversion of phc_bias_act_fwd, fused."""
+@pytest.mark.parametrize("pre_dtype", [torch.float32, torch.float16])
+def test_bias_silu_split_to_grouped(pre_dtype):
+    """Layer 1: one [m, k] x [2n, k]^T GEMM, pre kept SPLIT [m, 2n] (fp32, or f16 as autocast keeps
+    it), silu written GROUPED [2, m, n] in f16 — the twin layout conversion of phc_bias_act_fwd,
+    fused."""
     from puffer_phc_amd import _native as N
 
     g = torch.Generator(device=DEV).manual_seed(2)
@@ -57,11 +59,14 @@ def test_bias_silu_split_to_grouped():
     a = torch.randn((m, k), device=DEV, generator=g).half()
     w = (torch.randn((2 * n, k), device=DEV, generator=g) / k ** 0.5).half()
     bias = torch.randn(2 * n, device=DEV, generator=g)
-    pre = torch.empty((m, 2 * n), device=DEV)
+    pre = torch.empty((m, 2 * n), device=DEV, dtype=pre_dtype)
     z = torch.empty((2, m, n), dtype=torch.float16, device=DEV)
     N.twin_gemm(a, w, N.EPI_BIAS_SILU, z, (2, n), bias=bias, aux=pre, aux_layout=N.SPLIT, out_layout=N.GROUPED)
     ref_pre = a.float() @ w.float().t() + bias
-    torch.testing.assert_close(pre, ref_pre, rtol=2e-5, atol=2e-5)
+    if pre_dtype == torch.float32:
+        torch.testing.assert_close(pre, ref_pre, rtol=2e-5, atol=2e-5)
+    else:
+        torch.testing.assert_close(pre.float(), ref_pre, rtol=2.0 ** -10, atol=2e-5)
     ref_z = torch.nn.functional.silu(ref_pre).view(m, 2, n).permute(1, 0, 2)
     torch.testing.assert_close(z.float(), ref_z, rtol=2.0 ** -10, atol=2e-5)
 
@@ -81,8 +86,9 @@ def test_bias_fp32_out_batched(dtype):
     torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("pre_dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("out_layout", [0, 1])
-def test_silu_grad_and_bias_grad(out_layout):
+def test_silu_grad_and_bias_grad(out_layout, pre_dtype):
     """Input gradient of a SiLU layer: dz = g @ W (W pre-transposed to [k_in, n_out]), then
     dz * silu'(pre + b) rounded to f16, and the bias gradient from the fp32 products."""
     from puffer_phc_amd import _native as N
@@ -93,7 +99,7 @@ def test_silu_grad_and_bias_grad(out_layout):
     w = (torch.randn((2, n_out, k_in), device=DEV, generator=g) / n_out ** 0.5).half()
     wt = w.transpose(1, 2).contiguous()  # [2, k_in, n_out]
     pre_shape = (m, 2 * k_in) if out_layout == N.SPLIT else (2, m, k_in)
-    pre = torch.randn(pre_shape, device=DEV, generator=g) * 2
+    pre = (torch.randn(pre_shape, device=DEV, generator=g) * 2).to(pre_dtype)
     pb = torch.randn(2 * k_in, device=DEV, generator=g)
     gout = torch.empty(pre_shape, dtype=torch.float16, device=DEV)
     db = torch.empty(2 * k_in, device=DEV)
@@ -104,7 +110,7 @@ def test_silu_grad_and_bias_grad(out_layout):
         return t.view(m, 2, k_in).permute(1, 0, 2) if out_layout == N.SPLIT else t
 
     dz = torch.bmm(gr.float(), w.float())  # [2, m, k_in]
-    p = (grouped(pre) + pb.view(2, 1, k_in)).clone().requires_grad_(True)
+    p = (grouped(pre).float() + pb.view(2, 1, k_in)).clone().requires_grad_(True)
     torch.nn.functional.silu(p).backward(dz)
     torch.testing.assert_close(grouped(gout).float(), p.grad, rtol=2.0 ** -10, atol=1e-4)
     torch.testing.assert_close(db, p.grad.sum(1).reshape(-1), rtol=1e-4, atol=1e-3)

@@ -5,7 +5,8 @@ torch.amp.GradScaler for the fp16 path) on the same parameters and gradients (ne
 Tolerance: parameters within rel 2e-6 / abs 1e-8 after several steps (Adam's update is
 lr * m / (sqrt(v) + eps) in fp32 in both; torch's moment updates use lerp / addcmul, a different
 rounding order; the clip coefficient here comes from a double-precision norm).  The logged norm
-(sum of per-parameter norms) within rel 1e-5.  Skip / scale decisions are exact.
+(sum of per-parameter norms) within rel 1e-5, the logged L2-init distance within rel 1e-4
+(double accumulation here, fp32 per-parameter means in torch).  Skip / scale decisions are exact.
 """
 
 import pytest
@@ -40,10 +41,14 @@ def test_clip_adam_matches_torch(max_norm):
     ours = _params(0)
     opt_ref = torch.optim.Adam(ref, lr=3e-4, eps=1e-5)
     fg, opt = _flat(ours)
+    opt.track_init_distance()
+    init = [p.detach().clone() for p in ref]
     for step in range(4):
         for p, g in zip(ref, _grads(step)):
             p.grad = g.clone()
         norms = torch.stack([p.grad.norm() for p in ref])
+        # the L2-init regulariser of the parameters before this step (core.py:352-359)
+        l2 = sum(((p.detach() - p0) ** 2).mean() for p, p0 in zip(ref, init))
         torch.nn.utils.clip_grad_norm_(ref, max_norm)
         opt_ref.step()
         fg.zero()
@@ -51,6 +56,7 @@ def test_clip_adam_matches_torch(max_norm):
             p.grad.copy_(g)
         out = opt.fused_step(max_norm)
         torch.testing.assert_close(out[0], norms.sum(), rtol=1e-5, atol=0)
+        torch.testing.assert_close(out[2], l2, rtol=1e-4, atol=1e-12)
         for a, b in zip(ours, ref):
             torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-6, atol=1e-8)
     # the module parameters are views of the flat buffer

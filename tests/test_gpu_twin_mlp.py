@@ -280,3 +280,25 @@ def test_mfma_trunks_match_library_path(precision):
     assert rel(mf[0], lib[0]) <= tol
     worst = max(rel(mf[2][k], lib[2][k]) for k in lib[2])
     assert worst <= tol, worst
+
+
+def test_direct_gradient_writes_match_autograd():
+    """With gradient views bound (FlatGrads), the MFMA trunk writes its weight / bias gradients
+    straight into them (phc_reduce_into) and accumulates onto what is there; without, autograd
+    receives them.  Same values up to the split-K partial summation order (rel 1e-6)."""
+    from puffer_phc_amd.distributed import FlatGrads
+
+    pol = _policy()
+    g = torch.Generator(device=DEV).manual_seed(7)
+    obs = torch.randn((2048, 934), device=DEV, generator=g)
+    act = torch.randn((2048, 69), device=DEV, generator=g) * 0.3
+    _, _, ref = _run(pol, obs, act, fused=True, precision=torch.float16)
+    fg = FlatGrads(pol.parameters())
+    for p in fg.params:
+        p.grad.fill_(0.25)  # accumulate semantics: the bound values are added to
+    with torch.autocast("cuda", dtype=torch.float16):
+        _, logp, _, value = pol(obs, action=act)
+    (logp.sum() * 1e-3 + (value.float() ** 2).sum()).backward()
+    for n, p in pol.named_parameters():
+        if n in ref:
+            torch.testing.assert_close(p.grad - 0.25, ref[n], rtol=1e-5, atol=1e-6)

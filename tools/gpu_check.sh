@@ -12,7 +12,7 @@ MODES=${MODES:-ppo env}
 BENCH_ARGS=${BENCH_ARGS:-}
 
 if [ "${TESTS:-1}" = "1" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
   rc=$?
   echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
