@@ -86,7 +86,11 @@ __device__ __forceinline__ int64_t gemm_twin_off(const GemmArgs &g, int layout, 
   return ((int64_t)grp * g.m + row) * g.tc + j;
 }
 
-__device__ __forceinline__ float gemm_silu(float a) { return a / (1.0f + expf(-a)); }
+// sigmoid from the hardware exp2 / reciprocal (1-ulp class, the values land in f16 / bf16 operands)
+__device__ __forceinline__ float gemm_sigmoid(float a) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-a * 1.44269504088896341f));
+}
+__device__ __forceinline__ float gemm_silu(float a) { return a * gemm_sigmoid(a); }
 
 template <typename OutT> __device__ __forceinline__ void gemm_store(void *p, int64_t off, float v) {
   static_cast<OutT *>(p)[off] = (OutT)v;
@@ -136,11 +140,12 @@ template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_> struct Tile {
   static constexpr int kStageBytes = (BM + BN) * kGBK * 2;
   static constexpr int kLoadsPerTile = (BM + BN) / 8 / kWaves;  // glds per thread per K-step
   static constexpr int kOpBytes = STAGES * kStageBytes;
-  // epilogue: wave rows per pass through the fp32 LDS image (reusing the operand buffers)
-  static constexpr int kEpWaveRows = (kOpBytes / (TM * BN * 4)) >= WGM ? WGM : (kOpBytes / (TM * BN * 4));
-  static constexpr int kEpRows = kEpWaveRows * TM;
+  // epilogue: the fp32 LDS image (reusing the operand buffers) holds the whole tile, or passes of
+  // every wave's next TM / kEpPasses rows (so half the accumulators die after the first pass)
+  static constexpr int kEpPasses = (BM * BN * 4 + kOpBytes - 1) / kOpBytes;
+  static constexpr int kEpRows = BM / kEpPasses, kEpWaveRows = TM / kEpPasses, kEpMI = MI / kEpPasses;
   static constexpr int kLdsBytes = kOpBytes;
-  static_assert(kEpWaveRows >= 1 && WGM % kEpWaveRows == 0, "epilogue image must fit the operand buffers");
+  static_assert(MI % kEpPasses == 0 && kEpRows * BN * 4 <= kOpBytes, "epilogue image must fit the operand buffers");
   static_assert(MI >= 1 && NI >= 1 && TM % 16 == 0 && TN % 16 == 0, "bad wave tile");
 };
 
@@ -254,66 +259,91 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
   }
   // ---- epilogue.  The accumulators (lane: column lane & 15, rows 4 * (lane >> 4) + e of each
   // 16 x 16 block) go through LDS as an fp32 [rows][BN] image, 16-column groups XOR-swizzled by
-  // (row >> 2) & 3 so both the scattered writes and the row reads are conflict-free (in passes of
-  // kEpRows rows when the whole tile does not fit); then each thread owns 4 consecutive columns
-  // of every kRowGroups-th row: 16-B loads / stores, BN * 4 contiguous bytes per row.
+  // (row >> 2) & 3 so both the scattered writes and the row reads are conflict-free; pass p holds
+  // rows [p * kEpWaveRows, (p + 1) * kEpWaveRows) of every wave row.  Then each thread owns 4
+  // consecutive columns of every kRowGroups-th image row: 16-B loads / stores, BN * 4
+  // contiguous bytes per row.
   constexpr int kColThreads = BN / 4, kRowGroups = TL::kThreads / kColThreads;
+  constexpr int WR = TL::kEpWaveRows, IT = TL::kEpRows / kRowGroups;
   float *ep = reinterpret_cast<float *>(smem);
   const int c4 = (tid % kColThreads) * 4, rg = tid / kColThreads;
   const int gcol = n0 + c4;
   const bool vec = gcol + 3 < g.n && g.tc % 4 == 0;
+  const bool full = vec && m0 + BM <= g.m;
   float bias4[4] = {0.0f, 0.0f, 0.0f, 0.0f}, csum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (EPI != PHC_EPI_STORE && g.bias) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (gcol + q < g.n) bias4[q] = g.bias[bt * g.n + gcol + q];
   }
-#pragma unroll 1
-  for (int pass = 0; pass < TL::WGM / TL::kEpWaveRows; ++pass) {
+  // element offsets of this thread's 4 columns: base + row * stride in either layout
+  const int lc = bt * g.n + gcol;
+  const int grp = lc / g.tc, jc = lc - grp * g.tc;
+  auto lin = [&](int layout, int64_t &base, int64_t &stride) {
+    if (layout == PHC_LAYOUT_SPLIT) { base = lc; stride = (int64_t)g.tg * g.tc; }
+    else { base = (int64_t)grp * g.m * g.tc + jc; stride = g.tc; }
+  };
+  int64_t ob, os, ab = 0, as = 0;
+  lin(g.out_layout, ob, os);
+  lin(g.aux_layout, ab, as);
+  // tile row of this thread's it-th image row in pass p
+  auto trow = [&](int p, int it) {
+    const int r = rg + kRowGroups * it;
+    return (r / WR) * TL::TM + p * WR + r % WR;
+  };
+#pragma unroll
+  for (int pass = 0; pass < TL::kEpPasses; ++pass) {
     __syncthreads();  // operand tiles / the previous pass's image are no longer read
-    if (wm / TL::kEpWaveRows == pass) {
-      const int rbase = (wm % TL::kEpWaveRows) * TL::TM;
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+    for (int i = pass * TL::kEpMI; i < (pass + 1) * TL::kEpMI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = rbase + i * 16 + 4 * (lane >> 4) + e;
-            const int c = wn * TL::TN + j * 16 + (lane & 15);
-            ep[r * BN + (c ^ (((r >> 2) & 3) << 4))] = acc[i][j][e];
-          }
-    }
+        for (int e = 0; e < 4; ++e) {
+          const int r = wm * WR + (i - pass * TL::kEpMI) * 16 + 4 * (lane >> 4) + e;
+          const int c = wn * TL::TN + j * 16 + (lane & 15);
+          ep[r * BN + (c ^ (((r >> 2) & 3) << 4))] = acc[i][j][e];
+        }
     __syncthreads();
-    const int64_t prow0 = m0 + (int64_t)pass * TL::kEpRows;  // first row of this pass
-    if (vec && prow0 + TL::kEpRows <= g.m) {
-      // full pass, 4 whole columns per thread: offsets are base + row * stride, and the rows go
-      // in batches of 4 with their aux loads issued together
-      const int lc = bt * g.n + gcol;
-      const int grp = lc / g.tc, jc = lc - grp * g.tc;
-      auto lin = [&](int layout, int64_t &base, int64_t &stride) {
-        if (layout == PHC_LAYOUT_SPLIT) { base = lc; stride = (int64_t)g.tg * g.tc; }
-        else { base = (int64_t)grp * g.m * g.tc + jc; stride = g.tc; }
-      };
-      int64_t ob, os, ab = 0, as = 0;
-      lin(g.out_layout, ob, os);
-      lin(g.aux_layout, ab, as);
-      constexpr int IT = TL::kEpRows / kRowGroups, U = EPI == PHC_EPI_SILU_GRAD ? 2 : 4;
+    if (full) {
+      // whole tile in range, 4 whole columns per thread: offsets are base + row * stride, rows
+      // in batches of U; a half-precision aux is software-pipelined (batch b + 1's loads in
+      // flight while batch b is processed), an fp32 one loaded per batch
+      constexpr int U = 4;
       static_assert(IT % U == 0, "row batches");
-#pragma unroll 1
-      for (int i0 = 0; i0 < IT; i0 += U) {
-        float4 av[U];
+      const bool pipe = EPI == PHC_EPI_SILU_GRAD && g.aux_half;
+      uint2 raw[2][EPI == PHC_EPI_SILU_GRAD ? U : 1];
+      auto load_raw = [&](int b) {
         if constexpr (EPI == PHC_EPI_SILU_GRAD) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const int64_t row = prow0 + rg + kRowGroups * (i0 + u);
-            av[u] = aux_load4<T>(g, ab + row * as);
+            const int64_t row = m0 + trow(pass, b * U + u);
+            raw[b & 1][u] = *reinterpret_cast<const uint2 *>(static_cast<const T *>(g.aux) + ab + row * as);
+          }
+        }
+      };
+      if (pipe) load_raw(0);
+#pragma unroll
+      for (int i0 = 0; i0 < IT; i0 += U) {
+        float4 av[U];
+        if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+          if (pipe) {
+            if (i0 + U < IT) load_raw(i0 / U + 1);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              T h[4];
+              __builtin_memcpy(h, &raw[(i0 / U) & 1][u], sizeof(h));
+              av[u] = float4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) av[u] = aux_load4<T>(g, ab + (m0 + trow(pass, i0 + u)) * as);
           }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int r = rg + kRowGroups * (i0 + u);
-          const int64_t row = prow0 + r;
+          const int64_t row = m0 + trow(pass, i0 + u);
           const float4 t = *reinterpret_cast<const float4 *>(&ep[r * BN + (c4 ^ (((r >> 2) & 3) << 4))]);
           float v[4] = {t.x, t.y, t.z, t.w};
           if constexpr (EPI == PHC_EPI_SILU_GRAD) {
@@ -321,7 +351,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const float x = a[q] + bias4[q];
-              const float sg = 1.0f / (1.0f + expf(-x));
+              const float sg = gemm_sigmoid(x);
               v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
               csum[q] += v[q];
             }
@@ -339,14 +369,13 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
       }
       continue;
     }
-    for (int it = 0; it < TL::kEpRows / kRowGroups; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int r = rg + kRowGroups * it;
-      const int64_t row = m0 + (int64_t)pass * TL::kEpRows + r;
-      if (row >= g.m) break;
+      const int64_t row = m0 + trow(pass, it);
+      if (row >= g.m) continue;
       const float4 t = *reinterpret_cast<const float4 *>(&ep[r * BN + (c4 ^ (((r >> 2) & 3) << 4))]);
       float v[4] = {t.x, t.y, t.z, t.w};
       float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      const int lc = bt * g.n + gcol;
       if constexpr (EPI == PHC_EPI_SILU_GRAD) {
         if (vec) {
           const float4 av = aux_load4<T>(g, gemm_twin_off(g, g.aux_layout, row, lc));
@@ -364,7 +393,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
           if constexpr (EPI == PHC_EPI_BIAS_SILU) v[q] = gemm_silu(v[q]);
         } else if constexpr (EPI == PHC_EPI_SILU_GRAD) {
           const float x = a[q] + bias4[q];
-          const float sg = 1.0f / (1.0f + expf(-x));
+          const float sg = gemm_sigmoid(x);
           v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
           csum[q] += gcol + q < g.n ? v[q] : 0.0f;
         }
