@@ -444,9 +444,8 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
 
 // tile configurations
 using Tile128x2 = Tile<128, 128, 2, 2, 2>;
-using Tile256x3 = Tile<256, 128, 4, 2, 3>;
 using Tile256sq = Tile<256, 256, 2, 4, 2>;
-enum { kCfg128 = 0, kCfg256x128 = 1, kCfg256sq = 2 };
+enum { kCfg128 = 0, kCfg256sq = 2 };
 
 // 256 x 256 tiles when they still give every CU two or more tiles, else 128 x 128 (the
 // rollout's 4096-row GEMMs)
@@ -479,11 +478,8 @@ static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
 
 template <typename T, typename OutT, int EPI>
 static void launch_cfg(int cfg, const GemmArgs &g, int64_t blocks, hipStream_t st) {
-  switch (cfg) {
-    case kCfg128: launch_one<T, OutT, EPI, Tile128x2>(g, blocks, st); break;
-    case kCfg256x128: launch_one<T, OutT, EPI, Tile256x3>(g, blocks, st); break;
-    default: launch_one<T, OutT, EPI, Tile256sq>(g, blocks, st); break;
-  }
+  if (cfg == kCfg128) launch_one<T, OutT, EPI, Tile128x2>(g, blocks, st);
+  else launch_one<T, OutT, EPI, Tile256sq>(g, blocks, st);
 }
 
 template <typename T, typename OutT>

@@ -116,6 +116,41 @@ def test_silu_grad_and_bias_grad(out_layout, pre_dtype):
     torch.testing.assert_close(db, p.grad.sum(1).reshape(-1), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("epi", ["bias_silu", "bias_f32", "silu_grad"])
+def test_large_ragged_256_tiles(epi):
+    """Shapes large enough for the 256 x 256 tile configuration (>= 512 tiles), with ragged rows
+    (16500 = 64.45 tiles) and ragged columns (1000 = 3.9 tiles): masked rows / columns of the
+    register epilogue, twin offsets across the batch."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(7)
+    m, n, k = 16500, 1000, 192
+    a = torch.randn((2, m, k), device=DEV, generator=g).half()
+    w = (torch.randn((2, n, k), device=DEV, generator=g) / k ** 0.5).half()
+    b = torch.randn(2 * n, device=DEV, generator=g)
+    y = torch.bmm(a.float(), w.float().transpose(1, 2))  # [2, m, n]
+    if epi == "bias_f32":
+        out = torch.empty((2, m, n), device=DEV)
+        N.twin_gemm(a, w, N.EPI_BIAS, out, (2, n), bias=b)
+        torch.testing.assert_close(out, y + b.view(2, 1, n), rtol=2e-5, atol=2e-5)
+    elif epi == "bias_silu":
+        out = torch.empty((2, m, n), dtype=torch.float16, device=DEV)
+        pre = torch.empty((2, m, n), dtype=torch.float16, device=DEV)
+        N.twin_gemm(a, w, N.EPI_BIAS_SILU, out, (2, n), bias=b, aux=pre)
+        ref = y + b.view(2, 1, n)
+        torch.testing.assert_close(pre.float(), ref, rtol=2.0 ** -10, atol=1e-4)
+        torch.testing.assert_close(out.float(), torch.nn.functional.silu(ref), rtol=2.0 ** -10, atol=1e-4)
+    else:
+        pre = (torch.randn((2, m, n), device=DEV, generator=g) * 2).half()
+        gout = torch.empty((2, m, n), dtype=torch.float16, device=DEV)
+        db = torch.empty(2 * n, device=DEV)
+        N.twin_gemm(a, w, N.EPI_SILU_GRAD, gout, (2, n), aux=pre, bias_grad=db)
+        p = pre.float().clone().requires_grad_(True)
+        torch.nn.functional.silu(p).backward(y)
+        torch.testing.assert_close(gout.float(), p.grad, rtol=2.0 ** -10, atol=1e-4)
+        torch.testing.assert_close(db, p.grad.sum(1).reshape(-1), rtol=1e-4, atol=2e-2)
+
+
 def test_rejects_unpadded_k():
     from puffer_phc_amd import _native as N
 
