@@ -395,6 +395,31 @@ int phc_ppo_loss_bwd(const float *mu, const float *log_sigma, const float *actio
                      const float *grad_loss, int64_t m, int32_t a, const phc_ppo_coefs *coefs, float *grad_mu,
                      float *grad_value, void *stream);
 
+/* R19 + R21: the row-wise PPO minibatch tail after the twin trunks (policies/phc_policy.py:16-61
+ * LayerNorm + SiLU of both trunks and the critic's value head; their backward).  Forward: h_actor
+ * [rows, hidden] (the fp32 operand of the mu-head GEMM) and value [rows].  Backward: from d h_actor
+ * [rows, hidden] (= dmu W_mu), dmu [rows, num_actions] and dvalue [rows] (phc_ppo_loss_bwd):
+ * dy [2, rows, hidden] in dtype (f16 / bf16: the trunk backward's operand) and per-block partial
+ * rows [phc_tail_blocks(rows), stride] whose column offsets phc_tail_layout returns (b_mu,
+ * w_value, b_value, ln gamma [2][hidden], ln beta [2][hidden], last trunk layer bias [2][hidden],
+ * stride).  hidden == 512, num_actions <= 72. */
+typedef struct phc_tail_ln_args {
+  const float *trunk_out;          /* [2, rows, hidden] fp32 (actor, critic) */
+  const float *ln_gamma[2];        /* [hidden] each */
+  const float *ln_beta[2];         /* [hidden] each */
+  const float *w_value, *b_value;  /* [hidden], [1] */
+  float *h_actor;                  /* [rows, hidden], written by the forward */
+  float *value;                    /* [rows], written by the forward */
+  int64_t rows;
+  int32_t hidden;
+  float ln_eps;
+} phc_tail_ln_args;
+int phc_tail_layout(int32_t num_actions, int32_t hidden, int32_t *offsets /* [7] */);
+int32_t phc_tail_blocks(int64_t rows);
+int phc_tail_ln_fwd(const phc_tail_ln_args *args, void *stream);
+int phc_tail_ln_bwd(const phc_tail_ln_args *args, const float *dh_actor, const float *dmu, const float *dvalue,
+                    int32_t num_actions, void *dy, int32_t dtype, float *partial, void *stream);
+
 /* Library version and last error (thread-local). */
 int phc_version(void);
 const char *phc_last_error(void);

@@ -76,6 +76,12 @@ class PpoCoefsC(ctypes.Structure):
 PPO_STATS = 7
 
 
+class TailLnArgsC(ctypes.Structure):
+    _fields_ = [("trunk_out", c_vp), ("ln_gamma", c_vp * 2), ("ln_beta", c_vp * 2), ("w_value", c_vp),
+                ("b_value", c_vp), ("h_actor", c_vp), ("value", c_vp), ("rows", c_i64), ("hidden", ctypes.c_int32),
+                ("ln_eps", ctypes.c_float)]
+
+
 class AmpBuffersC(ctypes.Structure):
     _fields_ = [("amp_obs", c_vp), ("amp_obs_demo", c_vp), ("num_steps", ctypes.c_int32)]
 
@@ -159,6 +165,11 @@ _EXPORTS = {
     "phc_opt_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, ctypes.c_int32, c_vp, ctypes.c_int32,
                                      ctypes.POINTER(AdamParamsC), c_vp, c_vp, c_vp, c_vp, c_vp]),
     "phc_ppo_workspace_bytes": (ctypes.c_size_t, [c_i64]),
+    "phc_tail_layout": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    "phc_tail_blocks": (ctypes.c_int32, [c_i64]),
+    "phc_tail_ln_fwd": (ctypes.c_int, [ctypes.POINTER(TailLnArgsC), c_vp]),
+    "phc_tail_ln_bwd": (ctypes.c_int, [ctypes.POINTER(TailLnArgsC), c_vp, c_vp, c_vp, ctypes.c_int32, c_vp,
+                                        ctypes.c_int32, c_vp, c_vp]),
     "phc_ppo_loss_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
                                          ctypes.POINTER(PpoCoefsC), c_vp, c_vp, c_vp, c_vp]),
     "phc_ppo_loss_bwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
@@ -629,6 +640,58 @@ def ppo_loss_bwd(mu, log_sigma, actions, row_coef, grad_loss, coefs):
                                   gmu.data_ptr(), gv.data_ptr(), _stream()),
            "phc_ppo_loss_bwd")
     return gmu, gv
+
+
+# ------------------------------------------------------ fused PPO tail --
+TAIL_HIDDEN = 512
+TAIL_MAX_ACTIONS = 72
+TAIL_FIELDS = ("b_mu", "w_value", "b_value", "gamma", "beta", "b6", "stride")
+
+
+def tail_layout(num_actions, hidden=TAIL_HIDDEN):
+    """Column offsets of one block's partial row of phc_tail_ln_bwd (dict over TAIL_FIELDS)."""
+    off = (ctypes.c_int32 * 7)()
+    _check(lib().phc_tail_layout(num_actions, hidden, off), "phc_tail_layout")
+    return dict(zip(TAIL_FIELDS, list(off)))
+
+
+class TailLN:
+    """phc_tail_ln_fwd / _bwd for one minibatch: LayerNorm + SiLU of both trunks of y [2, M, 512]
+    fp32 with the critic's value head; h_actor and value are allocated here."""
+
+    def __init__(self, y, ln_a, ln_c, eps, w_v, b_v):
+        G, M, H = y.shape
+        if G != 2 or H != TAIL_HIDDEN:
+            raise ValueError(f"tail_ln: y must be [2, rows, {TAIL_HIDDEN}]")
+        f32, dev = torch.float32, y.device
+        self.M, self.H = M, H
+        self.h_actor = torch.empty((M, H), dtype=f32, device=dev)
+        self.value = torch.empty(M, dtype=f32, device=dev)
+        self.keep = (y, ln_a, ln_c, w_v, b_v)  # the pointers below stay valid while this object lives
+        self.args = TailLnArgsC(
+            _ptr(y, f32, (2, M, H), "trunk_out"),
+            (c_vp * 2)(_ptr(ln_a[0], f32, (H,), "actor ln weight"), _ptr(ln_c[0], f32, (H,), "critic ln weight")),
+            (c_vp * 2)(_ptr(ln_a[1], f32, (H,), "actor ln bias"), _ptr(ln_c[1], f32, (H,), "critic ln bias")),
+            _ptr(w_v.reshape(-1), f32, (H,), "w_value"), _ptr(b_v.reshape(-1), f32, (1,), "b_value"),
+            self.h_actor.data_ptr(), self.value.data_ptr(), M, H, float(eps))
+
+    def forward(self):
+        _check(lib().phc_tail_ln_fwd(ctypes.byref(self.args), _stream()), "phc_tail_ln_fwd")
+        return self.h_actor, self.value
+
+    def backward(self, dh_actor, dmu, dvalue, dtype):
+        """(dy [2, M, H] in dtype, partial [blocks, stride] fp32, layout)."""
+        M, H = self.M, self.H
+        A = dmu.shape[1]
+        f32, dev = torch.float32, self.value.device
+        lay = tail_layout(A, H)
+        part = torch.empty((int(lib().phc_tail_blocks(M)), lay["stride"]), dtype=f32, device=dev)
+        dy = torch.empty((2, M, H), dtype=dtype, device=dev)
+        _check(lib().phc_tail_ln_bwd(ctypes.byref(self.args), _ptr(dh_actor, f32, (M, H), "dh_actor"),
+                                     _ptr(dmu, f32, (M, A), "dmu"), _ptr(dvalue.reshape(-1), f32, (M,), "dvalue"),
+                                     A, dy.data_ptr(), DTYPE_CODE[dtype], part.data_ptr(), _stream()),
+               "phc_tail_ln_bwd")
+        return dy, part, lay
 
 
 # ------------------------------------------------------- experience store --

@@ -21,8 +21,9 @@ import torch
 from .. import _native
 from .. import distributed as D
 from ..optim import FlatAdam
+from ..policies.fused_ppo import fused_ppo_loss, fused_ppo_supported
 from ..policies.twin_mlp import refresh_twin
-from .ppo_loss import ppo_objective
+from .ppo_loss import ppo_coefs, ppo_objective
 from .structs import Experience, LossComponents, Profile, StatsData, TrainComponents, TrainInfo, Utilization
 from .utils import count_params, save_checkpoint, seed_everything
 
@@ -309,6 +310,7 @@ def train(components, info, utilization=None):
                 amp_mb = amp_obs_demo.shape[0]
         total_minibatches = experience.num_minibatches * cfg.update_epochs
         adv_ms = None
+        tail_coefs = None
         fused_loss = (cfg.fused_loss and hasattr(pol, "forward_train") and getattr(pol, "fused", False)
                       and experience.lstm_h is None)
         obs_dim = components.vecenv.single_observation_space.shape[0]
@@ -326,14 +328,30 @@ def train(components, info, utilization=None):
                     adv = experience.b_advantages[mb]
                     ret = experience.b_returns[mb]
                 fused_obj = fused_loss and obs.is_cuda
+                fused_mb = False
                 with profile.train_forward, autocast(cfg):
-                    if fused_obj:
+                    if fused_obj and fused_ppo_supported(pol, obs):
+                        # the whole minibatch (trunks + LayerNorm/heads + PPO objective) as one
+                        # autograd node (policies/fused_ppo.py)
+                        fused_mb = True
+                        if cfg.norm_adv:
+                            if adv_ms is None:
+                                adv_ms = D.global_mean_std_rows(experience.b_advantages)
+                            ms = adv_ms[mb]
+                        else:
+                            ms = torch.tensor([0.0, 1.0], dtype=torch.float32, device=obs.device)
+                        if tail_coefs is None:
+                            tail_coefs = ppo_coefs(cfg, pol.soft_bound)
+                        loss, st = fused_ppo_loss(pol, obs, atn, log_probs, adv, ms, val, ret, tail_coefs)
+                    elif fused_obj:
                         mu, newvalue = pol.forward_train(obs)
                     else:
                         _, newlogprob, entropy, newvalue = components.policy(obs, action=atn)
                 with profile.train_misc:
                     adv = adv.reshape(-1)
-                    if fused_obj:
+                    if fused_mb:
+                        pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac, mbl_f = st.unbind(0)
+                    elif fused_obj:
                         # PPO objective in two HIP kernels (clean_pufferl/ppo_loss.py); the
                         # per-minibatch advantage mean / std of every minibatch at once
                         if cfg.norm_adv:

@@ -31,10 +31,15 @@ class _PPOObjective(torch.autograd.Function):
         return gmu, gv.view(ctx.value_shape), None, None, None, None, None, None, None, None
 
 
+def ppo_coefs(cfg, soft_bound):
+    """phc_ppo_coefs of a TrainConfig (the bound term only when bound_coef > 0)."""
+    return _native.ppo_coefs(cfg.clip_coef, cfg.vf_clip_coef, cfg.vf_coef, cfg.ent_coef,
+                             cfg.bound_coef if cfg.bound_coef > 0 else 0.0, soft_bound, cfg.clip_vloss)
+
+
 def ppo_objective(mu, value, log_sigma, actions, old_logprob, adv, adv_mean, adv_std, old_value, returns, cfg,
                   soft_bound):
-    coefs = _native.ppo_coefs(cfg.clip_coef, cfg.vf_clip_coef, cfg.vf_coef, cfg.ent_coef,
-                              cfg.bound_coef if cfg.bound_coef > 0 else 0.0, soft_bound, cfg.clip_vloss)
+    coefs = ppo_coefs(cfg, soft_bound)
     if adv_std is None:  # adv_mean is already the device [2] (mean, std) pair
         ms = adv_mean
     else:

@@ -12,9 +12,11 @@
 //   action = mu + std * noise (std = exp(sigma), clamped to 1e-6 in deterministic mode),
 //   logprob = sum_j Normal(mu, std).log_prob(action) — one launch instead of a LayerNorm kernel,
 //   two GEMMs and ~20 elementwise / reduction launches.  Rows are independent; a 320-thread
-//   block owns kActRows rows: LayerNorm one row per wave at a time (64 lanes x H/64 values), the
-//   actor's h rows kept in LDS, W_mu streamed through LDS in 64-deep k chunks, each thread
-//   accumulating 4 rows x 1 action of mu in fp32 (float4 LDS reads, 16 FMAs per 4-deep step).
+//   block owns kActRows = 8 rows (512 blocks at 4096 rows, two or more per CU): LayerNorm one
+//   row per wave (64 lanes x H/64 values, every row's loads issued before the first reduction),
+//   the actor's h rows kept in LDS; thread (half, group, action) accumulates 4 rows x 1 action
+//   of mu over one half of k in fp32, its W_mu row read as float4 straight from L2 (no staging
+//   barriers), the two halves added through LDS.
 #include "phc_common.h"
 
 namespace phc {
@@ -32,13 +34,28 @@ __global__ __launch_bounds__(256) void k_obs_half(const float *__restrict__ obs,
   const int c0 = (i - r * chunks) * 8;
   const int64_t src = rows ? rows[r] : r;
   const float *x = obs + src * d;
+  float xv[8], mv[8], vv[8];
+  if (c0 + 8 <= d && (((uintptr_t)(x + c0)) & 7) == 0) {  // 8-byte aligned run: float2 loads
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const float2 t = *reinterpret_cast<const float2 *>(x + c0 + e);
+      xv[e] = t.x; xv[e + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = c0 + e < d ? x[c0 + e] : 0.0f;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mv[e] = c0 + e < d ? mean[c0 + e] : 0.0f;
+    vv[e] = c0 + e < d ? var[c0 + e] : 1.0f;
+  }
   T o[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int c = c0 + e;
     float v = 0.0f;
-    if (c < d) {
-      v = (x[c] - mean[c]) / sqrtf(var[c] + eps);  // same expression as k_rms_normalize
+    if (c0 + e < d) {
+      v = (xv[e] - mv[e]) / sqrtf(vv[e] + eps);  // same expression as k_rms_normalize
       v = v < -clip ? -clip : (v > clip ? clip : v);
     }
     o[e] = (T)v;
@@ -49,12 +66,11 @@ __global__ __launch_bounds__(256) void k_obs_half(const float *__restrict__ obs,
 }
 
 // --------------------------------------------------------------- policy_act --
-constexpr int kActRows = 16;     // rows per block
-constexpr int kActK = 64;        // k chunk of W_mu staged in LDS
+constexpr int kActRows = 8;      // rows per block
 constexpr int kActMaxA = 72;     // actions supported (PHC_NUM_DOF + 3)
-constexpr int kActThreads = 320; // (kActRows / 4) row groups x up to 72 actions, 5 waves
-static_assert((kActRows / 4) * kActMaxA <= kActThreads, "one (row group, action) per thread");
-static_assert(kActMaxA * (kActK + 4) >= kActRows * kActMaxA, "log_prob terms reuse wts");
+constexpr int kActThreads = 320; // 2 k halves x 2 row groups x up to 72 actions (288), 5 waves
+constexpr int kActTasks = (2 * kActRows + kActThreads / 64 - 1) / (kActThreads / 64);  // LN rows per wave
+static_assert(2 * (kActRows / 4) * kActMaxA <= kActThreads, "one (k half, row group, action) per thread");
 
 __device__ __forceinline__ float wave_sum(float s) {
 #pragma unroll
@@ -98,38 +114,49 @@ __device__ __forceinline__ void ln_silu_row(float x[C][4], const float *__restri
 template <int C>
 __global__ __launch_bounds__(kActThreads) void k_policy_act(phc_policy_act_args a) {
   constexpr int H = C * 256;
-  constexpr int kWs = kActK + 4;  // padded row of the staged W_mu chunk ([j][k]: float4 reads conflict-free)
+  constexpr int kWaves = kActThreads / 64;
   __shared__ __attribute__((aligned(16))) float hs[kActRows][H];
-  __shared__ __attribute__((aligned(16))) float wts[kActMaxA][kWs];
+  __shared__ float part[kActRows][kActMaxA];  // the second k half's mu partials, then log_prob terms
   __shared__ float red[kActRows];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * kActRows;
   const int A = a.num_actions;
   const float *y = a.trunk_out;
 
-  // LayerNorm + SiLU: rows of both trunks, one wave per row
-  for (int q = wave; q < 2 * kActRows; q += kActThreads / 64) {
-    const int grp = q / kActRows, rr = q % kActRows;
-    const int64_t row = r0 + rr;
-    if (row >= a.rows) continue;
-    float x[C][4];
-    const float *src = y + ((int64_t)grp * a.rows + row) * H;
+  // LayerNorm + SiLU: task q = (trunk, row) of the block, one wave per task; all of a wave's
+  // row loads are issued before its first reduction
+  float x[kActTasks][C][4];
 #pragma unroll
-    for (int k = 0; k < C; ++k) {
-      const float4 t = *reinterpret_cast<const float4 *>(src + 4 * (lane + 64 * k));
-      x[k][0] = t.x; x[k][1] = t.y; x[k][2] = t.z; x[k][3] = t.w;
+  for (int t = 0; t < kActTasks; ++t) {
+    const int q = wave + kWaves * t;
+    const int grp = q / kActRows;
+    const int64_t row = r0 + q % kActRows;
+    if (q < 2 * kActRows && row < a.rows) {
+      const float *src = y + ((int64_t)grp * a.rows + row) * H;
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        const float4 v = *reinterpret_cast<const float4 *>(src + 4 * (lane + 64 * k));
+        x[t][k][0] = v.x; x[t][k][1] = v.y; x[t][k][2] = v.z; x[t][k][3] = v.w;
+      }
     }
-    ln_silu_row<C>(x, a.ln_gamma[grp], a.ln_beta[grp], lane, a.ln_eps);
+  }
+#pragma unroll
+  for (int t = 0; t < kActTasks; ++t) {
+    const int q = wave + kWaves * t;
+    const int grp = q / kActRows, rr = q % kActRows;
+    if (q >= 2 * kActRows || r0 + rr >= a.rows) continue;
+    ln_silu_row<C>(x[t], a.ln_gamma[grp], a.ln_beta[grp], lane, a.ln_eps);
     if (grp == 0) {
 #pragma unroll
       for (int k = 0; k < C; ++k)
-        *reinterpret_cast<float4 *>(&hs[rr][4 * (lane + 64 * k)]) = float4{x[k][0], x[k][1], x[k][2], x[k][3]};
+        *reinterpret_cast<float4 *>(&hs[rr][4 * (lane + 64 * k)]) =
+            float4{x[t][k][0], x[t][k][1], x[t][k][2], x[t][k][3]};
     } else {
       float s = 0.0f;
 #pragma unroll
       for (int k = 0; k < C; ++k) {
         const float *w = a.w_value + 4 * (lane + 64 * k);
-        s += x[k][0] * w[0] + x[k][1] * w[1] + x[k][2] * w[2] + x[k][3] * w[3];
+        s += x[t][k][0] * w[0] + x[t][k][1] * w[1] + x[t][k][2] * w[2] + x[t][k][3] * w[3];
       }
       s = wave_sum(s);
       if (lane == 0) red[rr] = s + a.b_value[0];
@@ -138,39 +165,39 @@ __global__ __launch_bounds__(kActThreads) void k_policy_act(phc_policy_act_args 
   __syncthreads();
   if (tid < kActRows && r0 + tid < a.rows) a.value[r0 + tid] = red[tid];
 
-  // mu head: thread (g, j) owns rows 4g..4g+3 of action j; per 4-deep k step one float4 of its
-  // W_mu row and one broadcast float4 of each h row, 16 FMAs
-  const int g = tid / A, j = tid - g * A;
-  const bool active = g < kActRows / 4;
+  // mu head: thread (kh, g, j) owns rows 4g..4g+3 of action j over k in [kh H/2, (kh+1) H/2);
+  // per 4-deep k step one float4 of its W_mu row (L2) and one broadcast float4 of each h row
+  constexpr int kGroups = kActRows / 4;
+  const int kh = tid / (kGroups * A), g = (tid / A) % kGroups, j = tid % A;
+  const bool active = tid < 2 * kGroups * A;
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int k0 = 0; k0 < H; k0 += kActK) {
-    __syncthreads();  // previous chunk no longer read
-    for (int e = tid; e < kActK * A; e += kActThreads) {
-      const int jj = e / kActK, kk = e - jj * kActK;
-      wts[jj][kk] = a.w_mu[(int64_t)jj * H + k0 + kk];  // coalesced along k
-    }
-    __syncthreads();
-    if (active) {
-#pragma unroll 4
-      for (int kk = 0; kk < kActK; kk += 4) {
-        const float4 w = *reinterpret_cast<const float4 *>(&wts[j][kk]);
+  if (active) {
+    const float *w = a.w_mu + (int64_t)j * H + kh * (H / 2);
+    const float *h0 = &hs[4 * g][kh * (H / 2)];
+#pragma unroll 8
+    for (int kk = 0; kk < H / 2; kk += 4) {
+      float4 wv;  // W_mu may be a view into a flat parameter buffer: 4-byte alignment only
+      wv.x = w[kk]; wv.y = w[kk + 1]; wv.z = w[kk + 2]; wv.w = w[kk + 3];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float4 h = *reinterpret_cast<const float4 *>(&hs[4 * g + r][k0 + kk]);
-          acc[r] += h.x * w.x;
-          acc[r] += h.y * w.y;
-          acc[r] += h.z * w.z;
-          acc[r] += h.w * w.w;
-        }
+      for (int r = 0; r < 4; ++r) {
+        const float4 h = *reinterpret_cast<const float4 *>(h0 + r * H + kk);
+        acc[r] += h.x * wv.x;
+        acc[r] += h.y * wv.y;
+        acc[r] += h.z * wv.z;
+        acc[r] += h.w * wv.w;
       }
     }
+    if (kh == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[4 * g + r][j] = acc[r];
+    }
   }
+  __syncthreads();
   // action / logprob: the Normal's log_prob terms per (row, action), summed per row in a fixed
   // order (deterministic: a captured rollout graph and the eager step give identical bits)
-  __syncthreads();  // wts no longer read: reused as the [kActRows][A] log_prob terms
-  float *lps = &wts[0][0];
   const float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
-  if (active) {
+  float lp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (active && kh == 0) {
     float sd = expf(a.log_sigma[j]);
     sd = sd > a.std_max ? a.std_max : sd;
     const float bj = a.b_mu[j];
@@ -179,18 +206,23 @@ __global__ __launch_bounds__(kActThreads) void k_policy_act(phc_policy_act_args 
       const int rr = 4 * g + r;
       const int64_t row = r0 + rr;
       if (row >= a.rows) break;
-      const float mu = acc[r] + bj;
+      const float mu = (acc[r] + part[rr][j]) + bj;
       const float act = mu + sd * a.noise[row * A + j];
       const float d = act - mu;
-      lps[rr * A + j] = -(d * d) / (2.0f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
+      lp[r] = -(d * d) / (2.0f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
       a.actions[row * A + j] = act;
       if (a.mu) a.mu[row * A + j] = mu;
     }
   }
+  __syncthreads();  // every mu partial has been read
+  if (active && kh == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[4 * g + r][j] = lp[r];
+  }
   __syncthreads();
   if (tid < kActRows && r0 + tid < a.rows) {
     float s = 0.0f;
-    for (int jj = 0; jj < A; ++jj) s += lps[tid * A + jj];
+    for (int jj = 0; jj < A; ++jj) s += part[tid][jj];
     a.logprob[r0 + tid] = s;
   }
 }

@@ -18,6 +18,8 @@
 namespace phc {
 
 constexpr int kPpoBlock = 256;
+constexpr int kPpoWaveRows = 16;                          // k_ppo_fwd: rows per wave
+constexpr int kPpoRows = kPpoWaveRows * kPpoBlock / 64;   // k_ppo_fwd: rows per block
 constexpr int kPpoStats = PHC_PPO_STATS;
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
 
@@ -37,28 +39,62 @@ __device__ __forceinline__ void dmax(float x, float y, float *gx, float *gy) {
   else { *gx = 0.5f; *gy = 0.5f; }
 }
 
+// one wave per kPpoWaveRows rows: the per-action log-prob / bound terms of a row are formed with
+// the actions across the lanes (coalesced row reads) and summed by a butterfly; lane i keeps row
+// i's sums, then lanes 0..kPpoWaveRows-1 finish their rows
+__device__ __forceinline__ float ppo_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(kPpoBlock) void k_ppo_fwd(PpoArgs p, float *__restrict__ row_coef,
                                                        float *__restrict__ partial) {
   __shared__ float red[kPpoStats][kPpoBlock / 64];
-  const int64_t r = (int64_t)blockIdx.x * kPpoBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t rbase = (int64_t)blockIdx.x * kPpoRows + wv * kPpoWaveRows;
+  const int64_t r = rbase + lane;
+  // per-action constants of the fixed-sigma Normal (std = exp(sigma), phc_policy.py decode_actions;
+  // Normal.log_prob / entropy use scale.log())
+  float var[2], ls[2];
+  bool act_ok[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = lane + 64 * h;
+    act_ok[h] = j < p.a;
+    const float sg = act_ok[h] ? expf(p.log_sigma[j]) : 1.0f;
+    ls[h] = logf(sg);
+    var[h] = sg * sg;
+  }
+  const float ent = ppo_wave_sum((act_ok[0] ? 0.5f + kLogSqrt2Pi + ls[0] : 0.0f) +
+                                 (act_ok[1] ? 0.5f + kLogSqrt2Pi + ls[1] : 0.0f));
+  const float b = p.c.soft_bound;
+  float lp = 0.0f, bound = 0.0f;
+#pragma unroll 4
+  for (int i = 0; i < kPpoWaveRows; ++i) {
+    const int64_t row = rbase + i;
+    const bool row_ok = row < p.m;  // wave-uniform
+    float tl = 0.0f, tb = 0.0f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!act_ok[h] || !row_ok) continue;
+      const int j = lane + 64 * h;
+      const float m = p.mu[row * p.a + j];
+      const float d = p.actions[row * p.a + j] - m;
+      tl += -(d * d) / (2.0f * var[h]) - ls[h] - kLogSqrt2Pi;
+      tb += m > b ? (m - b) * (m - b) : (m < -b ? (m + b) * (m + b) : 0.0f);
+    }
+    tl = ppo_wave_sum(tl);
+    tb = ppo_wave_sum(tb);
+    if (lane == i) {
+      lp = tl;
+      bound = tb;
+    }
+  }
   float s[kPpoStats];
 #pragma unroll
   for (int k = 0; k < kPpoStats; ++k) s[k] = 0.0f;
-  if (r < p.m) {
-    const float *mu = p.mu + r * p.a;
-    const float *act = p.actions + r * p.a;
-    const float b = p.c.soft_bound;
-    float lp = 0.0f, ent = 0.0f, bound = 0.0f;
-    for (int j = 0; j < p.a; ++j) {
-      const float sg = expf(p.log_sigma[j]);  // std = exp(sigma) (phc_policy.py decode_actions)
-      const float ls = logf(sg);               // Normal.log_prob / entropy use scale.log()
-      const float var = sg * sg;
-      const float d = act[j] - mu[j];
-      lp += -(d * d) / (2.0f * var) - ls - kLogSqrt2Pi;
-      ent += 0.5f + kLogSqrt2Pi + ls;
-      const float m = mu[j];
-      bound += m > b ? (m - b) * (m - b) : (m < -b ? (m + b) * (m + b) : 0.0f);
-    }
+  if (lane < kPpoWaveRows && r < p.m) {
     const float logratio = lp - p.old_logprob[r];
     const float ratio = expf(logratio);
     const float A = (p.adv[r] - p.adv_mean_std[0]) / (p.adv_mean_std[1] + 1e-8f);
@@ -95,13 +131,10 @@ __global__ __launch_bounds__(kPpoBlock) void k_ppo_fwd(PpoArgs p, float *__restr
     s[6] = bound;
   }
   // block reduction: wave sums by butterfly, then the 4 wave partials
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < kPpoStats; ++k) {
-    float v = s[k];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) red[k][w] = v;
+    const float v = ppo_wave_sum(s[k]);
+    if (lane == 0) red[k][wv] = v;
   }
   __syncthreads();
   if (threadIdx.x < kPpoStats) {
@@ -110,15 +143,29 @@ __global__ __launch_bounds__(kPpoBlock) void k_ppo_fwd(PpoArgs p, float *__restr
   }
 }
 
-// stats[0] = loss, then pg, v, ent, old_approx_kl, approx_kl, clipfrac, bound (means); one wave
-__global__ __launch_bounds__(64) void k_ppo_reduce(const float *__restrict__ partial, int blocks, int64_t m, int a,
-                                                   phc_ppo_coefs c, float *__restrict__ stats) {
+// stats[0] = loss, then pg, v, ent, old_approx_kl, approx_kl, clipfrac, bound (means): 256
+// threads accumulate strided block partials in double, then one wave adds the 256 sums in order
+__global__ __launch_bounds__(256) void k_ppo_reduce(const float *__restrict__ partial, int blocks, int64_t m, int a,
+                                                    phc_ppo_coefs c, float *__restrict__ stats) {
+  __shared__ double red[kPpoStats][256];
+  double acc[kPpoStats];
+#pragma unroll
+  for (int k = 0; k < kPpoStats; ++k) acc[k] = 0.0;
+  for (int i = threadIdx.x; i < blocks; i += 256)
+#pragma unroll
+    for (int k = 0; k < kPpoStats; ++k) acc[k] += partial[(int64_t)i * kPpoStats + k];
+#pragma unroll
+  for (int k = 0; k < kPpoStats; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
   const int k = threadIdx.x;
-  double acc = 0.0;
-  if (k < kPpoStats)
-    for (int i = 0; i < blocks; ++i) acc += partial[(int64_t)i * kPpoStats + k];
-  const float mean = (float)(k == 6 ? acc / ((double)m * a) : acc / (double)m);
-  if (k < kPpoStats) stats[1 + k] = mean;
+  float mean = 0.0f;
+  if (k < kPpoStats) {
+    double t = 0.0;
+    for (int i = 0; i < 256; ++i) t += red[k][i];
+    mean = (float)(k == 6 ? t / ((double)m * a) : t / (double)m);
+    stats[1 + k] = mean;
+  }
   const float pg = __shfl(mean, 0, 64), v = __shfl(mean, 1, 64), ent = __shfl(mean, 2, 64),
               bound = __shfl(mean, 6, 64);
   if (k == 0) stats[0] = pg - c.ent_coef * ent + c.vf_coef * v + c.bound_coef * bound;
@@ -158,7 +205,7 @@ static int check_ppo(const PpoArgs &p) {
 using namespace phc;
 
 extern "C" size_t phc_ppo_workspace_bytes(int64_t m) {
-  return m <= 0 ? 0 : (size_t)((m + kPpoBlock - 1) / kPpoBlock) * kPpoStats * sizeof(float);
+  return m <= 0 ? 0 : (size_t)((m + kPpoRows - 1) / kPpoRows) * kPpoStats * sizeof(float);
 }
 
 extern "C" int phc_ppo_loss_fwd(const float *mu, const float *log_sigma, const float *actions,
@@ -169,11 +216,11 @@ extern "C" int phc_ppo_loss_fwd(const float *mu, const float *log_sigma, const f
   PHC_REQUIRE(coefs && row_coef && stats && workspace, "ppo_loss_fwd: null output/workspace");
   const PpoArgs p{mu, log_sigma, actions, old_logprob, adv, adv_mean_std, value, old_value, returns, m, a, *coefs};
   if (int rc = check_ppo(p)) return rc;
-  const int blocks = (int)((m + kPpoBlock - 1) / kPpoBlock);
+  const int blocks = (int)((m + kPpoRows - 1) / kPpoRows);
   float *partial = static_cast<float *>(workspace);
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(k_ppo_fwd, dim3(blocks), dim3(kPpoBlock), 0, st, p, row_coef, partial);
-  hipLaunchKernelGGL(k_ppo_reduce, dim3(1), dim3(64), 0, st, partial, blocks, m, (int)a, *coefs, stats);
+  hipLaunchKernelGGL(k_ppo_reduce, dim3(1), dim3(256), 0, st, partial, blocks, m, (int)a, *coefs, stats);
   return check_launch("ppo_loss_fwd");
 }
 

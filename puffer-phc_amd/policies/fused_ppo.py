@@ -1,0 +1,104 @@
+"""The PPO minibatch as one autograd node on the device (R19 + R21).
+
+forward: MFMA twin trunks (twin_mlp.mfma_trunk_forward) -> phc_tail_ln_fwd (LayerNorm + SiLU of
+both trunks, the critic's value head) -> the fp32 mu head GEMM -> the PPO objective kernels
+(phc_ppo_loss_fwd).  backward: phc_ppo_loss_bwd (d mu, d value) -> d h_a = dmu W_mu and the split-K
+W_mu gradient (fp32 GEMMs) -> phc_tail_ln_bwd (LayerNorm + SiLU backward of both trunks; dy in the
+trunk's operand type; every remaining tail gradient as per-block column sums) -> the trunk
+backward.  Same math as PHCPolicy.forward_train + ppo_objective (reference:
+policies/phc_policy.py:16-61, clean_pufferl/core.py:298-352) without the ~30 elementwise, fill,
+copy and reduction launches autograd runs between those pieces; the unfused path stays for fp32
+storage and other shapes."""
+
+import torch
+
+from .. import _native as N
+from .twin_mlp import (_compute_dtype, _use_mfma, _weight_grad, _weight_grad_parts, direct_grads_bound,
+                       mfma_trunk_backward, mfma_trunk_forward)
+
+
+class FusedPPOLossFn(torch.autograd.Function):
+    """apply(x, weights, (ln_eps, log_sigma, coefs), data, n_trunk, *trunk_params, *tail_params)
+    -> (loss, stats [7]); tail_params = actor LN (w, b), critic LN (w, b), mu head (w, b), value
+    head (w, b); data = (actions, old_logprob, adv, adv_mean_std, old_value, returns)."""
+
+    @staticmethod
+    def forward(ctx, x, weights, cfg, data, n_trunk, *params):
+        eps, log_sigma, coefs = cfg
+        y, saved = mfma_trunk_forward(x, weights, True)
+        la_w, la_b, lc_w, lc_b, mu_w, mu_b, v_w, v_b = [p.detach() for p in params[n_trunk:]]
+        actions, old_logprob, adv, adv_ms, old_value, returns = data
+        with torch.no_grad(), torch.autocast("cuda", enabled=False):
+            tail = N.TailLN(y, (la_w, la_b), (lc_w, lc_b), eps, v_w, v_b)
+            h_a, value = tail.forward()
+            mu = torch.addmm(mu_b, h_a, mu_w.t())  # fp32 head, as HeadLinearFn
+            stats, row_coef = N.ppo_loss_fwd(mu, log_sigma, actions, old_logprob, adv, adv_ms, value, old_value,
+                                             returns, coefs)
+        ctx.saved, ctx.tail, ctx.params, ctx.n_trunk = saved, tail, params, n_trunk
+        ctx.ppo = (mu, log_sigma, actions, row_coef, coefs)
+        st = stats[1:]
+        ctx.mark_non_differentiable(st)
+        return stats[0], st
+
+    @staticmethod
+    def backward(ctx, g_loss, _g_stats):
+        saved, tail, params, n = ctx.saved, ctx.tail, ctx.params, ctx.n_trunk
+        mu, log_sigma, actions, row_coef, coefs = ctx.ppo
+        la_w, la_b, lc_w, lc_b, mu_w, mu_b, v_w, v_b = params[n:]
+        direct = direct_grads_bound(params)
+        with torch.no_grad(), torch.autocast("cuda", enabled=False):
+            gmu, gv = N.ppo_loss_bwd(mu, log_sigma, actions, row_coef, g_loss.float().contiguous(), coefs)
+            dh_a = torch.mm(gmu, mu_w.detach())
+            dy, part, lay = tail.backward(dh_a, gmu, gv, saved.xc.dtype)
+            sums = part.sum(0)
+            A, H = gmu.shape[1], tail.H
+
+            def seg(key, width):
+                return sums[lay[key]:lay[key] + width]
+
+            tail_srcs = [(seg("gamma", H), la_w), (seg("beta", H), la_b), (seg("gamma", 2 * H)[H:], lc_w),
+                         (seg("beta", 2 * H)[H:], lc_b), (seg("b_mu", A), mu_b), (seg("w_value", H), v_w),
+                         (seg("b_value", 1), v_b)]
+            db6 = seg("b6", 2 * H)
+            if direct:
+                jobs = [(_weight_grad_parts(gmu[None], tail.h_actor[None])[0], mu_w.grad)]
+                jobs += [(s.view(1, -1), p.grad) for s, p in tail_srcs]
+                N.reduce_into(jobs, accumulate=True)
+                mfma_trunk_backward(saved, dy, db6, params[:n], True)
+                grads = [None] * len(params)
+            else:
+                g_mu_w = _weight_grad(gmu[None], tail.h_actor[None])[0]
+                tg = {id(p): s.reshape(p.shape).clone() for s, p in tail_srcs}
+                tg[id(mu_w)] = g_mu_w
+                trunk = mfma_trunk_backward(saved, dy, db6.clone(), params[:n], False)
+                grads = list(trunk) + [tg[id(p)] for p in params[n:]]
+        ctx.saved = ctx.tail = ctx.ppo = None
+        return (None, None, None, None, None, *grads)
+
+
+def fused_ppo_supported(policy, obs):
+    """The fused minibatch needs the MFMA trunks (f16 / bf16 autocast), the half-precision GEMM
+    operand as input, hidden 512 and at most 72 actions."""
+    if not (getattr(policy, "fused", False) and getattr(policy, "fused_ln", False) and obs.is_cuda):
+        return False
+    dt = _compute_dtype()
+    if dt == torch.float32 or obs.dtype != dt or not _use_mfma(policy._twin, dt):
+        return False
+    h = policy._head
+    return (policy.actor_mlp[h].weight.shape[0] == N.TAIL_HIDDEN
+            and policy.mu[0].weight.shape[0] <= N.TAIL_MAX_ACTIONS)
+
+
+def fused_ppo_loss(policy, obs, actions, old_logprob, adv, adv_mean_std, old_value, returns, coefs):
+    """(loss, stats [7]: pg, v, entropy, old_approx_kl, approx_kl, clipfrac, bound) of one
+    minibatch; the backward writes every policy gradient."""
+    h = policy._head
+    la, lc = policy.actor_mlp[h], policy.critic_mlp[h]
+    vh, mh = policy.critic_mlp[h + 2], policy.mu[0]
+    tail = [la.weight, la.bias, lc.weight, lc.bias, mh.weight, mh.bias, vh.weight, vh.bias]
+    trunk = policy._twin.params()
+    f = lambda t: t.detach().float().contiguous().reshape(-1)  # noqa: E731
+    data = (actions.detach().float().contiguous(), f(old_logprob), f(adv), adv_mean_std.detach().float().contiguous(),
+            f(old_value), f(returns))
+    cfg = (la.eps, policy.sigma.detach().float().contiguous().reshape(-1), coefs)
+    return FusedPPOLossFn.apply(obs, policy._twin, cfg, data, len(trunk), *trunk, *tail)

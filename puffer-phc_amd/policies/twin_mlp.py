@@ -196,116 +196,149 @@ def mfma_operands(weights, dtype):
     return ops
 
 
+class MfmaTrunkSaved:
+    """What the MFMA trunk backward needs from its forward: the padded input, the transposed
+    weights, the pre-activations and the post-activations (layer inputs) of every layer."""
+
+    def __init__(self, xc, wt, pres, zs, K0):
+        self.xc, self.wt, self.pres, self.zs, self.K0 = xc, wt, pres, zs, K0
+        self.L = len(wt) + 1
+
+
+def mfma_trunk_forward(x, weights, need_grad):
+    """Both trunks on the hand-written MFMA GEMM (phc_gemm.hip) for f16 / bf16 operands: every
+    forward GEMM carries its bias + SiLU epilogue (pre-activation kept for backward in the operand
+    type, see PRE_HALF), the last layer its bias (fp32 out).  Returns (y [2, M, n] fp32,
+    MfmaTrunkSaved or None)."""
+    dt = _compute_dtype()
+    with torch.autocast("cuda", enabled=False):
+        ops = mfma_operands(weights, dt)
+        B = ops.b
+        M = x.shape[0]
+        K0 = weights.pairs[0][0].weight.shape[1]
+        Kp = ops.w0.shape[1]
+        if x.dtype == dt and x.shape[1] == Kp and x.is_contiguous():
+            xc = x  # already the padded GEMM operand (obs_half_input)
+        else:
+            xc = torch.empty((M, Kp), dtype=dt, device=x.device)
+            xc[:, :K0].copy_(x)
+            if Kp != K0:
+                xc[:, K0:].zero_()  # K padding (the padded weight columns are zero too)
+        n1 = ops.w0.shape[0] // 2
+        z = torch.empty((2, M, n1), dtype=dt, device=x.device)
+        pdt = dt if PRE_HALF else torch.float32
+        pre = torch.empty((M, 2 * n1), dtype=pdt, device=x.device) if need_grad else None
+        N.twin_gemm(xc, ops.w0, N.EPI_BIAS_SILU, z, (2, n1), bias=B[0], aux=pre, aux_layout=N.SPLIT,
+                    out_layout=N.GROUPED)
+        pres, zs = [pre], [z]
+        L = len(ops.w) + 1
+        for l in range(1, L):
+            n = ops.w[l - 1].shape[1]
+            if l < L - 1:
+                z = torch.empty((2, M, n), dtype=dt, device=x.device)
+                pre = torch.empty((2, M, n), dtype=pdt, device=x.device) if need_grad else None
+                N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS_SILU, z, (2, n), bias=B[l], aux=pre)
+                pres.append(pre)
+                zs.append(z)
+            else:
+                y = torch.empty((2, M, n), dtype=torch.float32, device=x.device)
+                N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS, y, (2, n), bias=B[l])
+    saved = MfmaTrunkSaved(xc, list(ops.wt), pres, zs, K0) if need_grad else None
+    return y, saved
+
+
+def mfma_trunk_backward(saved, g, db, params, direct):
+    """Backward of mfma_trunk_forward from g = d loss / d (last layer output) [2, M, n] in the
+    operand dtype and db = its fp32 column sums [2n] (the last layer's bias gradient; in direct
+    mode also [parts, 2n] partial rows, summed into the bias gradients).  Every
+    input-gradient GEMM carries its SiLU-backward + bias-gradient epilogue; weight gradients are
+    split-K library GEMMs (their reduction runs over the M rows).  direct: the gradients are
+    summed straight into the parameters' bound .grad views (phc_reduce_into) and None is
+    returned; otherwise the per-parameter gradient list (trunk params order)."""
+    L, K0 = saved.L, saved.K0
+    xc, WT, pres, zs = saved.xc, saved.wt, saved.pres, saved.zs
+    dt = xc.dtype
+    M = xc.shape[0]
+    grads = [None] * (2 * L)
+    jobs = []
+
+    def put(l, dW_parts, db):
+        """dW_parts: ([parts, 2n, k] or [2, parts, n, k] partials, layer-1 flag), db [2n]."""
+        if not direct:
+            grads[2 * l], grads[2 * l + 1] = dW_parts, db
+            return
+        wa, ba, wc, bc = params[4 * l:4 * l + 4]
+        n, k = wa.shape
+        if l == 0:
+            jobs.extend([(dW_parts[:, :n, :k], wa.grad), (dW_parts[:, n:, :k], wc.grad)])
+        else:
+            jobs.extend([(dW_parts[0], wa.grad), (dW_parts[1], wc.grad)])
+        if db.dim() == 2:  # [parts, 2n] partial rows (the fused PPO tail)
+            jobs.extend([(db[:, :n].unsqueeze(1), ba.grad), (db[:, n:].unsqueeze(1), bc.grad)])
+        else:
+            jobs.extend([(db[:n].view(1, n), ba.grad), (db[n:].view(1, n), bc.grad)])
+
+    with torch.autocast("cuda", enabled=False):
+        for l in range(L - 1, 0, -1):
+            put(l, _weight_grad_parts(g, zs[l - 1]) if direct else _weight_grad(g, zs[l - 1]), db)
+            k = WT[l - 1].shape[1]
+            db = torch.empty(2 * k, dtype=torch.float32, device=g.device)
+            if l > 1:
+                gp = torch.empty((2, M, k), dtype=dt, device=g.device)
+                N.twin_gemm(g, WT[l - 1], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[l - 1], bias_grad=db)
+            else:  # into the first layer's SPLIT [M, 2k] layout, the operand of its weight gradient
+                gp = torch.empty((M, 2 * k), dtype=dt, device=g.device)
+                N.twin_gemm(g, WT[0], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[0], aux_layout=N.SPLIT,
+                            out_layout=N.SPLIT, bias_grad=db)
+                if direct:
+                    put(0, _weight_grad_parts(gp[None], xc[None])[0], db)
+                else:
+                    put(0, _weight_grad(gp[None], xc[None])[0][:, :K0], db)
+            g = gp
+        if direct:
+            N.reduce_into(jobs, accumulate=True)
+            return None
+    out = []
+    for l in range(L):
+        dW, db = grads[2 * l], grads[2 * l + 1]
+        n = db.shape[0] // 2
+        dWa, dWc = (dW[:n], dW[n:]) if l == 0 else (dW[0], dW[1])
+        out += [dWa, db[:n], dWc, db[n:]]
+    return out
+
+
+def direct_grads_bound(params):
+    """True when every parameter's .grad is a bound dense fp32 view (FlatGrads): the backward
+    then writes gradients in place instead of returning them to autograd."""
+    return DIRECT_GRADS and all(p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+                                for p in params)
+
+
 class TwinTrunkMfmaFn(torch.autograd.Function):
-    """TwinTrunkFn on the hand-written MFMA GEMM (phc_gemm.hip) for f16 / bf16 operands: every
-    forward GEMM carries its bias + SiLU epilogue (pre-activation kept for backward in the
-    operand type, see PRE_HALF),
-    every input-gradient GEMM its SiLU-backward + bias-gradient epilogue, so no activation
-    makes a separate elementwise round trip.  Weight gradients stay split-K library GEMMs
-    (their reduction runs over the 32768 rows)."""
+    """TwinTrunkFn on the hand-written MFMA GEMM (mfma_trunk_forward / mfma_trunk_backward)."""
 
     @staticmethod
     def forward(ctx, x, weights, need_grad, *params):
-        dt = _compute_dtype()
-        with torch.autocast("cuda", enabled=False):
-            ops = mfma_operands(weights, dt)
-            B = ops.b
-            M = x.shape[0]
-            K0 = weights.pairs[0][0].weight.shape[1]
-            Kp = ops.w0.shape[1]
-            if x.dtype == dt and x.shape[1] == Kp and x.is_contiguous():
-                xc = x  # already the padded GEMM operand (obs_half_input)
-            else:
-                xc = torch.empty((M, Kp), dtype=dt, device=x.device)
-                xc[:, :K0].copy_(x)
-                if Kp != K0:
-                    xc[:, K0:].zero_()  # K padding (the padded weight columns are zero too)
-            n1 = ops.w0.shape[0] // 2
-            z = torch.empty((2, M, n1), dtype=dt, device=x.device)
-            pdt = dt if PRE_HALF else torch.float32
-            pre = torch.empty((M, 2 * n1), dtype=pdt, device=x.device) if need_grad else None
-            N.twin_gemm(xc, ops.w0, N.EPI_BIAS_SILU, z, (2, n1), bias=B[0], aux=pre, aux_layout=N.SPLIT,
-                        out_layout=N.GROUPED)
-            pres, zs = [pre], [z]
-            L = len(ops.w) + 1
-            for l in range(1, L):
-                n = ops.w[l - 1].shape[1]
-                if l < L - 1:
-                    z = torch.empty((2, M, n), dtype=dt, device=x.device)
-                    pre = torch.empty((2, M, n), dtype=pdt, device=x.device) if need_grad else None
-                    N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS_SILU, z, (2, n), bias=B[l], aux=pre)
-                    pres.append(pre)
-                    zs.append(z)
-                else:
-                    y = torch.empty((2, M, n), dtype=torch.float32, device=x.device)
-                    N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS, y, (2, n), bias=B[l])
+        y, saved = mfma_trunk_forward(x, weights, need_grad)
         if need_grad:
-            ctx.save_for_backward(xc, *ops.wt, *pres, *zs)  # pres: pre-activations, biases included
-            ctx.L, ctx.K0 = L, K0
+            ctx.saved = saved
             ctx.params = params
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        L, K0 = ctx.L, ctx.K0
-        saved = ctx.saved_tensors
-        xc, WT = saved[0], saved[1:L]
-        pres, zs = saved[L:2 * L - 1], saved[2 * L - 1:3 * L - 2]
-        dt = xc.dtype
-        M = xc.shape[0]
-        params = ctx.params
-        # with gradient views already bound (FlatGrads), the weight / bias gradients go straight
-        # into them (phc_reduce_into sums the split-K partials there): no per-parameter
-        # accumulation launches
-        direct = DIRECT_GRADS and all(p.grad is not None and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
-                                      for p in params)
-        grads = [None] * (2 * L)
-        jobs = []
-
-        def put(l, dW_parts, db):
-            """dW_parts: ([parts, 2n, k] or [2, parts, n, k] partials, layer-1 flag), db [2n]."""
-            if not direct:
-                grads[2 * l], grads[2 * l + 1] = dW_parts, db
-                return
-            wa, ba, wc, bc = params[4 * l:4 * l + 4]
-            n, k = wa.shape
-            if l == 0:
-                jobs.extend([(dW_parts[:, :n, :k], wa.grad), (dW_parts[:, n:, :k], wc.grad)])
-            else:
-                jobs.extend([(dW_parts[0], wa.grad), (dW_parts[1], wc.grad)])
-            jobs.extend([(db[:n].view(1, n), ba.grad), (db[n:].view(1, n), bc.grad)])
-
+        saved, params = ctx.saved, ctx.params
+        direct = direct_grads_bound(params)
         with torch.autocast("cuda", enabled=False):
             gy = gy.float().contiguous()
-            n = gy.shape[2]
+            M, n = gy.shape[1], gy.shape[2]
             db = torch.empty(2 * n, dtype=torch.float32, device=gy.device)
-            g = torch.empty(gy.shape, dtype=dt, device=gy.device)
+            g = torch.empty(gy.shape, dtype=saved.xc.dtype, device=gy.device)
             N.act_bwd(gy, N.GROUPED, None, N.GROUPED, g, N.GROUPED, db, M, 2, n, N.ACT_NONE)
-            for l in range(L - 1, 0, -1):
-                put(l, _weight_grad_parts(g, zs[l - 1]) if direct else _weight_grad(g, zs[l - 1]), db)
-                k = WT[l - 1].shape[1]
-                db = torch.empty(2 * k, dtype=torch.float32, device=g.device)
-                if l > 1:
-                    gp = torch.empty((2, M, k), dtype=dt, device=g.device)
-                    N.twin_gemm(g, WT[l - 1], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[l - 1], bias_grad=db)
-                else:  # into the first layer's SPLIT [M, 2k] layout, the operand of its weight gradient
-                    gp = torch.empty((M, 2 * k), dtype=dt, device=g.device)
-                    N.twin_gemm(g, WT[0], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[0], aux_layout=N.SPLIT,
-                                out_layout=N.SPLIT, bias_grad=db)
-                    if direct:
-                        put(0, _weight_grad_parts(gp[None], xc[None])[0], db)
-                    else:
-                        put(0, _weight_grad(gp[None], xc[None])[0][:, :K0], db)
-                g = gp
-            if direct:
-                N.reduce_into(jobs, accumulate=True)
-                return (None, None, None) + (None,) * (4 * L)
-        out = []
-        for l in range(L):
-            dW, db = grads[2 * l], grads[2 * l + 1]
-            n = db.shape[0] // 2
-            dWa, dWc = (dW[:n], dW[n:]) if l == 0 else (dW[0], dW[1])
-            out += [dWa, db[:n], dWc, db[n:]]
+        out = mfma_trunk_backward(saved, g, db, params, direct)
+        ctx.saved = None
+        if direct:
+            return (None, None, None) + (None,) * len(params)
         return (None, None, None, *out)
 
 
