@@ -48,6 +48,7 @@ phc_amd_path.register()
 
 BYTES_PER_ENV_STEP = 10886
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+MFMA_F16_PEAK_TFS = 2500.0  # dense f16 / bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
 DEFAULTS = {"env": (200, 20), "rollout": (64, 8), "ppo": (3, 1)}
 
 
@@ -212,9 +213,13 @@ def main():
     for _ in range(args.warmup):
         runner.step()
     torch.cuda.synchronize()
-    from puffer_phc_amd._native import KernelTimer
+    from puffer_phc_amd._native import KernelTimer, gemm_set_timer
 
     timer = env.env.kernel_timer = KernelTimer(capacity=max(4096, 64 * args.steps))
+    # every phc_twin_gemm launch outside the replayed rollout graph (the training trunks' fused-
+    # epilogue GEMMs) timed by its own dispatch events, with its 2 m n k FLOPs
+    gtimer = KernelTimer(capacity=max(4096, 256 * args.steps))
+    gemm_set_timer(gtimer)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -232,6 +237,9 @@ def main():
     env_steps = timer.count  # phc_env_step launches in the timed region, each timed by its dispatch events
     kern_s = timer.total_ms() / max(env_steps, 1) * 1e-3
     env.env.kernel_timer = None
+    gemm_set_timer(None)
+    gemm_launches, gemm_flops = gtimer.count, gtimer.work
+    gemm_s = gtimer.total_ms() * 1e-3 if gemm_launches else 0.0
     t = torch.tensor([elapsed, kern_s], dtype=torch.float64, device=device)
     tot = torch.tensor([float(processed)], dtype=torch.float64, device=device)
     if world > 1:
@@ -285,12 +293,23 @@ def main():
                        if args.mode != "env" else None,
                        "optimizer_steps_skipped_by_loss_scaler": skipped,
                        "phase_ms_per_step": runner.phase_ms(args.steps)},
-            "roofline": {"bound": "hbm", "kernel": "phc_env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel_us": kern_s * 1e6, "launches_timed": env_steps,
-                         "algorithmic_bytes_per_env_step": BYTES_PER_ENV_STEP},
             "cpu_baseline": cpu,
         }
+        env_roof = {"bound": "hbm", "kernel": "phc_env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "kernel_us": kern_s * 1e6, "launches_timed": env_steps,
+                    "algorithmic_bytes_per_env_step": BYTES_PER_ENV_STEP}
+        if gemm_launches:
+            # the dominant kernel of the PPO / rollout modes: the trunk GEMMs (MFMA-bound)
+            tfs = gemm_flops / gemm_s / 1e12
+            out["roofline"] = {"bound": "mfma", "kernel": "phc_twin_gemm (fused-epilogue trunk GEMMs, training)",
+                               "achieved": tfs, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
+                               "frac": tfs / MFMA_F16_PEAK_TFS, "traffic": None,
+                               "kernel_us": gemm_s / gemm_launches * 1e6, "launches_timed": gemm_launches,
+                               "algorithmic_flops_per_launch": gemm_flops / gemm_launches}
+            out["roofline_env_step"] = env_roof
+        else:
+            out["roofline"] = env_roof
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -131,6 +131,10 @@ void phc_timer_destroy(phc_kernel_timer *timer);
 void phc_timer_reset(phc_kernel_timer *timer);
 int32_t phc_timer_count(const phc_kernel_timer *timer);
 double phc_timer_total_ms(phc_kernel_timer *timer);
+double phc_timer_work(const phc_kernel_timer *timer); /* algorithmic work of the timed launches (GEMM: FLOPs) */
+/* phc_twin_gemm launches outside graph capture record into `timer` (NULL: off) with their
+ * 2 m n k batch FLOPs; a measurement aid for bench.py's GEMM roofline. */
+void phc_gemm_set_timer(phc_kernel_timer *timer);
 int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
                        phc_kernel_timer *timer, void *stream);
 

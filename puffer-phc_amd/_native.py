@@ -138,6 +138,8 @@ _EXPORTS = {
     "phc_timer_reset": (None, [c_vp]),
     "phc_timer_count": (ctypes.c_int32, [c_vp]),
     "phc_timer_total_ms": (ctypes.c_double, [c_vp]),
+    "phc_timer_work": (ctypes.c_double, [c_vp]),
+    "phc_gemm_set_timer": (None, [c_vp]),
     "phc_env_step_timed": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                            ctypes.POINTER(StepParamsC), c_vp, c_vp]),
     "phc_reset_envs": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
@@ -375,6 +377,16 @@ class KernelTimer:
         if ms < 0:
             raise RuntimeError("phc_timer_total_ms failed")
         return ms
+
+    @property
+    def work(self):
+        """Algorithmic work of the timed launches (phc_twin_gemm: FLOPs)."""
+        return lib().phc_timer_work(self.handle)
+
+
+def gemm_set_timer(timer):
+    """Time every phc_twin_gemm launch outside graph capture into `timer` (None: off)."""
+    lib().phc_gemm_set_timer(timer.handle if timer is not None else None)
 
     def __del__(self):
         if getattr(self, "handle", None) and _lib is not None:

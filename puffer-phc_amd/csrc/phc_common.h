@@ -4,6 +4,7 @@
 
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "phc.h"
 #include "phc_quat.h"
@@ -23,6 +24,18 @@ int check_launch(const char *what);
   } while (0)
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace phc
+
+// measurement timer (phc_timer_*): one start/stop event pair per timed launch, recorded by the
+// dispatch itself, plus the algorithmic work (bytes or FLOPs) the timed launches did
+struct phc_kernel_timer {
+  std::vector<hipEvent_t> start, stop;
+  int32_t used = 0;
+  double work = 0.0;
+};
+
+namespace phc {
 
 constexpr int kBodies = PHC_NUM_BODIES;
 constexpr int kRec = PHC_BODY_STRIDE;  // floats per rigid-body record

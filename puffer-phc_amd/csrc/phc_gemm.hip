@@ -23,6 +23,8 @@
 // to the last row, stores are masked); k must be a multiple of 64.
 #include "phc_common.h"
 
+#include <hip/hip_ext.h>
+
 #include <cstdlib>
 #include <type_traits>
 
@@ -464,6 +466,9 @@ static void gemm_tile_dims(int cfg, int *bm, int *bn) {
   *bn = cfg == kCfg256sq ? 256 : 128;
 }
 
+static phc_kernel_timer *g_gemm_timer = nullptr;  // bench.py measurement aid (phc_gemm_set_timer)
+static thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;  // this launch's timer events
+
 template <typename T, typename OutT, int EPI, typename TL>
 static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
   auto kernel = k_twin_gemm<T, OutT, EPI, TL>;
@@ -473,7 +478,10 @@ static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
     return true;
   }();
   (void)attr;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
+  if (g_ev0)
+    hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g_ev0, g_ev1, 0, g);
+  else
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
 }
 
 template <typename T, typename OutT, int EPI>
@@ -506,6 +514,8 @@ static void launch_gemm(int dtype, int out_dtype, int epi, int cfg, const GemmAr
 }  // namespace phc
 
 using namespace phc;
+
+extern "C" void phc_gemm_set_timer(phc_kernel_timer *timer) { g_gemm_timer = timer; }
 
 extern "C" size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_t n) {
   if (m <= 0 || batch <= 0 || n <= 0) return 0;
@@ -564,7 +574,18 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
   g.discard = discard ? 1 : 0;
   hipStream_t st = as_stream(stream);
+  g_ev0 = g_ev1 = nullptr;
+  if (g_gemm_timer && g_gemm_timer->used < (int32_t)g_gemm_timer->start.size()) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+      g_ev0 = g_gemm_timer->start[g_gemm_timer->used];
+      g_ev1 = g_gemm_timer->stop[g_gemm_timer->used];
+      g_gemm_timer->used += 1;
+      g_gemm_timer->work += 2.0 * (double)d->m * d->n * d->k * d->batch;
+    }
+  }
   launch_gemm(d->dtype, d->out_dtype, d->epilogue, cfg, g, blocks, st);
+  g_ev0 = g_ev1 = nullptr;
   if (bias_grad) {
     const int c = d->batch * d->n;
     hipLaunchKernelGGL(k_colsum<>, dim3((unsigned)((c + 63) / 64)), dim3(256), 0, st,

@@ -495,12 +495,8 @@ extern "C" int phc_motion_state(const phc_motion_lib *lib, const int64_t *ids, c
   return check_launch("motion_state");
 }
 
-// Kernel timer: start/stop events recorded by the dispatch itself (hipExtLaunchKernel), so the
-// measured span is the kernel's own execution, as rocprofv3 reports it.
-struct phc_kernel_timer {
-  std::vector<hipEvent_t> start, stop;
-  int32_t used = 0;
-};
+// Kernel timer (struct in phc_common.h): start/stop events recorded by the dispatch itself
+// (hipExtLaunchKernel), so the measured span is the kernel's own execution, as rocprofv3 reports it.
 
 extern "C" phc_kernel_timer *phc_timer_create(int32_t capacity) {
   if (capacity <= 0) return nullptr;
@@ -526,8 +522,13 @@ extern "C" void phc_timer_destroy(phc_kernel_timer *t) {
 }
 
 extern "C" void phc_timer_reset(phc_kernel_timer *t) {
-  if (t) t->used = 0;
+  if (t) {
+    t->used = 0;
+    t->work = 0.0;
+  }
 }
+
+extern "C" double phc_timer_work(const phc_kernel_timer *t) { return t ? t->work : 0.0; }
 
 extern "C" int32_t phc_timer_count(const phc_kernel_timer *t) { return t ? t->used : 0; }
 
