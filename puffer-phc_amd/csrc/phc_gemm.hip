@@ -94,6 +94,14 @@ __device__ __forceinline__ float gemm_sigmoid(float a) {
 }
 __device__ __forceinline__ float gemm_silu(float a) { return a * gemm_sigmoid(a); }
 
+// workgroup barrier for the epilogue's LDS hand-offs: waits for this wave's LDS operations only
+// (lgkmcnt), not for its global stores (__syncthreads' fence waits vmcnt(0)), so the stores of one
+// image pass drain while the next pass runs, and past the end of the block while the CU's next
+// tile starts its main loop
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <typename OutT> __device__ __forceinline__ void gemm_store(void *p, int64_t off, float v) {
   static_cast<OutT *>(p)[off] = (OutT)v;
 }
@@ -295,7 +303,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
   };
 #pragma unroll
   for (int pass = 0; pass < TL::kEpPasses; ++pass) {
-    __syncthreads();  // operand tiles / the previous pass's image are no longer read
+    lds_barrier();  // operand tiles / the previous pass's image are no longer read
 #pragma unroll
     for (int i = pass * TL::kEpMI; i < (pass + 1) * TL::kEpMI; ++i)
 #pragma unroll
@@ -306,7 +314,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
           const int c = wn * TL::TN + j * 16 + (lane & 15);
           ep[r * BN + (c ^ (((r >> 2) & 3) << 4))] = acc[i][j][e];
         }
-    __syncthreads();
+    lds_barrier();
     if (full) {
       // whole tile in range, 4 whole columns per thread: offsets are base + row * stride, rows
       // in batches of U; a half-precision aux is software-pipelined (batch b + 1's loads in
@@ -424,13 +432,13 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
       for (int q = 0; q < 4; ++q) csum[q] += __shfl_xor(csum[q], 32, 64);
     }
     constexpr int kWaveRows = kColThreads >= 64 ? 1 : 64 / kColThreads;  // rows one wave spans
-    __syncthreads();  // the epilogue image is no longer read
+    lds_barrier();  // the epilogue image is no longer read
     if (lane < 64 / kWaveRows) {
       const int wc = (kColThreads >= 64 ? (tid % kColThreads) : lane) * 4;
       const int slot = kColThreads >= 64 ? (tid / kColThreads) : wave;
       *reinterpret_cast<float4 *>(&ep[slot * BN + wc]) = float4{csum[0], csum[1], csum[2], csum[3]};
     }
-    __syncthreads();
+    lds_barrier();
     constexpr int kSlots = kColThreads >= 64 ? kRowGroups : TL::kWaves;
     if (tid < kColThreads) {
       float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
