@@ -302,9 +302,14 @@ def main():
         if gemm_launches:
             # the dominant kernel of the PPO / rollout modes: the trunk GEMMs (MFMA-bound)
             tfs = gemm_flops / gemm_s / 1e12
+            gtraffic = None  # HBM bytes per launch of the same launches (rocprofv3 PMC, tools/profile_round.sh)
+            gf = os.path.join(ROOT, "profiles", f"traffic_gemm_{args.envs}.json")
+            if os.path.exists(gf):
+                with open(gf) as f:
+                    gtraffic = json.load(f).get("bytes_per_launch")
             out["roofline"] = {"bound": "mfma", "kernel": "phc_twin_gemm (fused-epilogue trunk GEMMs, training)",
                                "achieved": tfs, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
-                               "frac": tfs / MFMA_F16_PEAK_TFS, "traffic": None,
+                               "frac": tfs / MFMA_F16_PEAK_TFS, "traffic": gtraffic, "traffic_unit": "bytes",
                                "kernel_us": gemm_s / gemm_launches * 1e6, "launches_timed": gemm_launches,
                                "algorithmic_flops_per_launch": gemm_flops / gemm_launches}
             out["roofline_env_step"] = env_roof
