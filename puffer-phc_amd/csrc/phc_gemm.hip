@@ -457,8 +457,8 @@ using Tile128x2 = Tile<128, 128, 2, 2, 2>;
 using Tile256sq = Tile<256, 256, 2, 4, 2>;
 enum { kCfg128 = 0, kCfg256sq = 2 };
 
-// 256 x 256 tiles when they still give every CU two or more tiles, else 128 x 128 (the
-// rollout's 4096-row GEMMs)
+// 256 x 256 tiles when they still give every CU a tile (measured: the rollout's 4096-row first
+// layer, 256 tiles, 43 vs 48 us), else 128 x 128 (the other 4096-row rollout GEMMs)
 static int gemm_config(int64_t m, int n, int batch) {
   static const int forced = [] {
     const char *e = getenv("PHC_GEMM_CFG");  // tuning aid (tools/twin_gemm_probe.py)
@@ -466,7 +466,7 @@ static int gemm_config(int64_t m, int n, int batch) {
   }();
   if (forced >= 0) return forced;
   const int64_t big = ((m + 255) / 256) * ((n + 255) / 256) * batch;
-  return big >= 512 ? kCfg256sq : kCfg128;
+  return big >= 256 ? kCfg256sq : kCfg128;
 }
 
 static void gemm_tile_dims(int cfg, int *bm, int *bn) {

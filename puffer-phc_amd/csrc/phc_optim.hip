@@ -62,40 +62,62 @@ __global__ __launch_bounds__(kOptBlock) void k_grad_partials(const float *__rest
   }
 }
 
-// one wave: per-segment norms (segment j owns blocks [seg_blk[j], seg_blk[j+1])), clip
-// coefficient, skip decision, loss-scale update, Adam step / bias corrections -> st
-__global__ __launch_bounds__(64) void k_opt_finish(const double *__restrict__ part_sq, const int *__restrict__ part_bad,
-                                                   const double *__restrict__ part_l2,
-                                                   const int64_t *__restrict__ blk_range,
-                                                   const int32_t *__restrict__ seg_blk, int nseg,
-                                                   phc_adam_params hp, phc_opt_state *__restrict__ st,
-                                                   float *__restrict__ norm_out) {
-  const int lane = threadIdx.x;
+// per-segment norms (segment j owns blocks [seg_blk[j], seg_blk[j+1])), clip coefficient, skip
+// decision, loss-scale update, Adam step / bias corrections -> st.  One 1024-thread block: wave w
+// takes segments w, w + 16, ...; its lanes stride over the segment's block partials and reduce by
+// butterfly, the 16 wave totals are added in wave order (a fixed order: deterministic)
+constexpr int kFinThreads = 1024, kFinWaves = kFinThreads / 64;
+__global__ __launch_bounds__(kFinThreads) void k_opt_finish(const double *__restrict__ part_sq,
+                                                            const int *__restrict__ part_bad,
+                                                            const double *__restrict__ part_l2,
+                                                            const int64_t *__restrict__ blk_range,
+                                                            const int32_t *__restrict__ seg_blk, int nseg,
+                                                            phc_adam_params hp, phc_opt_state *__restrict__ st,
+                                                            float *__restrict__ norm_out) {
+  __shared__ double s_tot[kFinWaves], s_norm[kFinWaves], s_l2[kFinWaves];
+  __shared__ int s_bad[kFinWaves];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float inv = hp.use_loss_scale ? 1.0f / st->loss_scale : 1.0f;
   double tot = 0.0, norm_sum = 0.0, l2 = 0.0;
   int bad = 0;
-  for (int j = lane; j < nseg; j += 64) {  // segment sums in block order
+  for (int j = wave; j < nseg; j += kFinWaves) {
     double sq = 0.0, dl = 0.0;
-    for (int b = seg_blk[j]; b < seg_blk[j + 1]; ++b) {
+    int bd = 0;
+    for (int b = seg_blk[j] + lane; b < seg_blk[j + 1]; b += 64) {
       sq += part_sq[b];
-      bad |= part_bad[b];
+      bd |= part_bad[b];
       if (part_l2) dl += part_l2[b];
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      sq += __shfl_xor(sq, o, 64);
+      dl += __shfl_xor(dl, o, 64);
+      bd |= __shfl_xor(bd, o, 64);
     }
     tot += sq;
     norm_sum += sqrt(sq) * (double)inv;
+    bad |= bd;
     if (part_l2 && seg_blk[j + 1] > seg_blk[j]) {  // mean over the parameter's elements
       const int64_t n = blk_range[2 * (seg_blk[j + 1] - 1) + 1] - blk_range[2 * seg_blk[j]];
       l2 += dl / (double)n;
     }
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    tot += __shfl_xor(tot, o, 64);
-    norm_sum += __shfl_xor(norm_sum, o, 64);
-    l2 += __shfl_xor(l2, o, 64);
-    bad |= __shfl_xor(bad, o, 64);
+  if (lane == 0) {
+    s_tot[wave] = tot;
+    s_norm[wave] = norm_sum;
+    s_l2[wave] = l2;
+    s_bad[wave] = bad;
   }
-  if (lane != 0) return;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  tot = norm_sum = l2 = 0.0;
+  bad = 0;
+  for (int w = 0; w < kFinWaves; ++w) {
+    tot += s_tot[w];
+    norm_sum += s_norm[w];
+    l2 += s_l2[w];
+    bad |= s_bad[w];
+  }
   // clip_grad_norm_: coefficient from the global norm of the (unscaled) gradients
   const float total_norm = (float)(sqrt(tot) * (double)inv);
   float clip = hp.max_norm / (total_norm + 1e-6f);
@@ -241,7 +263,7 @@ extern "C" int phc_opt_step(float *param, const float *grad, float *exp_avg, flo
   int *part_bad = reinterpret_cast<int *>(part_sq + 2 * (int64_t)nblk);
   hipLaunchKernelGGL(k_grad_partials, dim3((unsigned)nblk), dim3(kOptBlock), 0, st, grad, blk_range, part_sq,
                      part_bad, param, param_init, part_l2);
-  hipLaunchKernelGGL(k_opt_finish, dim3(1), dim3(64), 0, st, part_sq, part_bad, part_l2, blk_range, seg_blk,
+  hipLaunchKernelGGL(k_opt_finish, dim3(1), dim3(kFinThreads), 0, st, part_sq, part_bad, part_l2, blk_range, seg_blk,
                      (int)nseg, *hp, state, norm_out);
   const int64_t quads = (n + 3) / 4;
   const int64_t blocks = std::min<int64_t>((quads + kOptBlock - 1) / kOptBlock, 4096);
