@@ -61,7 +61,9 @@ def _split_k(m, n, k, groups):
     and the fp32 partials summed (measured: tools/gemm_shapes.py)."""
     tiles = max(1, -(-n // 256) * -(-k // 256) * groups)
     s = 1
-    while s * 2 * tiles <= 256 and s < 32 and m % (s * 2) == 0 and m // (s * 2) >= 1024:
+    # at most 8 chunks: past that the fp32 partials' round trip costs more than the extra
+    # workgroups gain (tools/wgrad_probe.py: 512x512 layer 82 us at S=32, 61 us at S=8)
+    while s * 2 * tiles <= 256 and s < 8 and m % (s * 2) == 0 and m // (s * 2) >= 1024:
         s *= 2
     return s
 
