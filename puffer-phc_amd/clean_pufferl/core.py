@@ -84,7 +84,9 @@ def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=Non
     if train_cfg.compile:
         policy = torch.compile(policy)
     autocast(train_cfg)  # validates the precision name
-    flat_grads = D.FlatGrads(uncompiled_policy.parameters())
+    inner = getattr(uncompiled_policy, "policy", uncompiled_policy)
+    order = inner.grad_ready_order() if hasattr(inner, "grad_ready_order") else None
+    flat_grads = D.FlatGrads(uncompiled_policy.parameters(), order=order)
     fp16 = train_cfg.precision == "fp16"
     if optimizer is None:
         if next(policy.parameters()).is_cuda:
@@ -410,8 +412,9 @@ def train(components, info, utilization=None):
                     flat.zero()
                     opt, scaler = components.optimizer, components.scaler
                     if isinstance(opt, FlatAdam):
+                        flat.overlap_begin()  # data parallel: per-layer all-reduces during the backward
                         opt.scale(loss).backward()  # loss * S under fp16 loss scaling
-                        flat.allreduce_mean()
+                        flat.overlap_finish()
                         gnorm = opt.fused_step(cfg.max_grad_norm)[0]  # unscale, clip, skip-on-inf, Adam
                     elif scaler is None:
                         loss.backward()

@@ -48,19 +48,71 @@ def init_from_env(backend=None):
 
 
 class FlatGrads:
-    """Parameters' gradients as views into one flat buffer, all-reduced (averaged) in buckets."""
+    """Parameters' gradients as views into one flat buffer, all-reduced (averaged) in buckets.
 
-    def __init__(self, params, bucket_bytes=32 << 20):
-        self.params = [p for p in params if p.requires_grad]
+    `order` (optional) lists parameters in the order the backward finishes their gradients
+    (PHCPolicy.grad_ready_order: the PPO tail, then the trunk layers from the last to the first);
+    the flat buffer is laid out in that order, so during an overlapped backward
+    (overlap_begin / overlap_finish) each group the backward reports done is one contiguous
+    slice whose all-reduce runs on RCCL's stream while the earlier layers' gradients are still
+    being computed."""
+
+    def __init__(self, params, bucket_bytes=32 << 20, order=None):
+        params = [p for p in params if p.requires_grad]
+        if order is not None:
+            first = [p for p in order if p.requires_grad]
+            ids = {id(p) for p in first}
+            params = first + [p for p in params if id(p) not in ids]
+        self.params = params
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._range = {}
         off = 0
         for p in self.params:
             k = p.numel()
             p.grad = self.flat[off:off + k].view_as(p)
+            self._range[id(p)] = (off, off + k)
             off += k
         self.bucket = max(1, bucket_bytes // 4)
+        self._works = None
+        self._done = None
+
+    def overlap_begin(self):
+        """Install the gradient-ready hook for one backward (a no-op without data parallelism)."""
+        if not is_dist():
+            return
+        from .policies import twin_mlp
+        self._works, self._done = [], set()
+        twin_mlp.GRAD_READY = self._on_ready
+
+    def _on_ready(self, params):
+        """All-reduce the (contiguous) slices of parameters whose gradients are final, async."""
+        spans = sorted(self._range[id(p)] for p in params if id(p) in self._range and id(p) not in self._done)
+        for p in params:
+            self._done.add(id(p))
+        s0 = e0 = None
+        for s, e in spans + [(None, None)]:
+            if s is not None and e0 == s:
+                e0 = e
+                continue
+            if s0 is not None:
+                self._works.append(dist.all_reduce(self.flat[s0:e0], async_op=True))
+            s0, e0 = s, e
+
+    def overlap_finish(self):
+        """Reduce every gradient not reported during the backward, wait, average."""
+        if not is_dist():
+            return
+        from .policies import twin_mlp
+        twin_mlp.GRAD_READY = None
+        rest = [p for p in self.params if id(p) not in self._done]
+        if rest:
+            self._on_ready(rest)
+        for w in self._works:
+            w.wait()
+        self._works, self._done = None, None
+        self.flat.div_(world_size())
 
     def zero(self):
         self.flat.zero_()

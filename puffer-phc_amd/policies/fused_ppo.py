@@ -13,6 +13,7 @@ storage and other shapes."""
 import torch
 
 from .. import _native as N
+from . import twin_mlp
 from .twin_mlp import (_compute_dtype, _use_mfma, _weight_grad, _weight_grad_parts, direct_grads_bound,
                        mfma_trunk_backward, mfma_trunk_forward)
 
@@ -64,6 +65,8 @@ class FusedPPOLossFn(torch.autograd.Function):
                 jobs = [(_weight_grad_parts(gmu[None], tail.h_actor[None])[0], mu_w.grad)]
                 jobs += [(s.view(1, -1), p.grad) for s, p in tail_srcs]
                 N.reduce_into(jobs, accumulate=True)
+                if twin_mlp.GRAD_READY is not None:  # data parallel: the tail's all-reduce starts now
+                    twin_mlp.GRAD_READY(params[n:])
                 mfma_trunk_backward(saved, dy, db6, params[:n], True)
                 grads = [None] * len(params)
             else:

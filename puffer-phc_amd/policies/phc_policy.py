@@ -39,6 +39,19 @@ class PHCPolicy(DiscriminatorPolicy):
         self.fused_ln = True  # LayerNorm + SiLU of both trunks in one kernel (False: torch modules)
         self._critic_trunk = None
 
+    def grad_ready_order(self):
+        """Parameters in the order the fused minibatch backward finishes their gradients (the
+        PPO tail, then the trunk layers from the last to the first): distributed.FlatGrads lays
+        the flat gradient buffer out this way so its all-reduce overlaps the backward."""
+        h = self._head
+        la, lc = self.actor_mlp[h], self.critic_mlp[h]
+        vh, mh = self.critic_mlp[h + 2], self.mu[0]
+        order = [la.weight, la.bias, lc.weight, lc.bias, mh.weight, mh.bias, vh.weight, vh.bias]
+        trunk = self._twin.params()
+        for l in range(len(trunk) // 4 - 1, -1, -1):
+            order += trunk[4 * l:4 * l + 4]
+        return order
+
     def _compute_dtype(self):
         return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else torch.float32
 

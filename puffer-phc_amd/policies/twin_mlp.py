@@ -279,6 +279,10 @@ def mfma_trunk_backward(saved, g, db, params, direct):
             jobs.extend([(db[:, :n].unsqueeze(1), ba.grad), (db[:, n:].unsqueeze(1), bc.grad)])
         else:
             jobs.extend([(db[:n].view(1, n), ba.grad), (db[n:].view(1, n), bc.grad)])
+        if GRAD_READY is not None:  # data parallel: this layer's gradients now, then its all-reduce
+            N.reduce_into(jobs, accumulate=True)
+            jobs.clear()
+            GRAD_READY(params[4 * l:4 * l + 4])
 
     with torch.autocast("cuda", enabled=False):
         for l in range(L - 1, 0, -1):
@@ -298,7 +302,8 @@ def mfma_trunk_backward(saved, g, db, params, direct):
                     put(0, _weight_grad(gp[None], xc[None])[0][:, :K0], db)
             g = gp
         if direct:
-            N.reduce_into(jobs, accumulate=True)
+            if jobs:
+                N.reduce_into(jobs, accumulate=True)
             return None
     out = []
     for l in range(L):
@@ -433,6 +438,9 @@ DIRECT_GRADS = os.environ.get("PHC_DIRECT_GRADS", "1") == "1"
 # Linear returns f16 / bf16 and SiLU saves that input), not fp32: a third less epilogue traffic
 # (PHC_PRE_HALF=0: fp32)
 PRE_HALF = os.environ.get("PHC_PRE_HALF", "1") == "1"
+# data-parallel hook (distributed.FlatGrads.overlap_begin): called with the parameters whose
+# gradients a direct-mode backward has just finished, so their all-reduce can start early
+GRAD_READY = None
 
 
 def _use_mfma(weights, dtype):

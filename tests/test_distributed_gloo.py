@@ -60,6 +60,22 @@ def _worker(rank, world, port, root):
         ((ref_net(xs) - ys) ** 2).mean().backward()
         for p, q in zip(net.parameters(), ref_net.parameters()):
             torch.testing.assert_close(p.grad, q.grad, atol=1e-6, rtol=1e-5)
+        # (1b) overlapped all-reduce: FlatGrads laid out in a given order, groups reported
+        # ready during the "backward" (twin_mlp.GRAD_READY), the rest at overlap_finish
+        from puffer_phc_amd.policies import twin_mlp
+
+        ps = list(net.parameters())
+        fo = D.FlatGrads(ps, order=[ps[2], ps[3], ps[0]])  # layer 2 (w, b), then layer 1's weight
+        assert fo.params[:3] == [ps[2], ps[3], ps[0]] and fo.params[3] is ps[1]
+        fo.zero()
+        ((net(x) - y) ** 2).mean().backward()
+        fo.overlap_begin()
+        assert twin_mlp.GRAD_READY is not None
+        twin_mlp.GRAD_READY([ps[2], ps[3]])
+        fo.overlap_finish()
+        assert twin_mlp.GRAD_READY is None
+        for p, q in zip(net.parameters(), ref_net.parameters()):
+            torch.testing.assert_close(p.grad, q.grad, atol=1e-6, rtol=1e-5)
         # (2) global advantage statistics
         adv = x[:, 0].contiguous()
         m, s = D.global_mean_std(adv)
