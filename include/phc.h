@@ -268,6 +268,43 @@ typedef struct phc_gemm_desc {
 size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_t n);
 int phc_twin_gemm(const phc_gemm_desc *desc, float *bias_grad, void *workspace, void *stream);
 
+/* R21: the twin trunks' weight gradients (the reference's autograd of nn.Linear,
+ * policies/phc_policy.py:10-38 under clean_pufferl/core.py:354 loss.backward()).  For b < batch
+ * and split s < splits: out[s][b] = G[b][rows_s]^T · Z[b][rows_s] with G[b] [rows, m] (ldg) the
+ * layer's output gradient and Z[b] [rows, n] (ldz) its input, row-major f16 / bf16 (dtype), the
+ * feature dimension contiguous (as phc_twin_gemm writes them), rows_s the s-th of `splits` equal
+ * row chunks; fp32 accumulation, out fp32 [splits, batch, m, n] (summed by the caller, e.g.
+ * phc_reduce_into straight into the gradient buffers).  m, n, ldg, ldz, batch strides % 8 == 0,
+ * rows % (64 * splits) == 0, 16-byte aligned operands; a batch stride of 0 shares the operand. */
+typedef struct phc_wgrad_desc {
+  const void *g;
+  const void *z;
+  int64_t g_batch_stride, z_batch_stride; /* elements */
+  int64_t ldg, ldz;                       /* elements */
+  int64_t rows;
+  int32_t m, n, batch, dtype;
+  int32_t splits, reserved;
+  float *out;
+} phc_wgrad_desc;
+int phc_weight_grad(const phc_wgrad_desc *desc, void *stream);
+
+/* The same weight gradients for up to 8 layers in one launch, without a split: problem i adds
+ * (accumulate) or stores G[b]^T · Z[b] over all `rows` into fp32 destinations — output row r of
+ * batch b goes to dst[b + (r >= split_row)] row r (- split_row when r >= split_row), columns
+ * < n_valid, row stride ldd (the first layer's SPLIT [rows, 2 * out] input gradient against the
+ * shared padded input: batch 1, split_row = out, n_valid = the unpadded width).  Every output
+ * element has one writer: deterministic.  rows % 64 == 0. */
+typedef struct phc_wgrad_problem {
+  const void *g;
+  const void *z;
+  int64_t g_batch_stride, z_batch_stride, ldg, ldz; /* elements */
+  float *dst[2];
+  int64_t ldd;
+  int32_t m, n, batch, split_row, n_valid, reserved;
+} phc_wgrad_problem;
+int phc_weight_grad_group(const phc_wgrad_problem *problems, int32_t count, int64_t rows, int32_t dtype,
+                          int32_t accumulate, void *stream);
+
 /* R17 + R19: RunningNorm forward (policies/running_norm.py:15-20) of float32 observations
  * obs [*, d], rows gathered through `rows` (int64 [m], nullable = identity), rounded into the
  * first trunk GEMM's f16 / bf16 operand out [m, ld_out] (columns d..ld_out-1 zero; ld_out % 8

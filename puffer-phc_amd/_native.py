@@ -98,6 +98,23 @@ class GemmDescC(ctypes.Structure):
 EPI_STORE, EPI_BIAS, EPI_BIAS_SILU, EPI_SILU_GRAD = 0, 1, 2, 3
 
 
+class WgradDescC(ctypes.Structure):
+    _fields_ = [("g", c_vp), ("z", c_vp), ("g_batch_stride", c_i64), ("z_batch_stride", c_i64), ("ldg", c_i64),
+                ("ldz", c_i64), ("rows", c_i64), ("m", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("batch", ctypes.c_int32), ("dtype", ctypes.c_int32), ("splits", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("out", c_vp)]
+
+
+class WgradProblemC(ctypes.Structure):
+    _fields_ = [("g", c_vp), ("z", c_vp), ("g_batch_stride", c_i64), ("z_batch_stride", c_i64), ("ldg", c_i64),
+                ("ldz", c_i64), ("dst", c_vp * 2), ("ldd", c_i64), ("m", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("batch", ctypes.c_int32), ("split_row", ctypes.c_int32), ("n_valid", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+WGRAD_GROUP_MAX = 8
+
+
 class ReduceJobC(ctypes.Structure):
     _fields_ = [("src", c_vp), ("dst", c_vp), ("rows", c_i64), ("cols", c_i64), ("src_ld", c_i64),
                 ("part_stride", c_i64), ("parts", ctypes.c_int32), ("accumulate", ctypes.c_int32)]
@@ -158,6 +175,9 @@ _EXPORTS = {
                                         ctypes.c_int32, ctypes.c_int32, c_vp, c_vp]),
     "phc_twin_gemm_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
     "phc_twin_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDescC), c_vp, c_vp, c_vp]),
+    "phc_weight_grad": (ctypes.c_int, [ctypes.POINTER(WgradDescC), c_vp]),
+    "phc_weight_grad_group": (ctypes.c_int, [ctypes.POINTER(WgradProblemC), ctypes.c_int32, c_i64, ctypes.c_int32,
+                                              ctypes.c_int32, c_vp]),
     "phc_reduce_into": (ctypes.c_int, [ctypes.POINTER(ReduceJobC), ctypes.c_int32, c_vp]),
     "phc_obs_half": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int32, c_vp, c_vp, ctypes.c_float, ctypes.c_float,
                                      c_vp, ctypes.c_int32, ctypes.c_int32, c_vp]),
@@ -519,6 +539,62 @@ def twin_gemm(a, b, epilogue, out, twin, bias=None, aux=None, aux_layout=GROUPED
                                _stream()),
            "phc_twin_gemm")
     return out
+
+
+def weight_grad(g, z, splits, out=None):
+    """Split-K partials of dW[b] = g[b]^T z[b] (phc_weight_grad): g [batch?, rows, m], z
+    [batch?, rows, n] f16 / bf16 with contiguous columns (a 2-D operand is shared by the batch);
+    returns fp32 [splits, batch, m, n] (sum over dim 0 = the gradient)."""
+    pg, gbs, ldg, bg, rows, m = _operand(g, "g")
+    pz, zbs, ldz, bz, rz, n = _operand(z, "z")
+    if rz != rows or (bg != bz and bg != 1 and bz != 1) or g.dtype != z.dtype:
+        raise ValueError(f"weight_grad: operands {tuple(g.shape)} / {tuple(z.shape)} do not match")
+    batch = max(bg, bz)
+    shape = (splits, batch, m, n)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=g.device)
+    elif out.dtype != torch.float32 or not out.is_contiguous() or tuple(out.shape) != shape:
+        raise ValueError(f"weight_grad: out must be a contiguous fp32 {shape} tensor")
+    d = WgradDescC(pg, pz, gbs, zbs, ldg, ldz, rows, m, n, batch, DTYPE_CODE[g.dtype], splits, 0, out.data_ptr())
+    _check(lib().phc_weight_grad(ctypes.byref(d), _stream()), "phc_weight_grad")
+    return out
+
+
+def weight_grad_group(problems, accumulate=True):
+    """Weight gradients of up to 8 layers in one launch (phc_weight_grad_group): each problem is
+    (g [batch?, rows, m], z [batch?, rows, n], dsts, split_row, n_valid) with dsts one or two dense
+    fp32 [*, n_valid] destinations; output row r of batch b goes to dsts[b + (r >= split_row)]
+    (split_row = m: no split).  dst (+)= g[b]^T z[b] over all rows."""
+    if not 1 <= len(problems) <= WGRAD_GROUP_MAX:
+        raise ValueError(f"weight_grad_group: 1..{WGRAD_GROUP_MAX} problems")
+    arr = (WgradProblemC * len(problems))()
+    rows = dtype = None
+    for i, (g, z, dsts, split_row, n_valid) in enumerate(problems):
+        pg, gbs, ldg, bg, r, m = _operand(g, "g")
+        pz, zbs, ldz, bz, rz, n = _operand(z, "z")
+        if rz != r or (bg != bz and bg != 1 and bz != 1) or g.dtype != z.dtype:
+            raise ValueError(f"weight_grad_group: problem {i}: operands {tuple(g.shape)} / {tuple(z.shape)}")
+        if rows is None:
+            rows, dtype = r, g.dtype
+        elif r != rows or g.dtype != dtype:
+            raise ValueError("weight_grad_group: every problem must share rows and dtype")
+        dsts = list(dsts)
+        for d in dsts:
+            if d.dtype != torch.float32 or not d.is_cuda or not d.is_contiguous() or d.shape[-1] != n_valid:
+                raise ValueError(f"weight_grad_group: problem {i}: destinations must be dense fp32 [*, {n_valid}]")
+        batch = max(bg, bz)
+        need = batch + (1 if split_row < m else 0)
+        if len(dsts) != need:
+            raise ValueError(f"weight_grad_group: problem {i}: {need} destinations expected")
+        rows_per = [split_row, m - split_row] if split_row < m else [m] * batch
+        for d, rr in zip(dsts, rows_per):
+            if d.numel() != rr * n_valid:
+                raise ValueError(f"weight_grad_group: problem {i}: destination of {rr} x {n_valid} expected")
+        ptrs = [d.data_ptr() for d in dsts] + [None] * (2 - len(dsts))
+        arr[i] = WgradProblemC(pg, pz, gbs, zbs, ldg, ldz, (c_vp * 2)(*ptrs), n_valid, m, n, batch, split_row,
+                               n_valid, 0)
+    _check(lib().phc_weight_grad_group(arr, len(problems), rows, DTYPE_CODE[dtype], int(accumulate), _stream()),
+           "phc_weight_grad_group")
 
 
 def reduce_into(jobs, accumulate=True):

@@ -452,6 +452,273 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ weight gradients (R21) --
+// dW[b] = G[b]^T · Z[b] summed over the rows of G [rows, m] (the layer's output gradient) and
+// Z [rows, n] (its input), both as the forward / input-gradient GEMMs wrote them: row-major, the
+// feature dimension contiguous, the reduction over rows.  Operand tiles are therefore staged as
+// [64 rows][BM or BN columns] (16-B chunks of the global rows, chunk c of LDS row r holding source
+// chunk c ^ wg_swz(r)), and the MFMA fragments, which want 8 consecutive reduction rows per lane,
+// are gathered column-wise by ds_read_b64_tr_b16: lane 4q + p of a 16-lane group names row q,
+// columns 4p..4p+3 of a 4 x 16 block and lane i receives column i of the 4 rows.  The XOR moves
+// 32-B column pairs, so the 8 rows a 32-lane half touches (k rows 8G + 4h + q of two groups) land
+// on 8 distinct pairs of the 256-B bank window: conflict-free.  Split-K over the rows (S chunks,
+// the split index slowest so every tile of a split streams the same rows at the same time and
+// the XCD's L2 serves the re-reads); the fp32 partials go to out[s][b][m][n].
+struct WgradArgs {
+  const char *g, *z;
+  int64_t g_bs, z_bs, ldg, ldz;  // element strides
+  int64_t rows_per_split;
+  int m, n, batch, splits;
+  int tiles_m, tiles_n;
+  float *out;
+  int discard;
+};
+
+__device__ __forceinline__ int wg_swz(int r) { return ((r & 3) | ((r >> 1) & 4)) << 1; }
+
+// global_load_lds of one 64-row x C-column operand tile (C / 8 wave-instructions over W waves)
+template <int C, int W>
+__device__ __forceinline__ void stage_tile_k(const char *base, int64_t ld, int64_t row0, int col0, int cols,
+                                             char *lds_tile, int wave, int lane) {
+  constexpr int CPR = C / 8;  // 16-B chunks per tile row
+  static_assert(CPR >= 16, "the swizzle moves chunks within aligned groups of 16");
+  static_assert((C / 8) % W == 0, "tile chunks must split evenly over the waves");
+#pragma unroll
+  for (int i = 0; i < C / 8 / W; ++i) {
+    const int q0 = (i * W + wave) * 64;
+    const int q = q0 + lane;
+    const int r = q / CPR, c = q % CPR;
+    int gc = col0 + ((c ^ wg_swz(r)) << 3);
+    gc = gc + 8 <= cols ? gc : cols - 8;  // ragged last tile: in-bounds filler, its outputs are masked
+    const char *src = base + ((row0 + r) * ld + gc) * 2;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (lds_void *)(lds_tile + q0 * 16), 16, 0, 0);
+  }
+}
+
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+
+// the 16x16x32 operand fragment of columns cb..cb+15, reduction rows 32 s..32 s+31 of a tile with
+// `rowbytes`-byte rows: lane l gets column cb + (l & 15), rows 32 s + 8 (l >> 4) + 0..7
+template <typename V8>
+__device__ __forceinline__ void read_frag_tr(const char *lds_tile, int rowbytes, int cb, int s, int lane, V8 &f) {
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ch = (cb >> 3) + (p >> 1);
+  const int r0 = 32 * s + 8 * grp + q, r1 = r0 + 4;
+  const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4v *)(lds_tile + r0 * rowbytes + ((ch ^ wg_swz(r0)) << 4) + 8 * (p & 1)));
+  const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4v *)(lds_tile + r1 * rowbytes + ((ch ^ wg_swz(r1)) << 4) + 8 * (p & 1)));
+  const s8v both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  f = __builtin_bit_cast(V8, both);
+}
+
+// One K-step: issue the DMA of the next operand tile into `wr` (when `issue`) and run the MFMAs
+// of the current one from `rd`.  The two LDS buffers are restrict parameters, so after inlining
+// the fragment reads and the LDS-DMA writes carry disjoint alias scopes and the compiler's wait
+// insertion does not drain the in-flight DMA (vmcnt(0)) before the first fragment read.
+template <typename T, typename TL>
+__device__ __forceinline__ void wgrad_step(const char *__restrict__ rd, char *__restrict__ wr, bool issue,
+                                           const char *A, int64_t lda, int am, const char *B, int64_t ldb, int bn,
+                                           int64_t row0, int m0, int n0, int wave, int lane,
+                                           f4 (&acc)[TL::MI][TL::NI]) {
+  constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
+  using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
+  const int wm = wave / TL::WGN, wn = wave % TL::WGN;
+  if (issue) {
+    stage_tile_k<BM, TL::kWaves>(A, lda, row0, m0, am, wr, wave, lane);
+    stage_tile_k<BN, TL::kWaves>(B, ldb, row0, n0, bn, wr + BM * 128, wave, lane);
+  }
+  const char *ta = rd;
+  const char *tb = rd + BM * 128;
+  constexpr int GP = MI / 2, NG = 2 * GP;
+  static_assert(MI % 2 == 0, "A fragments are walked in pairs");
+  V8 fa[2][2], fb[2][NI];
+  auto load_b = [&](V8 *f, int s) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) read_frag_tr(tb, BN * 2, wn * TL::TN + j * 16, s, lane, f[j]);
+  };
+  auto load_a = [&](V8 *f, int s, int p) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) read_frag_tr(ta, BM * 2, wm * TL::TM + (2 * p + ii) * 16, s, lane, f[ii]);
+  };
+  load_b(fb[0], 0);
+  load_a(fa[0], 0, 0);
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const int s = q / GP, p = q % GP;
+    if (q + 1 < NG) {
+      const int s1 = (q + 1) / GP, p1 = (q + 1) % GP;
+      if (s1 != s) load_b(fb[s1 & 1], s1);
+      load_a(fa[(q + 1) & 1], s1, p1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        f4 &c = acc[2 * p + ii][j];
+        if constexpr (std::is_same<T, _Float16>::value)
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
+        else
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
+      }
+  }
+}
+
+template <typename T, typename TL>
+__global__ __launch_bounds__(TL::kThreads) void k_wgrad(WgradArgs g) {
+  constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][A 64 x BM | B 64 x BN]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / TL::WGN, wn = wave % TL::WGN;
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tn = wg % g.tiles_n;
+  const int tm = (wg / g.tiles_n) % g.tiles_m;
+  const int rest = wg / (g.tiles_n * g.tiles_m);
+  const int bt = rest % g.batch, sp = rest / g.batch;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int64_t r0 = (int64_t)sp * g.rows_per_split;
+  const char *A = g.g + bt * g.g_bs * 2;
+  const char *B = g.z + bt * g.z_bs * 2;
+
+  f4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  const int kt_n = (int)(g.rows_per_split / kGBK);
+  stage_tile_k<BM, TL::kWaves>(A, g.ldg, r0, m0, g.m, smem, wave, lane);
+  stage_tile_k<BN, TL::kWaves>(B, g.ldz, r0, n0, g.n, smem + BM * 128, wave, lane);
+  for (int kt = 0; kt < kt_n; ++kt) {
+    __syncthreads();  // tile kt landed; buffer (kt + 1) & 1 is no longer read
+    char *cur = smem + (kt & 1) * TL::kStageBytes;
+    char *nxt = smem + ((kt + 1) & 1) * TL::kStageBytes;
+    wgrad_step<T, TL>(cur, nxt, kt + 1 < kt_n, A, g.ldg, g.m, B, g.ldz, g.n, r0 + (int64_t)(kt + 1) * kGBK, m0, n0,
+                      wave, lane, acc);
+  }
+  if (g.discard) {
+    float t = 0.0f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1234.5f) g.out[0] = t;
+    return;
+  }
+  // partial tile straight from the accumulators: lane holds column (lane & 15) of rows
+  // 4 (lane >> 4) + e of each 16 x 16 block (64-B row segments per store instruction)
+  float *o = g.out + ((int64_t)sp * g.batch + bt) * g.m * g.n;
+  const int cl = lane & 15, rl = 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int col = n0 + wn * TL::TN + j * 16 + cl;
+    if (col >= g.n) continue;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = m0 + wm * TL::TM + i * 16 + rl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (row + e < g.m) o[(int64_t)(row + e) * g.n + col] = acc[i][j][e];
+    }
+  }
+}
+
+// Grouped form: the weight gradients of several layers in ONE launch, no split: every output tile
+// of every layer reduces over all rows in one workgroup and adds (or stores) its fp32 result
+// straight into the gradient buffers — deterministic, no partials.  With equal rows per tile the
+// workgroups of all layers carry equal work, so the grid quantises over the CUs as a whole
+// (the default trunk: 64 + 96 + 48 + 32 + 16 = 256 tiles of 256 x 256, one per CU).
+constexpr int kWgradGroupMax = 8;
+struct WgradProblem {
+  const char *g, *z;
+  int64_t g_bs, z_bs, ldg, ldz, ldd;
+  float *dst[2];
+  int m, n, batch, split_row, n_valid, tiles_m, tiles_n, block0;
+};
+struct WgradGroupArgs {
+  WgradProblem p[kWgradGroupMax];
+  int count, accumulate, discard;
+  int64_t rows;
+};
+
+template <typename T, typename TL>
+__global__ __launch_bounds__(TL::kThreads) void k_wgrad_group(WgradGroupArgs ga) {
+  constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / TL::WGN, wn = wave % TL::WGN;
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < kWgradGroupMax; ++i)
+    if (i < ga.count && wg >= ga.p[i].block0) pi = i;
+  const WgradProblem &P = ga.p[pi];
+  const int local = wg - P.block0;
+  const int tn = local % P.tiles_n;
+  const int tm = (local / P.tiles_n) % P.tiles_m;
+  const int bt = local / (P.tiles_n * P.tiles_m);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const char *A = P.g + bt * P.g_bs * 2;
+  const char *B = P.z + bt * P.z_bs * 2;
+  const int64_t lda = P.ldg, ldb = P.ldz;
+  const int am = P.m, bn = P.n;
+
+  f4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  const int kt_n = (int)(ga.rows / kGBK);
+  stage_tile_k<BM, TL::kWaves>(A, lda, 0, m0, am, smem, wave, lane);
+  stage_tile_k<BN, TL::kWaves>(B, ldb, 0, n0, bn, smem + BM * 128, wave, lane);
+  for (int kt = 0; kt < kt_n; ++kt) {
+    __syncthreads();
+    char *cur = smem + (kt & 1) * TL::kStageBytes;
+    char *nxt = smem + ((kt + 1) & 1) * TL::kStageBytes;
+    wgrad_step<T, TL>(cur, nxt, kt + 1 < kt_n, A, lda, am, B, ldb, bn, (int64_t)(kt + 1) * kGBK, m0, n0, wave,
+                      lane, acc);
+  }
+  if (ga.discard) {
+    float t = 0.0f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1234.5f) P.dst[0][0] = t;
+    return;
+  }
+  // output row r of batch bt -> dst[bt + (r >= split_row)] row r (- split_row), columns < n_valid
+  const int cl = lane & 15, rl = 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int col = n0 + wn * TL::TN + j * 16 + cl;
+    if (col >= P.n_valid) continue;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = m0 + wm * TL::TM + i * 16 + rl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = row + e;
+        if (r >= P.m) continue;
+        const bool hi = r >= P.split_row;
+        float *d = P.dst[bt + (hi ? 1 : 0)] + (int64_t)(hi ? r - P.split_row : r) * P.ldd + col;
+        *d = ga.accumulate ? *d + acc[i][j][e] : acc[i][j][e];
+      }
+    }
+  }
+}
+
 // tile configurations
 using Tile128x2 = Tile<128, 128, 2, 2, 2>;
 using Tile256sq = Tile<256, 256, 2, 4, 2>;
@@ -517,6 +784,38 @@ static void launch_gemm(int dtype, int out_dtype, int epi, int cfg, const GemmAr
     if (out_dtype == PHC_DT_F32) launch_epi<__bf16, float>(epi, cfg, g, blocks, st);
     else launch_epi<__bf16, __bf16>(epi, cfg, g, blocks, st);
   }
+}
+
+template <typename T>
+static void launch_wgrad(const WgradArgs &g, int64_t blocks, hipStream_t st) {
+  using TL = Tile256sq;
+  auto kernel = k_wgrad<T, TL>;
+  static bool attr = [&] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              TL::kLdsBytes);
+    return true;
+  }();
+  (void)attr;
+  if (g_ev0)
+    hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g_ev0, g_ev1, 0, g);
+  else
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
+}
+
+template <typename T>
+static void launch_wgrad_group(const WgradGroupArgs &g, int64_t blocks, hipStream_t st) {
+  using TL = Tile256sq;
+  auto kernel = k_wgrad_group<T, TL>;
+  static bool attr = [&] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              TL::kLdsBytes);
+    return true;
+  }();
+  (void)attr;
+  if (g_ev0)
+    hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g_ev0, g_ev1, 0, g);
+  else
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
 }
 
 }  // namespace phc
@@ -600,4 +899,121 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
                        static_cast<const float *>(workspace), (int)tiles_m, c, bias_grad);
   }
   return check_launch("twin_gemm");
+}
+
+extern "C" int phc_weight_grad(const phc_wgrad_desc *d, void *stream) {
+  PHC_REQUIRE(d, "weight_grad: null descriptor");
+  PHC_REQUIRE(d->g && d->z && d->out, "weight_grad: null operand");
+  PHC_REQUIRE(d->m >= 8 && d->n >= 8 && d->m % 8 == 0 && d->n % 8 == 0 && d->batch >= 1,
+              "weight_grad: m, n must be multiples of 8 (got %d, %d)", d->m, d->n);
+  PHC_REQUIRE(d->splits >= 1 && d->rows > 0 && d->rows % ((int64_t)d->splits * kGBK) == 0,
+              "weight_grad: rows (%lld) must be a multiple of 64 * splits (%d)", (long long)d->rows, d->splits);
+  PHC_REQUIRE(d->ldg >= d->m && d->ldz >= d->n && d->ldg % 8 == 0 && d->ldz % 8 == 0,
+              "weight_grad: leading dimensions must cover the columns and be multiples of 8");
+  PHC_REQUIRE(d->g_batch_stride % 8 == 0 && d->z_batch_stride % 8 == 0, "weight_grad: batch strides must be % 8");
+  PHC_REQUIRE((reinterpret_cast<uintptr_t>(d->g) & 15) == 0 && (reinterpret_cast<uintptr_t>(d->z) & 15) == 0,
+              "weight_grad: operands must be 16-byte aligned");
+  PHC_REQUIRE(d->dtype == PHC_DT_F16 || d->dtype == PHC_DT_BF16, "weight_grad: operands must be f16 or bf16");
+  const int64_t tiles_m = (d->m + 255) / 256, tiles_n = (d->n + 255) / 256;
+  const int64_t blocks = tiles_m * tiles_n * d->batch * d->splits;
+  PHC_REQUIRE(blocks < (1ll << 31), "weight_grad: grid too large");
+  WgradArgs g{};
+  g.g = static_cast<const char *>(d->g);
+  g.z = static_cast<const char *>(d->z);
+  g.g_bs = d->g_batch_stride;
+  g.z_bs = d->z_batch_stride;
+  g.ldg = d->ldg;
+  g.ldz = d->ldz;
+  g.rows_per_split = d->rows / d->splits;
+  g.m = d->m;
+  g.n = d->n;
+  g.batch = d->batch;
+  g.splits = d->splits;
+  g.tiles_m = (int)tiles_m;
+  g.tiles_n = (int)tiles_n;
+  g.out = d->out;
+  static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
+  g.discard = discard ? 1 : 0;
+  hipStream_t st = as_stream(stream);
+  g_ev0 = g_ev1 = nullptr;
+  if (g_gemm_timer && g_gemm_timer->used < (int32_t)g_gemm_timer->start.size()) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+      g_ev0 = g_gemm_timer->start[g_gemm_timer->used];
+      g_ev1 = g_gemm_timer->stop[g_gemm_timer->used];
+      g_gemm_timer->used += 1;
+      g_gemm_timer->work += 2.0 * (double)d->m * d->n * d->rows * d->batch;
+    }
+  }
+  if (d->dtype == PHC_DT_F16) launch_wgrad<_Float16>(g, blocks, st);
+  else launch_wgrad<__bf16>(g, blocks, st);
+  g_ev0 = g_ev1 = nullptr;
+  return check_launch("weight_grad");
+}
+
+extern "C" int phc_weight_grad_group(const phc_wgrad_problem *probs, int32_t count, int64_t rows, int32_t dtype,
+                                     int32_t accumulate, void *stream) {
+  PHC_REQUIRE(probs && count >= 1 && count <= kWgradGroupMax, "weight_grad_group: 1..%d problems", kWgradGroupMax);
+  PHC_REQUIRE(rows > 0 && rows % kGBK == 0, "weight_grad_group: rows (%lld) must be a multiple of %d",
+              (long long)rows, kGBK);
+  PHC_REQUIRE(dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "weight_grad_group: operands must be f16 or bf16");
+  WgradGroupArgs ga{};
+  int64_t blocks = 0;
+  double flops = 0.0;
+  for (int i = 0; i < count; ++i) {
+    const phc_wgrad_problem &d = probs[i];
+    PHC_REQUIRE(d.g && d.z && d.dst[0], "weight_grad_group: problem %d: null operand", i);
+    PHC_REQUIRE(d.m >= 8 && d.n >= 8 && d.m % 8 == 0 && d.n % 8 == 0 && (d.batch == 1 || d.batch == 2),
+                "weight_grad_group: problem %d: m, n % 8, batch 1 or 2", i);
+    PHC_REQUIRE(d.ldg >= d.m && d.ldz >= d.n && d.ldg % 8 == 0 && d.ldz % 8 == 0 && d.g_batch_stride % 8 == 0 &&
+                    d.z_batch_stride % 8 == 0,
+                "weight_grad_group: problem %d: leading dimensions / batch strides", i);
+    PHC_REQUIRE((reinterpret_cast<uintptr_t>(d.g) & 15) == 0 && (reinterpret_cast<uintptr_t>(d.z) & 15) == 0,
+                "weight_grad_group: problem %d: operands must be 16-byte aligned", i);
+    PHC_REQUIRE(d.n_valid >= 1 && d.n_valid <= d.n && d.ldd >= d.n_valid && d.split_row >= 1,
+                "weight_grad_group: problem %d: destination geometry", i);
+    const int ndst = d.batch + (d.split_row < d.m ? 1 : 0);
+    PHC_REQUIRE(ndst <= 2 && (ndst < 2 || d.dst[1]), "weight_grad_group: problem %d: needs dst[1]", i);
+    WgradProblem &p = ga.p[i];
+    p.g = static_cast<const char *>(d.g);
+    p.z = static_cast<const char *>(d.z);
+    p.g_bs = d.g_batch_stride;
+    p.z_bs = d.z_batch_stride;
+    p.ldg = d.ldg;
+    p.ldz = d.ldz;
+    p.ldd = d.ldd;
+    p.dst[0] = d.dst[0];
+    p.dst[1] = d.dst[1];
+    p.m = d.m;
+    p.n = d.n;
+    p.batch = d.batch;
+    p.split_row = d.split_row;
+    p.n_valid = d.n_valid;
+    p.tiles_m = (d.m + 255) / 256;
+    p.tiles_n = (d.n + 255) / 256;
+    p.block0 = (int)blocks;
+    blocks += (int64_t)p.tiles_m * p.tiles_n * d.batch;
+    flops += 2.0 * (double)d.m * d.n * rows * d.batch;
+  }
+  PHC_REQUIRE(blocks < (1ll << 31), "weight_grad_group: grid too large");
+  ga.count = count;
+  ga.accumulate = accumulate ? 1 : 0;
+  ga.rows = rows;
+  static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
+  ga.discard = discard ? 1 : 0;
+  hipStream_t st = as_stream(stream);
+  g_ev0 = g_ev1 = nullptr;
+  if (g_gemm_timer && g_gemm_timer->used < (int32_t)g_gemm_timer->start.size()) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+      g_ev0 = g_gemm_timer->start[g_gemm_timer->used];
+      g_ev1 = g_gemm_timer->stop[g_gemm_timer->used];
+      g_gemm_timer->used += 1;
+      g_gemm_timer->work += flops;
+    }
+  }
+  if (dtype == PHC_DT_F16) launch_wgrad_group<_Float16>(ga, blocks, st);
+  else launch_wgrad_group<__bf16>(ga, blocks, st);
+  g_ev0 = g_ev1 = nullptr;
+  return check_launch("weight_grad_group");
 }

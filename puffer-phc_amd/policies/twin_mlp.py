@@ -249,20 +249,68 @@ def mfma_trunk_forward(x, weights, need_grad):
     return y, saved
 
 
+_CU_COUNT = {}
+
+
+def _wgrad_tiles(g, z):
+    m, n = g.shape[-1], z.shape[-1]
+    return -(-m // 256) * -(-n // 256) * (g.shape[0] if g.dim() == 3 else 1)
+
+
+def _grouped_subset(problems, device, rest=False):
+    """Layers of the grouped weight-gradient launch: all of them when their 256 x 256 tiles fill
+    whole waves of the CUs (or fit one), else without the smallest layers that would open
+    another wave for a handful of tiles (each tile runs over all rows, so a partial wave costs a
+    whole one).  rest=True: the layers left out."""
+    key = torch.device(device).index or 0
+    cus = _CU_COUNT.get(key)
+    if cus is None:
+        cus = _CU_COUNT[key] = torch.cuda.get_device_properties(device).multi_processor_count
+    order = sorted(problems, key=lambda l: _wgrad_tiles(problems[l][1], problems[l][2]))
+    tiles = {l: _wgrad_tiles(problems[l][1], problems[l][2]) for l in problems}
+    total = sum(tiles.values())
+    keep = set(problems)
+    if total > cus and total % cus:
+        target = (total // cus) * cus
+        for l in order:  # smallest first
+            if total <= target or len(keep) == 1:
+                break
+            keep.discard(l)
+            total -= tiles[l]
+        if total % cus and total > cus:  # could not trim to whole waves: group everything
+            keep = set(problems)
+    sel = sorted(set(problems) - keep) if rest else sorted(keep, reverse=True)
+    return sel
+
+
 def mfma_trunk_backward(saved, g, db, params, direct):
     """Backward of mfma_trunk_forward from g = d loss / d (last layer output) [2, M, n] in the
     operand dtype and db = its fp32 column sums [2n] (the last layer's bias gradient; in direct
     mode also [parts, 2n] partial rows, summed into the bias gradients).  Every
-    input-gradient GEMM carries its SiLU-backward + bias-gradient epilogue; weight gradients are
-    split-K library GEMMs (their reduction runs over the M rows).  direct: the gradients are
-    summed straight into the parameters' bound .grad views (phc_reduce_into) and None is
-    returned; otherwise the per-parameter gradient list (trunk params order)."""
+    input-gradient GEMM carries its SiLU-backward + bias-gradient epilogue.  Weight gradients:
+    all layers in ONE grouped launch after the input-gradient chain (phc_weight_grad_group: one
+    workgroup per output tile over all M rows, no split, no partials), or — when a data-parallel
+    hook is set (GRAD_READY) — per layer as soon as the layer's output gradient exists (split-K
+    library GEMMs summed by phc_reduce_into), so each layer's all-reduce can start while the
+    backward continues.  direct: the gradients are summed straight into the parameters' bound
+    .grad views and None is returned; otherwise the per-parameter gradient list (trunk params
+    order)."""
     L, K0 = saved.L, saved.K0
     xc, WT, pres, zs = saved.xc, saved.wt, saved.pres, saved.zs
     dt = xc.dtype
     M = xc.shape[0]
     grads = [None] * (2 * L)
     jobs = []
+    grouped = GRAD_READY is None and GROUPED_WGRAD and M % 64 == 0 and L <= N.WGRAD_GROUP_MAX
+    problems = {}
+
+    def put_bias(l, db):
+        wa, ba, wc, bc = params[4 * l:4 * l + 4]
+        n = wa.shape[0]
+        if db.dim() == 2:  # [parts, 2n] partial rows (the fused PPO tail)
+            jobs.extend([(db[:, :n].unsqueeze(1), ba.grad), (db[:, n:].unsqueeze(1), bc.grad)])
+        else:
+            jobs.extend([(db[:n].view(1, n), ba.grad), (db[n:].view(1, n), bc.grad)])
 
     def put(l, dW_parts, db):
         """dW_parts: ([parts, 2n, k] or [2, parts, n, k] partials, layer-1 flag), db [2n]."""
@@ -275,18 +323,34 @@ def mfma_trunk_backward(saved, g, db, params, direct):
             jobs.extend([(dW_parts[:, :n, :k], wa.grad), (dW_parts[:, n:, :k], wc.grad)])
         else:
             jobs.extend([(dW_parts[0], wa.grad), (dW_parts[1], wc.grad)])
-        if db.dim() == 2:  # [parts, 2n] partial rows (the fused PPO tail)
-            jobs.extend([(db[:, :n].unsqueeze(1), ba.grad), (db[:, n:].unsqueeze(1), bc.grad)])
-        else:
-            jobs.extend([(db[:n].view(1, n), ba.grad), (db[n:].view(1, n), bc.grad)])
+        put_bias(l, db)
         if GRAD_READY is not None:  # data parallel: this layer's gradients now, then its all-reduce
             N.reduce_into(jobs, accumulate=True)
             jobs.clear()
             GRAD_READY(params[4 * l:4 * l + 4])
 
+    def wdst(l):
+        """Destinations of layer l's weight gradient: the bound .grad views (direct), or views of a
+        new [2, n, k] (layer 0: [2n, k]) tensor, returned as well."""
+        wa, _, wc, _ = params[4 * l:4 * l + 4]
+        if direct:
+            return [wa.grad, wc.grad], None
+        n = wa.shape[0]
+        W = torch.empty((2 * n, wa.shape[1]) if l == 0 else (2,) + tuple(wa.shape), dtype=torch.float32,
+                        device=xc.device)
+        return [W[:n], W[n:]] if l == 0 else [W[0], W[1]], W
+
     with torch.autocast("cuda", enabled=False):
         for l in range(L - 1, 0, -1):
-            put(l, _weight_grad_parts(g, zs[l - 1]) if direct else _weight_grad(g, zs[l - 1]), db)
+            if grouped:
+                d, W = wdst(l)
+                problems[l] = (l, g, zs[l - 1], (g, zs[l - 1], d, g.shape[2], zs[l - 1].shape[2]))
+                if direct:
+                    put_bias(l, db)
+                else:
+                    grads[2 * l], grads[2 * l + 1] = W, db
+            else:
+                put(l, _weight_grad_parts(g, zs[l - 1]) if direct else _weight_grad(g, zs[l - 1]), db)
             k = WT[l - 1].shape[1]
             db = torch.empty(2 * k, dtype=torch.float32, device=g.device)
             if l > 1:
@@ -296,11 +360,31 @@ def mfma_trunk_backward(saved, g, db, params, direct):
                 gp = torch.empty((M, 2 * k), dtype=dt, device=g.device)
                 N.twin_gemm(g, WT[0], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[0], aux_layout=N.SPLIT,
                             out_layout=N.SPLIT, bias_grad=db)
-                if direct:
+                if grouped:
+                    d, W = wdst(0)
+                    problems[0] = (0, gp, xc, (gp, xc, d, k, K0))
+                    if direct:
+                        put_bias(0, db)
+                    else:
+                        grads[0], grads[1] = W, db
+                elif direct:
                     put(0, _weight_grad_parts(gp[None], xc[None])[0], db)
                 else:
                     put(0, _weight_grad(gp[None], xc[None])[0][:, :K0], db)
             g = gp
+        if grouped:
+            for l in _grouped_subset(problems, xc.device, rest=True):
+                # layers left out of the grouped launch (they would start another whole wave)
+                _, gg, zz, (_, _, d, _, _) = problems[l]
+                if l == 0:
+                    part = _weight_grad_parts(gg[None], zz[None])[0]  # [S, 2n, Kp]
+                    n = d[0].shape[0]
+                    pairs = [(part[:, :n, :K0], d[0]), (part[:, n:, :K0], d[1])]
+                else:
+                    part = _weight_grad_parts(gg, zz)  # [2, S, n, k]
+                    pairs = [(part[0], d[0]), (part[1], d[1])]
+                N.reduce_into(pairs, accumulate=direct)
+            N.weight_grad_group([problems[l][3] for l in _grouped_subset(problems, xc.device)], accumulate=direct)
         if direct:
             if jobs:
                 N.reduce_into(jobs, accumulate=True)
@@ -441,6 +525,8 @@ PRE_HALF = os.environ.get("PHC_PRE_HALF", "1") == "1"
 # data-parallel hook (distributed.FlatGrads.overlap_begin): called with the parameters whose
 # gradients a direct-mode backward has just finished, so their all-reduce can start early
 GRAD_READY = None
+# one grouped weight-gradient launch per backward (False: per-layer split-K library GEMMs)
+GROUPED_WGRAD = True
 
 
 def _use_mfma(weights, dtype):

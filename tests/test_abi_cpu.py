@@ -62,7 +62,8 @@ def test_struct_offsets_match_c_compiler(tmp_path):
                "phc_ppo_coefs": _native.PpoCoefsC, "phc_gemm_desc": _native.GemmDescC,
                "phc_adam_params": _native.AdamParamsC, "phc_opt_state": _native.OptStateC,
                "phc_policy_act_args": _native.PolicyActArgsC, "phc_reduce_job": _native.ReduceJobC,
-               "phc_tail_ln_args": _native.TailLnArgsC}
+               "phc_tail_ln_args": _native.TailLnArgsC, "phc_wgrad_desc": _native.WgradDescC,
+               "phc_wgrad_problem": _native.WgradProblemC}
     lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "phc.h"', "int main(void){"]
     for s, cls in structs.items():
         lines.append(f'printf("{s} size %zu\\n", sizeof({s}));')

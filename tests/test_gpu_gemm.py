@@ -151,6 +151,69 @@ def test_large_ragged_256_tiles(epi):
         torch.testing.assert_close(db, p.grad.sum(1).reshape(-1), rtol=1e-4, atol=2e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("m,n,rows,batch,splits,shared_z", [
+    (512, 256, 1024, 2, 4, False),    # whole 256 tiles, split-K
+    (4096, 960, 2048, 1, 2, False),   # layer 1 as the trunk backward runs it: ragged 960 columns
+    (200, 136, 640, 2, 5, True),      # ragged rows and columns of one tile, shared z, odd split
+])
+def test_weight_grad_exact_integer_operands(dtype, m, n, rows, batch, splits, shared_z):
+    """phc_weight_grad: out[s][b] = g[b][rows_s]^T z[b][rows_s] on small-integer operands, bit-exact
+    against fp32 torch (every partial sum is an integer below 2^24); asymmetric ranges catch a
+    transposed fragment, the shared / ragged cases the column clamp of the transposed staging."""
+    from puffer_phc_amd import _native as N
+
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    g = _ints((batch, rows, m), gen, dtype)
+    z = _ints((rows, n) if shared_z else (batch, rows, n), gen, dtype, lo=-3, hi=7)
+    part = N.weight_grad(g, z, splits)
+    zz = z.expand(batch, rows, n) if shared_z else z
+    gs = g.float().view(batch, splits, rows // splits, m)
+    zs = zz.float().reshape(batch, splits, rows // splits, n)
+    ref = torch.einsum("bsrm,bsrn->sbmn", gs, zs)
+    assert torch.equal(part, ref)
+
+
+def test_weight_grad_random_strided():
+    """A row-strided g (the SPLIT [rows, 2k] first-layer input gradient viewed per trunk) on
+    random data: rel. 1e-5 of the fp32 product (summation order only)."""
+    from puffer_phc_amd import _native as N
+
+    gen = torch.Generator(device=DEV).manual_seed(12)
+    rows = 4096
+    gp = torch.randn((rows, 1024), device=DEV, generator=gen).half()
+    x = torch.randn((rows, 320), device=DEV, generator=gen).half()
+    part = N.weight_grad(gp[:, 512:], x, 4)
+    ref = gp[:, 512:].float().t() @ x.float()
+    torch.testing.assert_close(part.sum(0)[0], ref, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_weight_grad_group_exact_integer_operands(dtype):
+    """phc_weight_grad_group: three problems in one launch — a twin layer (batch 2), the first
+    layer's SPLIT input gradient against a shared padded input (batch 1, rows split over two
+    destinations, padded columns dropped) and a ragged single one — accumulated into existing
+    destinations; bit-exact on small integers."""
+    from puffer_phc_amd import _native as N
+
+    gen = torch.Generator(device=DEV).manual_seed(13)
+    rows = 1024
+    g1, z1 = _ints((2, rows, 256), gen, dtype), _ints((2, rows, 512), gen, dtype, lo=-3, hi=7)
+    gp, xc = _ints((rows, 2 * 128), gen, dtype), _ints((rows, 192), gen, dtype, lo=-3, hi=7)
+    xc[:, 180:] = 0  # padding columns
+    g3, z3 = _ints((1, rows, 72), gen, dtype), _ints((1, rows, 40), gen, dtype, lo=-3, hi=7)
+    d1 = [torch.randint(-50, 50, (256, 512), device=DEV, generator=gen).float() for _ in range(2)]
+    d2 = [torch.randint(-50, 50, (128, 180), device=DEV, generator=gen).float() for _ in range(2)]
+    d3 = [torch.zeros((72, 40), device=DEV)]
+    e1 = [d + (g1[b].float().t() @ z1[b].float()) for b, d in enumerate(d1)]
+    full2 = gp.float().t() @ xc.float()[:, :180]
+    e2 = [d2[0] + full2[:128], d2[1] + full2[128:]]
+    e3 = [g3[0].float().t() @ z3[0].float()]
+    N.weight_grad_group([(g1, z1, d1, 256, 512), (gp, xc, d2, 128, 180), (g3, z3, d3, 72, 40)], accumulate=True)
+    for got, exp in zip(d1 + d2 + d3, e1 + e2 + e3):
+        assert torch.equal(got, exp)
+
+
 def test_rejects_unpadded_k():
     from puffer_phc_amd import _native as N
 
