@@ -257,15 +257,30 @@ def _wgrad_tiles(g, z):
     return -(-m // 256) * -(-n // 256) * (g.shape[0] if g.dim() == 3 else 1)
 
 
+def _wgrad_splits(tiles, rows, device):
+    """Row chunks for a split-K phc_weight_grad launch: the largest power of two <= 32 that keeps
+    tiles * S within one wave of the CUs and >= 1024 rows (a multiple of 64) per chunk."""
+    cus = _cu_count(device)
+    S = 1
+    while S < 32 and tiles * S * 2 <= cus and rows % (S * 2 * 64) == 0 and rows // (S * 2) >= 1024:
+        S *= 2
+    return S
+
+
+def _cu_count(device):
+    key = torch.device(device).index or 0
+    cus = _CU_COUNT.get(key)
+    if cus is None:
+        cus = _CU_COUNT[key] = torch.cuda.get_device_properties(device).multi_processor_count
+    return cus
+
+
 def _grouped_subset(problems, device, rest=False):
     """Layers of the grouped weight-gradient launch: all of them when their 256 x 256 tiles fill
     whole waves of the CUs (or fit one), else without the smallest layers that would open
     another wave for a handful of tiles (each tile runs over all rows, so a partial wave costs a
     whole one).  rest=True: the layers left out."""
-    key = torch.device(device).index or 0
-    cus = _CU_COUNT.get(key)
-    if cus is None:
-        cus = _CU_COUNT[key] = torch.cuda.get_device_properties(device).multi_processor_count
+    cus = _cu_count(device)
     order = sorted(problems, key=lambda l: _wgrad_tiles(problems[l][1], problems[l][2]))
     tiles = {l: _wgrad_tiles(problems[l][1], problems[l][2]) for l in problems}
     total = sum(tiles.values())
@@ -374,15 +389,16 @@ def mfma_trunk_backward(saved, g, db, params, direct):
             g = gp
         if grouped:
             for l in _grouped_subset(problems, xc.device, rest=True):
-                # layers left out of the grouped launch (they would start another whole wave)
+                # layers left out of the grouped launch (they would start another whole wave): the
+                # split-K form of the same kernel, enough row chunks to give every CU a workgroup
                 _, gg, zz, (_, _, d, _, _) = problems[l]
+                S = _wgrad_splits(_wgrad_tiles(gg, zz), M, xc.device)
+                part = N.weight_grad(gg, zz, S)  # [S, B, m, n]
                 if l == 0:
-                    part = _weight_grad_parts(gg[None], zz[None])[0]  # [S, 2n, Kp]
                     n = d[0].shape[0]
-                    pairs = [(part[:, :n, :K0], d[0]), (part[:, n:, :K0], d[1])]
+                    pairs = [(part[:, 0, :n, :K0], d[0]), (part[:, 0, n:, :K0], d[1])]
                 else:
-                    part = _weight_grad_parts(gg, zz)  # [2, S, n, k]
-                    pairs = [(part[0], d[0]), (part[1], d[1])]
+                    pairs = [(part[:, 0], d[0]), (part[:, 1], d[1])]
                 N.reduce_into(pairs, accumulate=direct)
             N.weight_grad_group([problems[l][3] for l in _grouped_subset(problems, xc.device)], accumulate=direct)
         if direct:
