@@ -307,7 +307,9 @@ def main():
             if os.path.exists(gf):
                 with open(gf) as f:
                     gtraffic = json.load(f).get("bytes_per_launch")
-            out["roofline"] = {"bound": "mfma", "kernel": "phc_twin_gemm (fused-epilogue trunk GEMMs, training)",
+            out["roofline"] = {"bound": "mfma",
+                               "kernel": "PPO-update trunk GEMMs: phc_twin_gemm (forward / input-gradient, fused "
+                                         "epilogues) + phc_weight_grad_group / phc_weight_grad (weight gradients)",
                                "achieved": tfs, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
                                "frac": tfs / MFMA_F16_PEAK_TFS, "traffic": gtraffic, "traffic_unit": "bytes",
                                "kernel_us": gemm_s / gemm_launches * 1e6, "launches_timed": gemm_launches,

@@ -4,6 +4,11 @@ FETCH_SIZE KiB x 1024; WRITE_SIZE exact for wide stores), plus the same launches
 from a --kernel-trace pass when given.
 
 usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <kernel_regex> <out.json> [trace_dir] [alg_per_launch]
+
+kernel_regex "train_gemm" selects the launches bench.py's GEMM timer records (the PPO update's
+trunk GEMMs, launched outside the rollout graph): every k_wgrad* dispatch, and k_twin_gemm
+dispatches of the 256 x 256 configuration (512-thread workgroups) with more than 256 workgroups
+(the minibatch's 32768-row GEMMs; the rollout's 4096-row GEMMs have at most 256).
 """
 import csv
 import json
@@ -11,9 +16,18 @@ import re
 import sys
 
 
+def selected(r, kernel, grid="Grid_Size", wg="Workgroup_Size"):
+    name = r["Kernel_Name"]
+    if kernel != "train_gemm":
+        return re.search(kernel, name) is not None
+    if "k_wgrad" in name:
+        return True
+    return "k_twin_gemm" in name and int(r[wg]) == 512 and int(r[grid]) // 512 > 256
+
+
 def counter(d, kernel):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f"{d}/run_counter_collection.csv"))
-            if re.search(kernel, r["Kernel_Name"])]
+            if selected(r, kernel)]
     return sum(vals) / len(vals), len(vals)
 
 
@@ -26,7 +40,8 @@ def main():
            "note": "fetch = 2 x FETCH_SIZE (gfx950 half-count correction); includes Infinity-Cache hits"}
     if len(sys.argv) > 5:
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                for r in csv.DictReader(open(f"{sys.argv[5]}/run_kernel_trace.csv")) if re.search(kernel, r["Kernel_Name"])]
+                for r in csv.DictReader(open(f"{sys.argv[5]}/run_kernel_trace.csv"))
+                if selected(r, kernel, "Grid_Size_X", "Workgroup_Size_X")]
         res["trace_launches"] = len(durs)
         res["trace_mean_us"] = sum(durs) / len(durs) / 1e3
     if len(sys.argv) > 6:

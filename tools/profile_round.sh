@@ -14,7 +14,7 @@ tail -1 "$O/bench_ppo_4096.log" | cut -c1-200
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/trace_ppo" -o run --output-format csv -- \
   python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/trace_ppo.log" 2>&1
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "k_twin_gemm" -d "$O/pmc_gemm_$C" -o run \
+  timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "k_twin_gemm|k_wgrad" -d "$O/pmc_gemm_$C" -o run \
     --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > "$O/pmc_gemm_$C.log" 2>&1
 done
 for E in 4096 32768; do
@@ -27,5 +27,12 @@ for E in 4096 32768; do
       --output-format csv -- python3 "$ROOT/bench.py" --mode env --steps 20 --warmup 5 --envs $E --no-cpu-baseline \
       > "$O/pmc_env_${E}_$C.log" 2>&1
   done
+done
+
+# HBM bytes per launch (+ the trace's mean duration) of the same launches bench.py times
+python tools/pmc_summary.py "$O/pmc_gemm_FETCH_SIZE" "$O/pmc_gemm_WRITE_SIZE" train_gemm "$O/traffic_gemm_4096.json" "$O/trace_ppo"
+for E in 4096 32768; do
+  python tools/pmc_summary.py "$O/pmc_env_${E}_FETCH_SIZE" "$O/pmc_env_${E}_WRITE_SIZE" k_env_step "$O/traffic_$E.json" \
+    "$O/trace_env_$E" $((10886 * E))
 done
 echo "profile_round done"
