@@ -65,6 +65,67 @@ __global__ __launch_bounds__(256) void k_obs_half(const float *__restrict__ obs,
   *reinterpret_cast<uint4 *>(out + (int64_t)r * ldo + c0) = raw;
 }
 
+// Row-per-wave form (ld_out <= 1024): lane l owns output chunks l and l + 64 (8 columns each) of
+// every row its wave visits, so the per-column mean and sqrt(var + eps) are loaded and computed
+// once per lane instead of once per element; rows_per_wave rows per wave, loads of two rows in
+// flight.  Same expression as k_rms_normalize / the generic form: bit-identical outputs.
+template <typename T>
+__global__ __launch_bounds__(256) void k_obs_half_rows(const float *__restrict__ obs, const int64_t *__restrict__ rows,
+                                                       int64_t m, int d, int ldo, const float *__restrict__ mean,
+                                                       const float *__restrict__ var, float eps, float clip,
+                                                       int rows_per_wave, T *__restrict__ out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int chunks = ldo / 8;
+  float mv[2][8], dv[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int col = (lane + 64 * c) * 8 + e;
+      const bool in = col < d;
+      mv[c][e] = in ? mean[col] : 0.0f;
+      dv[c][e] = in ? sqrtf(var[col] + eps) : 1.0f;
+    }
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * rows_per_wave;
+#pragma unroll 2
+  for (int rr = 0; rr < rows_per_wave; ++rr) {
+    const int64_t r = row0 + rr;
+    if (r >= m) break;
+    const int64_t src = rows ? rows[r] : r;
+    const float *x = obs + src * d;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch >= chunks) continue;
+      const int c0 = ch * 8;
+      float xv[8];
+      if (c0 + 8 <= d && (((uintptr_t)(x + c0)) & 7) == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const float2 t = *reinterpret_cast<const float2 *>(x + c0 + e);
+          xv[e] = t.x; xv[e + 1] = t.y;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = c0 + e < d ? x[c0 + e] : 0.0f;
+      }
+      T o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = 0.0f;
+        if (c0 + e < d) {
+          v = (xv[e] - mv[c][e]) / dv[c][e];  // same expression as k_rms_normalize
+          v = v < -clip ? -clip : (v > clip ? clip : v);
+        }
+        o[e] = (T)v;
+      }
+      uint4 raw;
+      __builtin_memcpy(&raw, o, sizeof(raw));
+      *reinterpret_cast<uint4 *>(out + r * ldo + c0) = raw;
+    }
+  }
+}
+
 // --------------------------------------------------------------- policy_act --
 constexpr int kActRows = 8;      // rows per block
 constexpr int kActMaxA = 72;     // actions supported (PHC_NUM_DOF + 3)
@@ -239,10 +300,22 @@ extern "C" int phc_obs_half(const float *obs, const int64_t *rows, int64_t m, in
   PHC_REQUIRE(obs && mean && var && out, "obs_half: null argument");
   PHC_REQUIRE((reinterpret_cast<uintptr_t>(out) & 15) == 0, "obs_half: out must be 16-byte aligned");
   PHC_REQUIRE(dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "obs_half: dtype must be f16 or bf16");
+  hipStream_t st = as_stream(stream);
+  if (ld_out <= 1024) {  // row-per-wave form
+    const int rpw = m >= 65536 ? 8 : (m >= 16384 ? 4 : 1);
+    const int64_t blocks = (m + 4 * rpw - 1) / (4 * rpw);
+    PHC_REQUIRE(blocks < (1ll << 31), "obs_half: too many rows");
+    if (dtype == PHC_DT_F16)
+      hipLaunchKernelGGL(k_obs_half_rows<_Float16>, dim3((unsigned)blocks), dim3(256), 0, st, obs, rows, m, (int)d,
+                         (int)ld_out, mean, var, eps, clip, rpw, static_cast<_Float16 *>(out));
+    else
+      hipLaunchKernelGGL(k_obs_half_rows<__bf16>, dim3((unsigned)blocks), dim3(256), 0, st, obs, rows, m, (int)d,
+                         (int)ld_out, mean, var, eps, clip, rpw, static_cast<__bf16 *>(out));
+    return check_launch("obs_half");
+  }
   const int64_t threads = m * (ld_out / 8);
   PHC_REQUIRE(threads < (1ll << 31) - 256, "obs_half: too many rows");
   const dim3 grid((unsigned)((threads + 255) / 256));
-  hipStream_t st = as_stream(stream);
   if (dtype == PHC_DT_F16)
     hipLaunchKernelGGL(k_obs_half<_Float16>, grid, dim3(256), 0, st, obs, rows, m, (int)d, (int)ld_out, mean, var,
                        eps, clip, static_cast<_Float16 *>(out));

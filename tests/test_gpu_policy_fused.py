@@ -21,16 +21,17 @@ DEV = "cuda:0"
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("gather", [False, True])
-def test_obs_half_matches_rms_normalize(dtype, gather):
+@pytest.mark.parametrize("n", [1000, 20001, 70001])  # 1, 4 and 8 rows per wave, ragged last block
+def test_obs_half_matches_rms_normalize(dtype, gather, n):
     from puffer_phc_amd import _native as N
 
     g = torch.Generator(device=DEV).manual_seed(0)
-    n, d, ld = 1000, 934, 960
+    d, ld = 934, 960
     obs = torch.randn((n, d), device=DEV, generator=g) * 4 + 1
     mean = torch.rand((1, d), device=DEV, generator=g) - 0.5
     var = torch.rand((1, d), device=DEV, generator=g) * 2 + 0.01
-    rows = torch.randperm(n, device=DEV, generator=g)[:777] if gather else None
-    m = 777 if gather else n
+    m = n * 7 // 9 if gather else n
+    rows = torch.randperm(n, device=DEV, generator=g)[:m] if gather else None
     out = torch.full((m, ld), 7.0, dtype=dtype, device=DEV)
     N.obs_half(obs, mean, var, 1e-5, 10.0, out, rows)
     ref = N.rms_normalize((obs[rows] if gather else obs).contiguous(), mean, var, 1e-5, 10.0)
