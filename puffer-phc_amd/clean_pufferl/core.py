@@ -129,7 +129,15 @@ class RolloutStep:
         n = env.num_agents
         dev = env.observations.device
         self.value = torch.zeros(n, device=dev)
-        self.actions = torch.zeros((n, *env.single_action_space.shape), device=dev)
+        # the sampled actions go straight into the env's own action buffer, so PHCPufferEnv.step
+        # finds them in place (no per-step device copy)
+        act = getattr(env, "actions", None)
+        shape = (n, *env.single_action_space.shape)
+        if (isinstance(act, torch.Tensor) and tuple(act.shape) == shape and act.dtype == torch.float32
+                and act.device == torch.device(dev) and act.is_contiguous()):
+            self.actions = act
+        else:
+            self.actions = torch.zeros(shape, device=dev)
         self.logprob = torch.zeros(n, device=dev)
         self.noise = torch.zeros((n, *env.single_action_space.shape), device=dev)
         self.fused_act = getattr(info.config, "fused_act", True)
