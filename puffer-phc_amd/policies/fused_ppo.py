@@ -64,10 +64,12 @@ class FusedPPOLossFn(torch.autograd.Function):
             if direct:
                 jobs = [(_weight_grad_parts(gmu[None], tail.h_actor[None])[0], mu_w.grad)]
                 jobs += [(s.view(1, -1), p.grad) for s, p in tail_srcs]
-                N.reduce_into(jobs, accumulate=True)
                 if twin_mlp.GRAD_READY is not None:  # data parallel: the tail's all-reduce starts now
+                    N.reduce_into(jobs, accumulate=True)
                     twin_mlp.GRAD_READY(params[n:])
-                mfma_trunk_backward(saved, dy, db6, params[:n], True)
+                    jobs = None
+                # single-GPU: the tail's sums ride along with the trunk's final reduce launch
+                mfma_trunk_backward(saved, dy, db6, params[:n], True, extra_jobs=jobs)
                 grads = [None] * len(params)
             else:
                 g_mu_w = _weight_grad(gmu[None], tail.h_actor[None])[0]

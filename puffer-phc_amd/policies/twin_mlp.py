@@ -298,7 +298,7 @@ def _grouped_subset(problems, device, rest=False):
     return sel
 
 
-def mfma_trunk_backward(saved, g, db, params, direct):
+def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None):
     """Backward of mfma_trunk_forward from g = d loss / d (last layer output) [2, M, n] in the
     operand dtype and db = its fp32 column sums [2n] (the last layer's bias gradient; in direct
     mode also [parts, 2n] partial rows, summed into the bias gradients).  Every
@@ -309,13 +309,14 @@ def mfma_trunk_backward(saved, g, db, params, direct):
     library GEMMs summed by phc_reduce_into), so each layer's all-reduce can start while the
     backward continues.  direct: the gradients are summed straight into the parameters' bound
     .grad views and None is returned; otherwise the per-parameter gradient list (trunk params
-    order)."""
+    order).  extra_jobs: (src, dst) accumulate jobs of the caller, flushed with the trunk's own
+    bias-gradient sums in one phc_reduce_into launch (direct mode)."""
     L, K0 = saved.L, saved.K0
     xc, WT, pres, zs = saved.xc, saved.wt, saved.pres, saved.zs
     dt = xc.dtype
     M = xc.shape[0]
     grads = [None] * (2 * L)
-    jobs = []
+    jobs = list(extra_jobs) if (direct and extra_jobs) else []
     grouped = GRAD_READY is None and GROUPED_WGRAD and M % 64 == 0 and L <= N.WGRAD_GROUP_MAX
     problems = {}
 
@@ -399,7 +400,10 @@ def mfma_trunk_backward(saved, g, db, params, direct):
                     pairs = [(part[:, 0, :n, :K0], d[0]), (part[:, 0, n:, :K0], d[1])]
                 else:
                     pairs = [(part[:, 0], d[0]), (part[:, 1], d[1])]
-                N.reduce_into(pairs, accumulate=direct)
+                if direct:
+                    jobs.extend(pairs)  # summed with the bias jobs below
+                else:
+                    N.reduce_into(pairs, accumulate=False)
             N.weight_grad_group([problems[l][3] for l in _grouped_subset(problems, xc.device)], accumulate=direct)
         if direct:
             if jobs:
