@@ -724,8 +724,8 @@ using Tile128x2 = Tile<128, 128, 2, 2, 2>;
 using Tile256sq = Tile<256, 256, 2, 4, 2>;
 enum { kCfg128 = 0, kCfg256sq = 2 };
 
-// 256 x 256 tiles when they still give every CU a tile (measured: the rollout's 4096-row first
-// layer, 256 tiles, 43 vs 48 us), else 128 x 128 (the other 4096-row rollout GEMMs)
+// 256 x 256 tiles from 64 tiles up — even a quarter-filled grid of them beats 128 x 128 tiles on
+// the rollout's 4096-row GEMMs (measured: rollout mode 4.67-4.99 M -> 5.13-5.15 M env-steps/s)
 static int gemm_config(int64_t m, int n, int batch) {
   static const int forced = [] {
     const char *e = getenv("PHC_GEMM_CFG");  // tuning aid (tools/twin_gemm_probe.py)
@@ -733,7 +733,7 @@ static int gemm_config(int64_t m, int n, int batch) {
   }();
   if (forced >= 0) return forced;
   const int64_t big = ((m + 255) / 256) * ((n + 255) / 256) * batch;
-  return big >= 256 ? kCfg256sq : kCfg128;
+  return big >= 64 ? kCfg256sq : kCfg128;
 }
 
 static void gemm_tile_dims(int cfg, int *bm, int *bn) {
