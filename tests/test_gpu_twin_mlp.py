@@ -133,12 +133,17 @@ def _run(pol, obs, act, fused, precision, loss_scale=1.0):
     return logp.detach(), value.detach().float(), grads
 
 
-@pytest.mark.parametrize("precision,tol", [(None, 1e-4), (torch.float16, 3e-3), (torch.bfloat16, 3e-2)])
-def test_twin_policy_matches_unfused_fp32(precision, tol):
+@pytest.mark.parametrize("precision,tol,rows", [(None, 1e-4, 1000), (torch.float16, 3e-3, 1000),
+                                                (torch.bfloat16, 3e-2, 1000), (torch.float16, 3e-3, 2048),
+                                                (torch.bfloat16, 3e-2, 2048)])
+def test_twin_policy_matches_unfused_fp32(precision, tol, rows):
+    """rows = 1000: per-layer split-K weight gradients; rows = 2048 (a multiple of 64): the grouped
+    weight-gradient launch (phc_weight_grad_group) plus the split-K form for the layer it leaves out,
+    all against exact fp32 torch autograd."""
     pol = _policy()
     g = torch.Generator(device=DEV).manual_seed(1)
-    obs = torch.randn((1000, 934), device=DEV, generator=g) * 2
-    act = torch.randn((1000, 69), device=DEV, generator=g) * 0.3
+    obs = torch.randn((rows, 934), device=DEV, generator=g) * 2
+    act = torch.randn((rows, 69), device=DEV, generator=g) * 0.3
     prev = torch.get_float32_matmul_precision()
     try:
         torch.set_float32_matmul_precision("highest")
