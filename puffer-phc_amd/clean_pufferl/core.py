@@ -157,8 +157,9 @@ class RolloutStep:
         with torch.no_grad(), autocast(self.cfg):
             fused = False
             if self.fused_act and hasattr(pol, "act_rollout"):
-                # sample_logits' Normal draw, then the fused policy tail writes the staging buffers
-                self.noise.normal_()
+                # sample_logits' Normal draw (self.noise, drawn eagerly by run() before every step:
+                # an RNG op inside the captured graph would add the generator's seed / offset
+                # updates to every replay), then the fused policy tail writes the staging buffers
                 fused = pol.act_rollout(self.env.observations, self.noise, self.actions, self.logprob, self.value)
             if not fused:
                 actions, logprob, _, value = self.policy(self.env.observations)
@@ -170,6 +171,8 @@ class RolloutStep:
     def run(self, use_graph=True):
         if self.twin is not None:
             refresh_twin(self.twin, _compute_dtype(self.cfg))  # in-place refresh after optimizer steps
+        if self.fused_act:
+            self.noise.normal_()
         if self.graph is not None:
             self.graph.replay()
         elif not use_graph or self.eager_steps == 0:

@@ -724,16 +724,21 @@ using Tile128x2 = Tile<128, 128, 2, 2, 2>;
 using Tile256sq = Tile<256, 256, 2, 4, 2>;
 enum { kCfg128 = 0, kCfg256sq = 2 };
 
-// 256 x 256 tiles from 64 tiles up — even a quarter-filled grid of them beats 128 x 128 tiles on
-// the rollout's 4096-row GEMMs (measured: rollout mode 4.67-4.99 M -> 5.13-5.15 M env-steps/s)
+// 256 x 256 tiles when they still give every CU a tile (the rollout's 4096-row first layer), else
+// 128 x 128 (the other 4096-row rollout GEMMs: a half- or quarter-filled grid of 256 x 256 tiles is
+// slower there; PPO iteration 1.71 vs 1.68 M env-steps/s with the threshold at 64 tiles)
 static int gemm_config(int64_t m, int n, int batch) {
   static const int forced = [] {
     const char *e = getenv("PHC_GEMM_CFG");  // tuning aid (tools/twin_gemm_probe.py)
     return e ? atoi(e) : -1;
   }();
   if (forced >= 0) return forced;
+  static const int big_min = [] {
+    const char *e = getenv("PHC_GEMM_BIG_MIN");  // tuning aid: fewest 256 x 256 tiles that select them
+    return e ? atoi(e) : 256;
+  }();
   const int64_t big = ((m + 255) / 256) * ((n + 255) / 256) * batch;
-  return big >= 64 ? kCfg256sq : kCfg128;
+  return big >= big_min ? kCfg256sq : kCfg128;
 }
 
 static void gemm_tile_dims(int cfg, int *bm, int *bn) {
