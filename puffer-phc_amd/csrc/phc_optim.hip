@@ -209,8 +209,24 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_into(ReduceJobs js) {
     if (i >= total) break;
     const int64_t r = i / job.cols, c = i - r * job.cols;
     const float *src = job.src + r * job.src_ld + c;
-    float acc = src[0];
-    for (int s = 1; s < job.parts; ++s) acc += src[s * job.part_stride];
+    float acc;
+    if (job.parts <= 8) {
+      acc = src[0];
+      for (int s = 1; s < job.parts; ++s) acc += src[s * job.part_stride];
+    } else {
+      // many parts (a persistent kernel's per-block rows, fine split-K): 8 independent running
+      // sums (parts s = 8q + l) keep 8 loads in flight, combined in a fixed order: deterministic
+      float a8[8];
+#pragma unroll
+      for (int l = 0; l < 8; ++l) a8[l] = src[l * job.part_stride];
+      int s = 8;
+      for (; s + 8 <= job.parts; s += 8) {
+#pragma unroll
+        for (int l = 0; l < 8; ++l) a8[l] += src[(int64_t)(s + l) * job.part_stride];
+      }
+      for (int l = 0; s + l < job.parts; ++l) a8[l] += src[(int64_t)(s + l) * job.part_stride];
+      acc = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
+    }
     if (job.accumulate) job.dst[i] += acc;
     else job.dst[i] = acc;
   }
