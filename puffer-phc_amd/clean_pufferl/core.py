@@ -140,6 +140,9 @@ class RolloutStep:
             self.actions = torch.zeros(shape, device=dev)
         self.logprob = torch.zeros(n, device=dev)
         self.noise = torch.zeros((n, *env.single_action_space.shape), device=dev)
+        # mu of the latest step: train() reads the reference's mean_bound_loss from it (the value
+        # of the last rollout forward, core.py:225)
+        self.mu = torch.zeros((n, *env.single_action_space.shape), device=dev)
         self.fused_act = getattr(info.config, "fused_act", True)
         pairs = [(env.observations, exp.obs), (self.value, exp.values), (self.actions, exp.actions),
                  (self.logprob, exp.logprobs), (env.rewards, exp.rewards), (env.terminals, exp.dones),
@@ -160,12 +163,14 @@ class RolloutStep:
                 # sample_logits' Normal draw (self.noise, drawn eagerly by run() before every step:
                 # an RNG op inside the captured graph would add the generator's seed / offset
                 # updates to every replay), then the fused policy tail writes the staging buffers
-                fused = pol.act_rollout(self.env.observations, self.noise, self.actions, self.logprob, self.value)
+                fused = pol.act_rollout(self.env.observations, self.noise, self.actions, self.logprob, self.value,
+                                        mu=self.mu)
             if not fused:
                 actions, logprob, _, value = self.policy(self.env.observations)
                 self.value.copy_(value.flatten())
                 self.actions.copy_(actions)
                 self.logprob.copy_(logprob)
+            self.fused = fused
         self.store(self.env.masks)
 
     def run(self, use_graph=True):
@@ -185,6 +190,35 @@ class RolloutStep:
                 self._body()
             self.graph = g
             g.replay()
+
+
+def _global_count(n, device):
+    """n summed over ranks (the identity without data parallelism)."""
+    if not D.is_dist():
+        return int(n)
+    t = torch.tensor([int(n)], dtype=torch.int64, device=device)
+    return int(D.allreduce_sum_(t).item())
+
+
+def _global_mean(x):
+    """Mean of a device scalar over ranks, as a Python float (the identity on one rank)."""
+    t = torch.as_tensor(x, dtype=torch.float64).reshape(1).clone()
+    if D.is_dist():
+        D.allreduce_sum_(t)
+        t /= D.world_size()
+    return float(t.item())
+
+
+def _rollout_bound_loss(components, pol):
+    """The reference's mean_bound_loss as train() sees it: `getattr(policy, "mean_bound_loss")`
+    read once at the start of train() (core.py:225), i.e. bound_loss(mu) of the LAST rollout
+    forward (no_grad).  From the fused rollout's mu buffer, else the module's attribute."""
+    rs = getattr(components, "rollout", None)
+    if rs is not None and getattr(rs, "fused", False) and pol.training and hasattr(pol, "bound_loss"):
+        with torch.no_grad():
+            return pol.bound_loss(rs.mu)
+    mbl = getattr(pol, "mean_bound_loss", None)
+    return None if mbl is None else mbl.detach()
 
 
 def _compute_dtype(cfg):
@@ -225,7 +259,9 @@ def _evaluate_graph(components, info):
                         break
         with profile.eval_misc:
             n_valid, taken = rs.store.counts[2:4].tolist()
-            info.global_step += n_valid
+            # data parallel: every rank advances the same whole-job step count (its own mask-true
+            # rows differ with the envs' truncation patterns), so loop exits agree across ranks
+            info.global_step += _global_count(n_valid, rs.store.counts.device)
             experience.ptr = start + taken
             experience.step += steps
         for k, v in env_infos.items():
@@ -243,13 +279,14 @@ def evaluate(components, info):
         return _evaluate_graph(components, info)
     policy = components.policy
     env_infos = defaultdict(list)
+    local_steps = 0
     with profile.evaluate:
         while not experience.full:
             with profile.env:
                 o, r, d, t, env_info, env_id, mask = components.vecenv.recv()
             with profile.eval_misc:
                 n_valid = int(mask.sum().item())
-                info.global_step += n_valid
+                local_steps += n_valid
             with profile.eval_forward, torch.no_grad(), autocast(train_cfg):
                 actions, logprob, _, value = policy(o)
             with profile.eval_misc:
@@ -260,6 +297,7 @@ def evaluate(components, info):
                         env_infos[k].append(v)
             with profile.env:
                 components.vecenv.send(actions)
+        info.global_step += _global_count(local_steps, experience.obs.device)
         for k, v in env_infos.items():
             info.stats.extend(k, list(np.atleast_1d(v)))
     experience.ptr = 0
@@ -321,6 +359,8 @@ def train(components, info, utilization=None):
             if info.use_amp_obs:
                 amp_obs_demo = components.vecenv.fetch_amp_obs_demo()
                 amp_mb = amp_obs_demo.shape[0]
+            # the reference's bound term: a no-grad constant read once here (see config.py)
+            mbl_ref = None if cfg.bound_loss_grad else _rollout_bound_loss(components, pol)
         total_minibatches = experience.num_minibatches * cfg.update_epochs
         adv_ms = None
         tail_coefs = None
@@ -409,7 +449,11 @@ def train(components, info, utilization=None):
                         disc_loss = 0.5 * (bce(d_agent, torch.zeros_like(d_agent)) + bce(d_demo, torch.ones_like(d_demo)))
                         if cfg.disc_coef > 0:
                             loss = loss + disc_loss * cfg.disc_coef
-                    if fused_obj:
+                    if not cfg.bound_loss_grad:
+                        mbl = mbl_ref  # constant: changes the loss value only, never a gradient
+                        if cfg.bound_coef > 0 and mbl is not None:
+                            loss = loss + mbl * cfg.bound_coef
+                    elif fused_obj:
                         mbl = mbl_f  # already inside `loss` (bound_coef term of the fused objective)
                     else:
                         mbl = getattr(pol, "mean_bound_loss", None)
@@ -453,12 +497,21 @@ def train(components, info, utilization=None):
                                         (mbl.detach() if mbl is not None else torch.zeros((), device=cfg.device)),
                                         torch.zeros((), device=cfg.device),
                                         torch.zeros((), device=cfg.device)]).double() / total_minibatches
-            if cfg.target_kl is not None and float(approx_kl) > cfg.target_kl:
+            # ranks must agree on the early stop, or one would wait in the next minibatch's
+            # gradient all-reduce: the test reads the ranks' mean approx_kl
+            if cfg.target_kl is not None and _global_mean(approx_kl) > cfg.target_kl:
                 break
         with profile.train_misc:
+            if cfg.anneal_lr:  # core.py:405-408 (the caller's exp decay overrides it, as there)
+                frac = 1.0 - info.global_step / cfg.total_timesteps
+                components.optimizer.param_groups[0]["lr"] = frac * cfg.learning_rate
             p7, o3 = acc_ppo / total_minibatches, acc_opt / total_minibatches
             acc[[0, 1, 2, 3, 4, 5, 9]] += p7
             acc[[6, 7]] += o3[[0, 2]]
+            if mbl_ref is not None:
+                acc[9] = mbl_ref.double()  # the reference logs the rollout's value (constant)
+            elif not cfg.bound_loss_grad:
+                acc[9] = 0.0
             a = acc.cpu().numpy()
             losses = LossComponents(policy_loss=a[0], value_loss=a[1], entropy=a[2], old_approx_kl=a[3],
                                     approx_kl=a[4], clipfrac=a[5], before_clip_grad_norm=a[6],

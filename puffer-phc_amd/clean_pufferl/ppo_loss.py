@@ -2,9 +2,9 @@
 backward kernel (phc_ppo.hip) in place of the ~60 elementwise / reduction launches of the
 eager expression, with the same math (see the kernel header for the formulas and tie rules).
 
-`ppo_objective` returns the differentiable loss (pg - ent_coef ent + vf_coef v + bound_coef
-bound) and a detached [7] tensor of the logged means (pg, v, entropy, old_approx_kl, approx_kl,
-clipfrac, bound loss).  Gradients flow to mu and value only, as in the reference (sigma is a
+`ppo_objective` returns the differentiable loss (pg - ent_coef ent + vf_coef v, plus
+bound_coef bound only with TrainConfig.bound_loss_grad) and a detached [7] tensor of the logged
+means (pg, v, entropy, old_approx_kl, approx_kl, clipfrac, bound loss).  Gradients flow to mu and value only, as in the reference (sigma is a
 fixed parameter, the rollout tensors are data)."""
 
 import torch
@@ -32,9 +32,12 @@ class _PPOObjective(torch.autograd.Function):
 
 
 def ppo_coefs(cfg, soft_bound):
-    """phc_ppo_coefs of a TrainConfig (the bound term only when bound_coef > 0)."""
-    return _native.ppo_coefs(cfg.clip_coef, cfg.vf_clip_coef, cfg.vf_coef, cfg.ent_coef,
-                             cfg.bound_coef if cfg.bound_coef > 0 else 0.0, soft_bound, cfg.clip_vloss)
+    """phc_ppo_coefs of a TrainConfig.  The bound term enters the differentiable loss only with
+    TrainConfig.bound_loss_grad (the reference's bound term is a no-grad constant, see config.py);
+    the kernel still reports the minibatch's bound loss in stats[6]."""
+    bound = cfg.bound_coef if (cfg.bound_coef > 0 and getattr(cfg, "bound_loss_grad", False)) else 0.0
+    return _native.ppo_coefs(cfg.clip_coef, cfg.vf_clip_coef, cfg.vf_coef, cfg.ent_coef, bound, soft_bound,
+                             cfg.clip_vloss)
 
 
 def ppo_objective(mu, value, log_sigma, actions, old_logprob, adv, adv_mean, adv_std, old_value, returns, cfg,

@@ -172,6 +172,12 @@ class TrainConfig(DeviceConfig):
     ent_coef: float = 0.0
     disc_coef: float = 5.0
     bound_coef: float = 10.0
+    # the reference reads policy.mean_bound_loss ONCE at the start of train() (core.py:225): the
+    # value of the last rollout forward, computed under no_grad, so `loss += mean_bound_loss *
+    # bound_coef` (core.py:349-350) adds a constant -- no gradient -- and the logged value is
+    # that constant.  False (default) = exactly that; True = a per-minibatch bound loss that
+    # does backpropagate into mu (a deliberate deviation, off by default)
+    bound_loss_grad: bool = False
     l2_reg_coef: float = 0.0
     # policy GEMM arithmetic.  "fp16" (default) = fp16 GEMM operands on the hand-written MFMA
     # GEMM (phc_gemm.hip), fp32 accumulation and outputs, epilogues in fp32: TF32's arithmetic

@@ -71,7 +71,7 @@ class PHCPolicy(DiscriminatorPolicy):
         n = self.obs_norm
         return N.obs_half(obs, n.running_mean, n.running_var, n.epsilon, n.clip, out, rows)
 
-    def act_rollout(self, obs, noise, actions, logprob, value):
+    def act_rollout(self, obs, noise, actions, logprob, value, mu=None):
         """Rollout inference (encode_observations + decode_actions + sample_logits) writing the
         sampled actions, their log-probability and the value into the given buffers: half input
         (phc_obs_half), MFMA trunks, then LayerNorm+SiLU, both heads, the Normal sample and
@@ -87,7 +87,7 @@ class PHCPolicy(DiscriminatorPolicy):
         la, lc = self.actor_mlp[h], self.critic_mlp[h]
         vh, mh = self.critic_mlp[h + 2], self.mu[0]
         N.policy_act(y, (la.weight, la.bias), (lc.weight, lc.bias), la.eps, mh.weight, mh.bias, vh.weight, vh.bias,
-                     self.sigma, noise, actions, logprob, value,
+                     self.sigma, noise, actions, logprob, value, mu=mu,
                      std_max=1e-6 if self._deterministic_action is True else float("inf"))
         return True
 

@@ -96,6 +96,22 @@ def _worker(rank, world, port, root):
         t = torch.tensor([float(rank + 1)])
         D.allreduce_max_(t)
         assert float(t) == world
+        # (6) loop-control values agree across ranks: ranks with different
+        # truncation patterns store different mask-true row counts, and their minibatches give
+        # different approx_kl; the trainer's global_step and target_kl test use these reductions
+        from puffer_phc_amd.clean_pufferl import core as C
+
+        counts = [131072 - 17, 131072 - 905]
+        assert C._global_count(counts[rank], "cpu") == sum(counts)
+        kls = [0.004, 0.03]
+        kl = C._global_mean(torch.tensor(kls[rank]))
+        assert abs(kl - sum(kls) / world) < 1e-8
+        # target_kl = 0.02: rank 0 alone would continue and rank 1 alone would stop; both stop
+        # together or continue together on the shared mean
+        decision = torch.tensor([float(kl > 0.02)])
+        both = decision.clone()
+        D.allreduce_sum_(both)
+        assert float(both) in (0.0, float(world))
     finally:
         dist.destroy_process_group()
 

@@ -125,3 +125,27 @@ def test_state_dict_round_trip():
         o.fused_step(5.0)
     for x, y in zip(a, b):
         assert torch.equal(x.detach(), y.detach())
+
+
+@pytest.mark.parametrize("parts", [1, 2, 8, 9, 16, 17, 32])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_reduce_into_many_parts(parts, accumulate):
+    """phc_reduce_into (phc_optim.hip k_reduce_into) over many parts: the 8-running-sum branch
+    with its remainder loop (> 8 parts), a row stride wider than the columns and a part stride
+    wider than rows * row stride, several jobs of different shapes in one launch.  dst (+)=
+    src.sum(0) within rel 1e-6 of a float64 sum (the kernel sums in a fixed fp32 order)."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(parts)
+    jobs, refs = [], []
+    for rows, cols, pad_c, pad_p in [(37, 96, 8, 64), (1, 1000, 0, 24), (256, 69, 3, 0)]:
+        big = torch.randn((parts, rows * (cols + pad_c) + pad_p), device=DEV, generator=g)
+        src = big[:, :rows * (cols + pad_c)].reshape(parts, rows, cols + pad_c)[:, :, :cols]
+        dst = torch.randn((rows, cols), device=DEV, generator=g)
+        ref = src.double().sum(0) + (dst.double() if accumulate else 0.0)
+        jobs.append((src, dst))
+        refs.append(ref)
+    N.reduce_into(jobs, accumulate=accumulate)
+    torch.cuda.synchronize()
+    for (_, dst), ref in zip(jobs, refs):
+        torch.testing.assert_close(dst.double(), ref, rtol=1e-6, atol=1e-5)
