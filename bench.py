@@ -27,8 +27,10 @@ average kernel time from HIP start/stop events recorded by each launch's own dis
 `traffic` = HBM bytes per launch from rocprofv3 PMC counters (2 x FETCH_SIZE + WRITE_SIZE,
 gfx950 correction) read from profiles/traffic_<envs>.json when present, else null.
 
-cpu_baseline: the numpy oracle (oracle/phc_oracle.py) env step on the same 4096-env batch,
-1 thread, bounded to ~10 s, rank 0 at N=1 only (the PPO GEMMs have no CPU oracle).
+cpu_baseline: the numpy oracle (oracle/phc_oracle.py) env step on the same 4096-env batch at
+1 thread and over all available cores (forked env shards), plus the C restatement of the
+reference's GAE, bounded to ~10 s, rank 0 at N=1 only.  An env-step-only comparison (the PPO
+GEMMs have no CPU oracle); the line says so.
 """
 
 import argparse
@@ -104,10 +106,57 @@ def build_env(args, rank):
     return env, packed, cfg
 
 
-def cpu_baseline(env, packed, seconds):
-    """Oracle env step on the same batch (numpy, 1 thread)."""
+def _host_cpu():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def _host_workers():
+    """Worker processes for the all-cores leg: the CPUs this process may run on, capped at 16
+    (a GPU box's CPU share for one GPU; OMP_NUM_THREADS is set to it there)."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(avail, cap, 16))
+
+
+_CPU_SHARD = None  # (lib, args) of one worker, inherited through fork
+
+
+def _cpu_shard_run(job):
+    """One worker of the all-cores leg: `steps` oracle env steps over its env shard."""
     from oracle import phc_oracle as O
 
+    lo, hi, steps = job
+    lib, args = _CPU_SHARD
+    sub = tuple(a[lo:hi] for a in args)
+    O.env_step(lib, *sub)  # warm
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        O.env_step(lib, *sub)
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(env, packed, seconds):
+    """BASELINE.md §3 / SURVEY §8d: the CPU restatement of the env step (motion state x2 + reward
+    + reset + obs, the composition HumanoidPHC.step performs, physics excluded) on the same
+    4096-env batch, timed on this host at 1 thread and at all available cores (env shards over
+    forked worker processes, numpy fp32), plus the reference's GAE (oracle/gae.c, the Cython
+    loop restated in C) over one 131072-row batch.  This is an ENV-STEP-ONLY comparison: it
+    does not include policy inference or the PPO update that the headline value contains."""
+    import multiprocessing as mp
+
+    from oracle import c_oracle
+    from oracle import phc_oracle as O
+
+    global _CPU_SHARD
     fr = packed.frames.cpu().numpy()
     lib = O.MotionLib(fr[..., 0:3], fr[..., 3:7], packed.local_rot.cpu().numpy(), fr[..., 7:10], fr[..., 10:13],
                       packed.dof_vel.cpu().numpy(), packed.num_frames.cpu().numpy(),
@@ -118,18 +167,54 @@ def cpu_baseline(env, packed, seconds):
             e._global_offset.cpu().numpy(), e._rigid_body_state.cpu().numpy(), e._dof_vel.cpu().numpy(),
             e.dof_force_tensor.cpu().numpy())
     n = len(args[0])
+    half = seconds / 2
+    # 1 thread (the reference's setting after load_motions, motion_lib.py:335)
     O.env_step(lib, *args)  # warm
     t0 = time.perf_counter()
-    steps = 0
+    steps1 = 0
     while True:
         O.env_step(lib, *args)
-        steps += 1
-        if time.perf_counter() - t0 > seconds:
+        steps1 += 1
+        if time.perf_counter() - t0 > half:
             break
-    dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{steps} oracle env steps x {n} envs (motion state x2 + reward + reset + obs, numpy fp32, "
-                      f"1 thread, {dt:.1f}s)"}
+    dt1 = time.perf_counter() - t0
+    one = n * steps1 / dt1
+    # all cores: the same batch split into `workers` env shards, each stepped by a forked process
+    # (numpy only in the children: they never touch the GPU)
+    workers = _host_workers()
+    steps_all = max(2, int(round(half * one * workers * 0.75 / n)))  # ~half seconds at 75 % scaling
+    bounds = np.linspace(0, n, workers + 1).astype(int)
+    jobs = [(int(bounds[i]), int(bounds[i + 1]), steps_all) for i in range(workers)]
+    _CPU_SHARD = (lib, args)
+    try:
+        with mp.get_context("fork").Pool(workers) as pool:
+            pool.map(_cpu_shard_run, [(lo, min(hi, lo + 8), 1) for lo, hi, _ in jobs])  # fork + import warm-up
+            t0 = time.perf_counter()
+            per = pool.map(_cpu_shard_run, jobs)
+            dta = time.perf_counter() - t0
+    finally:
+        _CPU_SHARD = None
+    allc = n * steps_all / dta
+    # GAE (c_gae.pyx restated in C) over one PPO batch of 131072 rows, 1 thread
+    rng = np.random.default_rng(0)
+    B = 131072
+    d = (rng.random(B) < 0.01).astype(np.float32)
+    v, r = rng.standard_normal(B).astype(np.float32), rng.standard_normal(B).astype(np.float32)
+    c_oracle.compute_gae(d, v, r, 0.98, 0.2)
+    reps, t0 = 0, time.perf_counter()
+    while reps < 20 or time.perf_counter() - t0 < 0.5:
+        c_oracle.compute_gae(d, v, r, 0.98, 0.2)
+        reps += 1
+    gae_ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"value": allc, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "comparison": "env step only (motion state x2 + reward + reset + obs); no policy inference or PPO "
+                          "update, which the headline value includes",
+            "value_1_thread": one, "value_all_cores": allc, "cores_all": workers,
+            "host_nproc": os.cpu_count(), "host_cpu_model": _host_cpu(),
+            "gae_ms_131072_rows_1_thread": gae_ms,
+            "sample": f"{n} envs: {steps1} oracle env steps at 1 thread ({dt1:.1f}s); {steps_all} steps over "
+                      f"{workers} forked env shards ({dta:.1f}s, slowest shard {max(per):.1f}s); numpy fp32. "
+                      f"GAE: oracle/gae.c over 131072 rows x {reps}"}
 
 
 class Runner:

@@ -209,6 +209,11 @@ class HumanoidPHC:
         if isinstance(motion_train_file, PackedMotions):
             self._motion_train_lib = MotionLibSMPL.from_packed(motion_train_file, self.device, self.dt)
             self._motion_eval_lib = self._motion_lib = self._motion_train_lib
+            m = int(motion_train_file.num_frames.shape[0])
+            if m < self.num_envs:
+                # fewer clips than envs: env i plays clip i mod M (load_motions' remainder
+                # sampling, motion_lib.py:304-312); the kernels index the library by these ids
+                self._sampled_motion_ids.copy_(torch.arange(self.num_envs, device=self.device) % m)
             return
         mcfg = SimpleNamespace(motion_file=motion_train_file, device=self.device, fix_height=FixHeightMode.full_fix,
                                min_length=self.cfg.min_motion_len, max_length=self.cfg.max_episode_length,

@@ -5,10 +5,14 @@ within 1e-5); frame indices, reset and terminate flags bit-exact except where a 
 distance lies within 1e-6 of its threshold (ties are flagged, not compared).
 """
 
+import os
+
 import numpy as np
 import pytest
 
 from oracle import phc_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 ATOL = 1e-5
 RTOL = 1e-5
@@ -124,6 +128,19 @@ def test_gae(golden):
     np.testing.assert_array_equal(O.compute_gae(g["dones"], g["values"], g["rewards"], g["gamma"], g["lam"]), g["adv"])
     np.testing.assert_array_equal(O.compute_gae(g["dones2"], g["values2"], g["rewards2"], g["gamma2"], g["lam2"]),
                                   g["adv2"])
+
+
+def test_gae_c_restatement(golden):
+    """oracle/gae.c (the CPU baseline's GAE) == the reference's Cython output, bit for bit."""
+    import subprocess
+
+    from oracle import c_oracle
+
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    g = golden("gae")
+    for k in ("", "2"):
+        out = c_oracle.compute_gae(g["dones" + k], g["values" + k], g["rewards" + k], g["gamma" + k], g["lam" + k])
+        np.testing.assert_array_equal(out, g["adv" + k])
 
 
 def test_rms(golden):
