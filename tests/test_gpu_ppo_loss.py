@@ -25,6 +25,8 @@ class _Env:
 
 
 def _eager(pol, policy, obs, atn, old_lp, adv, val, ret, cfg):
+    # bound term: with cfg.bound_loss_grad a per-minibatch differentiable term; by default the
+    # reference's no-grad constant, which train() adds outside the objective (core.py:349-350)
     _, newlogprob, entropy, newvalue = policy(obs, action=atn)
     logratio = newlogprob - old_lp
     ratio = logratio.exp()
@@ -37,12 +39,15 @@ def _eager(pol, policy, obs, atn, old_lp, adv, val, ret, cfg):
     v_clipped = val + torch.clamp(v - val, -cfg.vf_clip_coef, cfg.vf_clip_coef)
     v_loss = torch.max((v - ret) ** 2, (v_clipped - ret) ** 2).mean()
     ent = entropy.mean()
-    loss = pg - cfg.ent_coef * ent + v_loss * cfg.vf_coef + pol.mean_bound_loss * cfg.bound_coef
+    loss = pg - cfg.ent_coef * ent + v_loss * cfg.vf_coef
+    if cfg.bound_loss_grad:
+        loss = loss + pol.mean_bound_loss * cfg.bound_coef
     stats = torch.stack([pg, v_loss, ent, old_kl, kl, clipfrac, pol.mean_bound_loss])
     return loss, stats.detach()
 
 
-def test_fused_objective_matches_eager():
+@pytest.mark.parametrize("bound_grad", [False, True])
+def test_fused_objective_matches_eager(bound_grad):
     from puffer_phc_amd.clean_pufferl.ppo_loss import ppo_objective
     from puffer_phc_amd.config import TrainConfig
     from puffer_phc_amd.policies import PHCPolicy, Policy
@@ -52,7 +57,7 @@ def test_fused_objective_matches_eager():
     pol = policy.policy
     with torch.no_grad():
         pol.mu[0].weight.mul_(100.0)  # push some |mu| past the 0.9 soft bound
-    cfg = TrainConfig(ent_coef=0.01)
+    cfg = TrainConfig(ent_coef=0.01, bound_loss_grad=bound_grad)
     g = torch.Generator(device=DEV).manual_seed(1)
     M = 4096
     obs = torch.randn((M, 934), device=DEV, generator=g)
