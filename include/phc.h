@@ -246,8 +246,13 @@ int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, 
  *             pre-activation BIAS_SILU wrote, bias included), and
  *             bias_grad[c] = column sums of that product in fp32 (nullable; needs
  *             phc_twin_gemm_workspace_bytes of workspace)
+ *   BIAS_RELU out = relu(C + bias[c])   (AMP discriminator Linear + ReLU,
+ *             puffer_phc/policies/discriminator_policy.py:43-53)
+ *   RELU_GRAD out = C * [aux + bias[c] > 0] (aux = the BIAS_RELU output, bias null: torch's
+ *             threshold_backward reads the ReLU result), bias_grad as SILU_GRAD
  * out is fp32 or dtype (out_dtype). */
-enum { PHC_EPI_STORE = 0, PHC_EPI_BIAS = 1, PHC_EPI_BIAS_SILU = 2, PHC_EPI_SILU_GRAD = 3 };
+enum { PHC_EPI_STORE = 0, PHC_EPI_BIAS = 1, PHC_EPI_BIAS_SILU = 2, PHC_EPI_SILU_GRAD = 3, PHC_EPI_BIAS_RELU = 4,
+       PHC_EPI_RELU_GRAD = 5 };
 typedef struct phc_gemm_desc {
   const void *a;
   const void *b;
@@ -460,6 +465,22 @@ int32_t phc_tail_blocks(int64_t rows);
 int phc_tail_ln_fwd(const phc_tail_ln_args *args, void *stream);
 int phc_tail_ln_bwd(const phc_tail_ln_args *args, const float *dh_actor, const float *dmu, const float *dvalue,
                     int32_t num_actions, void *dy, int32_t dtype, float *partial, void *stream);
+
+/* R22: the AMP discriminator's logits head (puffer_phc/policies/discriminator_policy.py:72-79:
+ * Linear(hidden, 1) after the second ReLU layer; the two wide layers run on phc_twin_gemm with the
+ * BIAS_RELU / RELU_GRAD epilogues) on h [rows, width] f16 / bf16 (ldh, 16-byte aligned; width
+ * 8..1024, % 8), fp32 weights w [width] and bias b [1]:
+ *   fwd: logits[r] = h[r] . w + b (nullable) and reward[r] = -log(max(1 - sigmoid(logits[r]), 1e-4))
+ *        (nullable; the adversarial reward of clean_pufferl/core.py:229-242).
+ *   bwd: from grad_logits [rows] fp32: grad_h[r, j] = grad_logits[r] * w[j] * [h[r, j] > 0] in dtype
+ *        (ldg), and per-block partial rows parts [phc_disc_head_bwd_blocks(rows), 2 * width + 4] =
+ *        [sum gl * h (head weight grad) | sum grad_h in fp32 (second layer bias grad) | sum gl (head
+ *        bias grad) | 3 zeros], to be summed over the blocks (phc_reduce_into). */
+int64_t phc_disc_head_bwd_blocks(int64_t rows);
+int phc_disc_head_fwd(const void *h, int64_t ldh, int64_t rows, int32_t width, int32_t dtype, const float *w,
+                      const float *b, float *logits, float *reward, void *stream);
+int phc_disc_head_bwd(const void *h, int64_t ldh, int64_t rows, int32_t width, int32_t dtype, const float *w,
+                      const float *grad_logits, void *grad_h, int64_t ldg, float *parts, void *stream);
 
 /* Library version and last error (thread-local). */
 int phc_version(void);

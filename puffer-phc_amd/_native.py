@@ -95,7 +95,7 @@ class GemmDescC(ctypes.Structure):
                 ("twin_cols", ctypes.c_int32), ("aux_dtype", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
-EPI_STORE, EPI_BIAS, EPI_BIAS_SILU, EPI_SILU_GRAD = 0, 1, 2, 3
+EPI_STORE, EPI_BIAS, EPI_BIAS_SILU, EPI_SILU_GRAD, EPI_BIAS_RELU, EPI_RELU_GRAD = 0, 1, 2, 3, 4, 5
 
 
 class WgradDescC(ctypes.Structure):
@@ -214,6 +214,11 @@ _EXPORTS = {
     "phc_rms_update": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "phc_rms_normalize": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, ctypes.c_float,
                                           c_vp]),
+    "phc_disc_head_bwd_blocks": (c_i64, [c_i64]),
+    "phc_disc_head_fwd": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.c_int32, ctypes.c_int32, c_vp, c_vp, c_vp, c_vp,
+                                          c_vp]),
+    "phc_disc_head_bwd": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.c_int32, ctypes.c_int32, c_vp, c_vp, c_vp, c_i64,
+                                          c_vp, c_vp]),
 }
 
 
@@ -691,6 +696,45 @@ def act_bwd(grad_out, go_layout, pre, pre_layout, grad_pre, gp_layout, bias_grad
                              gp_layout, _ptr(bias_grad, torch.float32, (groups * cols,), "bias_grad", nullable=True),
                              rows, groups, cols, act, DTYPE_CODE[dt], DTYPE_CODE[ot], ws, _stream()),
            "phc_act_bwd")
+
+
+# ------------------------------------------------------- AMP discriminator --
+def _half2d(t, name):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype not in (torch.float16, torch.bfloat16) \
+            or t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a 2-D f16 / bf16 device tensor with contiguous columns")
+    return t
+
+
+def disc_head_fwd(h, w, b, logits=None, reward=None):
+    """logits = h . w + b and / or the adversarial reward -log(max(1 - sigmoid(logits), 1e-4)) for
+    h [rows, width] f16 / bf16 (phc_disc_head_fwd)."""
+    _half2d(h, "disc_head_fwd h")
+    rows, width = h.shape
+    _check(lib().phc_disc_head_fwd(h.data_ptr(), h.stride(0), rows, width, DTYPE_CODE[h.dtype],
+                                   _ptr(w.reshape(-1), torch.float32, (width,), "w"),
+                                   _ptr(b.reshape(-1), torch.float32, (1,), "b"),
+                                   _ptr(logits, torch.float32, (rows,), "logits", nullable=True),
+                                   _ptr(reward, torch.float32, (rows,), "reward", nullable=True), _stream()),
+           "phc_disc_head_fwd")
+
+
+def disc_head_bwd(h, w, grad_logits, grad_h):
+    """grad_h = grad_logits * w * [h > 0] (operand dtype) and the per-block partial rows
+    [blocks, 2 * width + 4] = (head weight grad | second layer bias grad | head bias grad | 0 0 0)
+    (phc_disc_head_bwd); returns the partials."""
+    _half2d(h, "disc_head_bwd h")
+    _half2d(grad_h, "disc_head_bwd grad_h")
+    rows, width = h.shape
+    if tuple(grad_h.shape) != (rows, width) or grad_h.dtype != h.dtype:
+        raise ValueError("disc_head_bwd: grad_h must match h")
+    parts = torch.empty((lib().phc_disc_head_bwd_blocks(rows), 2 * width + 4), dtype=torch.float32, device=h.device)
+    _check(lib().phc_disc_head_bwd(h.data_ptr(), h.stride(0), rows, width, DTYPE_CODE[h.dtype],
+                                   _ptr(w.reshape(-1), torch.float32, (width,), "w"),
+                                   _ptr(grad_logits, torch.float32, (rows,), "grad_logits"), grad_h.data_ptr(),
+                                   grad_h.stride(0), parts.data_ptr(), _stream()),
+           "phc_disc_head_bwd")
+    return parts
 
 
 # ------------------------------------------------------------ PPO objective --

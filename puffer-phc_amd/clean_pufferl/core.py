@@ -325,10 +325,16 @@ def compute_advantages(components, info):
         else None
     if info.use_amp_obs and discriminate is not None:
         with torch.no_grad(), autocast(cfg):
-            for mb in range(experience.num_minibatches):
-                logits = discriminate(experience.b_amp_obs[mb]).squeeze()
-                prob = 1 / (1 + torch.exp(-logits))
-                adv_rew[mb] = -torch.log(torch.clamp(1 - prob, min=0.0001))
+            if hasattr(components.policy.policy, "adversarial_reward"):
+                # every minibatch's rows in one pass (rows are independent; same values as the
+                # reference's per-minibatch loop), gathered from the buffer by index
+                adv_rew = components.policy.policy.adversarial_reward(
+                    [(experience.amp_obs, experience.b_amp_idx.reshape(-1))]).view(adv_rew.shape)
+            else:
+                for mb in range(experience.num_minibatches):
+                    logits = discriminate(experience.b_amp_obs[mb]).squeeze()
+                    prob = 1 / (1 + torch.exp(-logits))
+                    adv_rew[mb] = -torch.log(torch.clamp(1 - prob, min=0.0001))
     # the adversarial reward is indexed like the reference: flat ravel of [num_mb, mb_size]
     advantages = components.gae(dones, values, (rewards + adv_rew.reshape(-1)).contiguous(), cfg.gamma,
                                 cfg.gae_lambda)
@@ -439,14 +445,20 @@ def train(components, info, utilization=None):
                         entropy_loss = entropy.mean()
                         loss = pg_loss - cfg.ent_coef * entropy_loss + v_loss * cfg.vf_coef
                     disc_loss = torch.zeros((), device=cfg.device)
+                    disc_acc = (torch.zeros((), device=cfg.device), torch.zeros((), device=cfg.device))
                     if info.use_amp_obs:
-                        amp_agent = torch.cat([experience.b_amp_obs[mb][:amp_mb],
-                                               experience.b_amp_obs_replay[mb][:amp_mb]])
+                        # agent rows, replay rows and demo rows through the discriminator in one
+                        # pass (core.py:336-344 calls it twice; rows are independent)
                         with autocast(cfg):
-                            d_agent = pol.discriminate(amp_agent).float()
-                            d_demo = pol.discriminate(amp_obs_demo).float()
+                            d_all = pol.discriminate_rows(
+                                [(experience.amp_obs, experience.b_amp_idx[mb][:amp_mb]),
+                                 (experience.amp_obs_replay, experience.b_amp_rep_idx[mb][:amp_mb]),
+                                 (amp_obs_demo, None)]).float()
+                        d_agent, d_demo = d_all[:2 * amp_mb], d_all[2 * amp_mb:]
                         bce = torch.nn.BCEWithLogitsLoss()
                         disc_loss = 0.5 * (bce(d_agent, torch.zeros_like(d_agent)) + bce(d_demo, torch.ones_like(d_demo)))
+                        # core.py:394-395
+                        disc_acc = ((d_agent.detach() < 0).float().mean(), (d_demo.detach() > 0).float().mean())
                         if cfg.disc_coef > 0:
                             loss = loss + disc_loss * cfg.disc_coef
                     if not cfg.bound_loss_grad:
@@ -495,8 +507,7 @@ def train(components, info, utilization=None):
                     acc += torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,
                                         approx_kl, clipfrac, gnorm, l2.detach(), disc_loss.detach(),
                                         (mbl.detach() if mbl is not None else torch.zeros((), device=cfg.device)),
-                                        torch.zeros((), device=cfg.device),
-                                        torch.zeros((), device=cfg.device)]).double() / total_minibatches
+                                        disc_acc[0], disc_acc[1]]).double() / total_minibatches
             # ranks must agree on the early stop, or one would wait in the next minibatch's
             # gradient all-reduce: the test reads the ranks' mean approx_kl
             if cfg.target_kl is not None and _global_mean(approx_kl) > cfg.target_kl:
@@ -515,7 +526,8 @@ def train(components, info, utilization=None):
             a = acc.cpu().numpy()
             losses = LossComponents(policy_loss=a[0], value_loss=a[1], entropy=a[2], old_approx_kl=a[3],
                                     approx_kl=a[4], clipfrac=a[5], before_clip_grad_norm=a[6],
-                                    l2_init_reg_loss=a[7], disc_loss=a[8], mean_bound_loss=a[9])
+                                    l2_init_reg_loss=a[7], disc_loss=a[8], mean_bound_loss=a[9],
+                                    disc_agent_acc=a[10], disc_demo_acc=a[11])
             y_pred = experience.sorted_values
             y_true = experience.returns
             var_y = torch.var(y_true, unbiased=False)

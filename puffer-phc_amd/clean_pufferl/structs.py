@@ -117,7 +117,9 @@ class Experience:
         self.b_truncated = self.truncateds[b_idxs]
         self.b_values = self.values[b_flat]
         if self.use_amp_obs:
-            self.b_amp_obs = self.amp_obs[b_flat]
+            # AMP rows stay where they are: the discriminator gathers them through these indices
+            # (b_amp_obs / b_amp_obs_replay below materialise the reference's tensors on demand)
+            self.b_amp_idx = b_flat
             if not self.amp_obs_replay_filled:
                 self.amp_obs_replay[:] = self.amp_obs[:]
                 self.amp_obs_replay_filled = True
@@ -126,7 +128,17 @@ class Experience:
                 self.amp_obs_replay[upd] = self.amp_obs[upd]
             rep = torch.randperm(self.batch_size, device=self.device).reshape(self.num_minibatches,
                                                                                self.minibatch_size)
-            self.b_amp_obs_replay = self.amp_obs_replay[rep]
+            self.b_amp_rep_idx = rep
+
+    @property
+    def b_amp_obs(self):
+        """amp_obs in minibatch order, [num_minibatches, minibatch_size, amp_obs_size] (structs.py:157)."""
+        return self.amp_obs[self.b_amp_idx]
+
+    @property
+    def b_amp_obs_replay(self):
+        """The replay rows drawn for each minibatch (structs.py:158-160)."""
+        return self.amp_obs_replay[self.b_amp_rep_idx]
 
 
 @dataclass

@@ -10,6 +10,10 @@
 //   PHC_EPI_BIAS_SILU : pre = acc + bias (aux, fp32 or the operand type, nullable), out = silu(pre)
 //   PHC_EPI_SILU_GRAD : out = acc * silu'(aux + bias) (bias nullable: aux is then the whole
 //                       pre-activation, as BIAS_SILU writes it); bias_grad = column sums of out
+//   PHC_EPI_BIAS_RELU : out = relu(acc + bias)   (the AMP discriminator's Linear + ReLU,
+//                       policies/discriminator_policy.py:43-53)
+//   PHC_EPI_RELU_GRAD : out = acc * [aux + bias > 0] (aux = the forward's ReLU output, bias null:
+//                       relu' from the output as torch's threshold_backward); bias_grad as above
 // so no fp32 GEMM output makes an HBM round trip through a separate elementwise kernel.
 //
 // Tiling: 128 x 128 output tile per 256-thread block (4 waves as 2 x 2, 64 x 64 per wave =
@@ -162,6 +166,8 @@ template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_> struct Tile {
 template <typename T, typename OutT, int EPI, typename TL>
 __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
   constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
+  constexpr bool kGrad = EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD;  // aux read + column sums
+  constexpr bool kBiasFwd = EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU || EPI == PHC_EPI_BIAS_RELU;
   using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][A BM rows | B BN rows]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -321,10 +327,10 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
       // flight while batch b is processed), an fp32 one loaded per batch
       constexpr int U = 4;
       static_assert(IT % U == 0, "row batches");
-      const bool pipe = EPI == PHC_EPI_SILU_GRAD && g.aux_half;
-      uint2 raw[2][EPI == PHC_EPI_SILU_GRAD ? U : 1];
+      const bool pipe = kGrad && g.aux_half;
+      uint2 raw[2][kGrad ? U : 1];
       auto load_raw = [&](int b) {
-        if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+        if constexpr (kGrad) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int64_t row = m0 + trow(pass, b * U + u);
@@ -336,7 +342,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
 #pragma unroll
       for (int i0 = 0; i0 < IT; i0 += U) {
         float4 av[U];
-        if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+        if constexpr (kGrad) {
           if (pipe) {
             if (i0 + U < IT) load_raw(i0 / U + 1);
 #pragma unroll
@@ -365,13 +371,23 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
               v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
               csum[q] += v[q];
             }
-          } else if constexpr (EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU) {
+          } else if constexpr (EPI == PHC_EPI_RELU_GRAD) {
+            const float a[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[q] = a[q] + bias4[q] > 0.0f ? v[q] : 0.0f;
+              csum[q] += v[q];
+            }
+          } else if constexpr (kBiasFwd) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] += bias4[q];
             if constexpr (EPI == PHC_EPI_BIAS_SILU) {
               if (g.aux) aux_store4<T>(g, ab + row * as, v);
 #pragma unroll
               for (int q = 0; q < 4; ++q) v[q] = gemm_silu(v[q]);
+            } else if constexpr (EPI == PHC_EPI_BIAS_RELU) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
             }
           }
           gemm_store4<OutT>(g.out, ob + row * os, v);
@@ -386,7 +402,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
       const float4 t = *reinterpret_cast<const float4 *>(&ep[r * BN + (c4 ^ (((r >> 2) & 3) << 4))]);
       float v[4] = {t.x, t.y, t.z, t.w};
       float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+      if constexpr (kGrad) {
         if (vec) {
           const float4 av = aux_load4<T>(g, gemm_twin_off(g, g.aux_layout, row, lc));
           a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
@@ -397,14 +413,18 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if constexpr (EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU) {
+        if constexpr (kBiasFwd) {
           v[q] += bias4[q];
           a[q] = v[q];
           if constexpr (EPI == PHC_EPI_BIAS_SILU) v[q] = gemm_silu(v[q]);
+          if constexpr (EPI == PHC_EPI_BIAS_RELU) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
         } else if constexpr (EPI == PHC_EPI_SILU_GRAD) {
           const float x = a[q] + bias4[q];
           const float sg = gemm_sigmoid(x);
           v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
+          csum[q] += gcol + q < g.n ? v[q] : 0.0f;
+        } else if constexpr (EPI == PHC_EPI_RELU_GRAD) {
+          v[q] = a[q] + bias4[q] > 0.0f ? v[q] : 0.0f;
           csum[q] += gcol + q < g.n ? v[q] : 0.0f;
         }
       }
@@ -424,7 +444,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
       }
     }
   }
-  if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+  if constexpr (kGrad) {
     if (!g.partial) return;
     // column sums over the tile's rows: row groups inside a wave by shuffle, the waves by LDS
     if constexpr (kColThreads == 32) {
@@ -776,7 +796,9 @@ static void launch_epi(int epi, int cfg, const GemmArgs &g, int64_t blocks, hipS
     case PHC_EPI_STORE: launch_cfg<T, OutT, PHC_EPI_STORE>(cfg, g, blocks, st); break;
     case PHC_EPI_BIAS: launch_cfg<T, OutT, PHC_EPI_BIAS>(cfg, g, blocks, st); break;
     case PHC_EPI_BIAS_SILU: launch_cfg<T, OutT, PHC_EPI_BIAS_SILU>(cfg, g, blocks, st); break;
-    default: launch_cfg<T, OutT, PHC_EPI_SILU_GRAD>(cfg, g, blocks, st); break;
+    case PHC_EPI_SILU_GRAD: launch_cfg<T, OutT, PHC_EPI_SILU_GRAD>(cfg, g, blocks, st); break;
+    case PHC_EPI_BIAS_RELU: launch_cfg<T, OutT, PHC_EPI_BIAS_RELU>(cfg, g, blocks, st); break;
+    default: launch_cfg<T, OutT, PHC_EPI_RELU_GRAD>(cfg, g, blocks, st); break;
   }
 }
 
@@ -845,15 +867,17 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
               "twin_gemm: operands must be 16-byte aligned");
   PHC_REQUIRE(d->dtype == PHC_DT_F16 || d->dtype == PHC_DT_BF16, "twin_gemm: operands must be f16 or bf16");
   PHC_REQUIRE(d->out_dtype == PHC_DT_F32 || d->out_dtype == d->dtype, "twin_gemm: out must be f32 or the operand type");
-  PHC_REQUIRE(d->epilogue >= PHC_EPI_STORE && d->epilogue <= PHC_EPI_SILU_GRAD, "twin_gemm: bad epilogue");
+  PHC_REQUIRE(d->epilogue >= PHC_EPI_STORE && d->epilogue <= PHC_EPI_RELU_GRAD, "twin_gemm: bad epilogue");
+  const bool grad_epi = d->epilogue == PHC_EPI_SILU_GRAD || d->epilogue == PHC_EPI_RELU_GRAD;
   PHC_REQUIRE(d->twin_groups >= 1 && d->twin_cols >= 1 && d->twin_groups * d->twin_cols == d->batch * d->n,
               "twin_gemm: twin geometry must cover batch * n columns");
-  PHC_REQUIRE(!(d->epilogue == PHC_EPI_BIAS || d->epilogue == PHC_EPI_BIAS_SILU) || d->bias,
+  PHC_REQUIRE(!(d->epilogue == PHC_EPI_BIAS || d->epilogue == PHC_EPI_BIAS_SILU || d->epilogue == PHC_EPI_BIAS_RELU) ||
+                  d->bias,
               "twin_gemm: epilogue needs the bias");
-  PHC_REQUIRE(d->epilogue != PHC_EPI_SILU_GRAD || d->aux, "twin_gemm: SILU_GRAD needs the pre-activation (aux)");
+  PHC_REQUIRE(!grad_epi || d->aux, "twin_gemm: SILU_GRAD / RELU_GRAD need the (pre-)activation (aux)");
   PHC_REQUIRE(d->aux_dtype == PHC_DT_F32 || d->aux_dtype == d->dtype, "twin_gemm: aux must be f32 or the operand type");
-  PHC_REQUIRE(!bias_grad || (d->epilogue == PHC_EPI_SILU_GRAD && workspace),
-              "twin_gemm: bias_grad needs the SILU_GRAD epilogue and a workspace");
+  PHC_REQUIRE(!bias_grad || (grad_epi && workspace),
+              "twin_gemm: bias_grad needs the SILU_GRAD / RELU_GRAD epilogue and a workspace");
   const int cfg = gemm_config(d->m, d->n, d->batch);
   int bm, bn;
   gemm_tile_dims(cfg, &bm, &bn);
@@ -915,7 +939,7 @@ extern "C" int phc_weight_grad(const phc_wgrad_desc *d, void *stream) {
               "weight_grad: rows (%lld) must be a multiple of 64 * splits (%d)", (long long)d->rows, d->splits);
   PHC_REQUIRE(d->ldg >= d->m && d->ldz >= d->n && d->ldg % 8 == 0 && d->ldz % 8 == 0,
               "weight_grad: leading dimensions must cover the columns and be multiples of 8");
-  PHC_REQUIRE(d->g_batch_stride % 8 == 0 && d->z_batch_stride % 8 == 0, "weight_grad: batch strides must be % 8");
+  PHC_REQUIRE(d->g_batch_stride % 8 == 0 && d->z_batch_stride % 8 == 0, "weight_grad: batch strides must be multiples of 8");
   PHC_REQUIRE((reinterpret_cast<uintptr_t>(d->g) & 15) == 0 && (reinterpret_cast<uintptr_t>(d->z) & 15) == 0,
               "weight_grad: operands must be 16-byte aligned");
   PHC_REQUIRE(d->dtype == PHC_DT_F16 || d->dtype == PHC_DT_BF16, "weight_grad: operands must be f16 or bf16");
@@ -969,7 +993,7 @@ extern "C" int phc_weight_grad_group(const phc_wgrad_problem *probs, int32_t cou
     const phc_wgrad_problem &d = probs[i];
     PHC_REQUIRE(d.g && d.z && d.dst[0], "weight_grad_group: problem %d: null operand", i);
     PHC_REQUIRE(d.m >= 8 && d.n >= 8 && d.m % 8 == 0 && d.n % 8 == 0 && (d.batch == 1 || d.batch == 2),
-                "weight_grad_group: problem %d: m, n % 8, batch 1 or 2", i);
+                "weight_grad_group: problem %d: m, n multiples of 8, batch 1 or 2", i);
     PHC_REQUIRE(d.ldg >= d.m && d.ldz >= d.n && d.ldg % 8 == 0 && d.ldz % 8 == 0 && d.g_batch_stride % 8 == 0 &&
                     d.z_batch_stride % 8 == 0,
                 "weight_grad_group: problem %d: leading dimensions / batch strides", i);

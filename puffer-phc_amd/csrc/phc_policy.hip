@@ -65,20 +65,21 @@ __global__ __launch_bounds__(256) void k_obs_half(const float *__restrict__ obs,
   *reinterpret_cast<uint4 *>(out + (int64_t)r * ldo + c0) = raw;
 }
 
-// Row-per-wave form (ld_out <= 1024): lane l owns output chunks l and l + 64 (8 columns each) of
-// every row its wave visits, so the per-column mean and sqrt(var + eps) are loaded and computed
+// Row-per-wave form (ld_out <= 64 * 8 * NC: 1024 for the policy's 934-wide obs, 2048 for the
+// 1960-wide AMP obs): lane l owns output chunks l + 64 c, c < NC (8 columns each) of every row its
+// wave visits, so the per-column mean and sqrt(var + eps) are loaded and computed
 // once per lane instead of once per element; rows_per_wave rows per wave, loads of two rows in
 // flight.  Same expression as k_rms_normalize / the generic form: bit-identical outputs.
-template <typename T>
+template <typename T, int NC>
 __global__ __launch_bounds__(256) void k_obs_half_rows(const float *__restrict__ obs, const int64_t *__restrict__ rows,
                                                        int64_t m, int d, int ldo, const float *__restrict__ mean,
                                                        const float *__restrict__ var, float eps, float clip,
                                                        int rows_per_wave, T *__restrict__ out) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int chunks = ldo / 8;
-  float mv[2][8], dv[2][8];
+  float mv[NC][8], dv[NC][8];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int col = (lane + 64 * c) * 8 + e;
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(256) void k_obs_half_rows(const float *__restrict__
     const int64_t src = rows ? rows[r] : r;
     const float *x = obs + src * d;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < NC; ++c) {
       const int ch = lane + 64 * c;
       if (ch >= chunks) continue;
       const int c0 = ch * 8;
@@ -301,16 +302,26 @@ extern "C" int phc_obs_half(const float *obs, const int64_t *rows, int64_t m, in
   PHC_REQUIRE((reinterpret_cast<uintptr_t>(out) & 15) == 0, "obs_half: out must be 16-byte aligned");
   PHC_REQUIRE(dtype == PHC_DT_F16 || dtype == PHC_DT_BF16, "obs_half: dtype must be f16 or bf16");
   hipStream_t st = as_stream(stream);
-  if (ld_out <= 1024) {  // row-per-wave form
+  if (ld_out <= 2048) {  // row-per-wave form
     const int rpw = m >= 65536 ? 8 : (m >= 16384 ? 4 : 1);
     const int64_t blocks = (m + 4 * rpw - 1) / (4 * rpw);
     PHC_REQUIRE(blocks < (1ll << 31), "obs_half: too many rows");
-    if (dtype == PHC_DT_F16)
-      hipLaunchKernelGGL(k_obs_half_rows<_Float16>, dim3((unsigned)blocks), dim3(256), 0, st, obs, rows, m, (int)d,
-                         (int)ld_out, mean, var, eps, clip, rpw, static_cast<_Float16 *>(out));
-    else
-      hipLaunchKernelGGL(k_obs_half_rows<__bf16>, dim3((unsigned)blocks), dim3(256), 0, st, obs, rows, m, (int)d,
-                         (int)ld_out, mean, var, eps, clip, rpw, static_cast<__bf16 *>(out));
+    const dim3 grid((unsigned)blocks);
+    if (dtype == PHC_DT_F16) {
+      if (ld_out <= 1024)
+        hipLaunchKernelGGL((k_obs_half_rows<_Float16, 2>), grid, dim3(256), 0, st, obs, rows, m, (int)d, (int)ld_out,
+                           mean, var, eps, clip, rpw, static_cast<_Float16 *>(out));
+      else
+        hipLaunchKernelGGL((k_obs_half_rows<_Float16, 4>), grid, dim3(256), 0, st, obs, rows, m, (int)d, (int)ld_out,
+                           mean, var, eps, clip, rpw, static_cast<_Float16 *>(out));
+    } else {
+      if (ld_out <= 1024)
+        hipLaunchKernelGGL((k_obs_half_rows<__bf16, 2>), grid, dim3(256), 0, st, obs, rows, m, (int)d, (int)ld_out,
+                           mean, var, eps, clip, rpw, static_cast<__bf16 *>(out));
+      else
+        hipLaunchKernelGGL((k_obs_half_rows<__bf16, 4>), grid, dim3(256), 0, st, obs, rows, m, (int)d, (int)ld_out,
+                           mean, var, eps, clip, rpw, static_cast<__bf16 *>(out));
+    }
     return check_launch("obs_half");
   }
   const int64_t threads = m * (ld_out / 8);

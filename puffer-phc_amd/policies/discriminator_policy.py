@@ -3,8 +3,11 @@
 import torch
 from torch import nn
 
+from . import disc_mlp
+from .disc_mlp import mfma_disc_supported
 from .pufferl_policy import Linear, layer_init
 from .running_norm import RunningNorm
+from .twin_mlp import _compute_dtype
 
 
 class DiscriminatorPolicy(nn.Module):
@@ -46,9 +49,30 @@ class DiscriminatorPolicy(nn.Module):
         self._deterministic_action = value
 
     def discriminate(self, amp_obs):
+        """Logits [rows, 1] (discriminator_policy.py:72-79); under f16 / bf16 autocast on the MFMA
+        path (disc_mlp.py), otherwise the nn.Linear modules in fp32."""
         if not self.use_amp_obs:
             return None
+        if mfma_disc_supported(self, _compute_dtype()):
+            return disc_mlp.discriminate_rows(self, [(amp_obs.float().contiguous(), None)])
         return self._disc_logits(self._disc_mlp(self.amp_obs_norm(amp_obs)))
+
+    def discriminate_rows(self, sources):
+        """discriminate() of the concatenated rows of (amp_obs [*, D], row index [n] or None)
+        sources, gathered inside the input kernel on the MFMA path (no copies of the rows)."""
+        if mfma_disc_supported(self, _compute_dtype()):
+            return disc_mlp.discriminate_rows(self, sources)
+        return self.discriminate(torch.cat([src if idx is None else src[idx] for src, idx in sources]))
+
+    @torch.no_grad()
+    def adversarial_reward(self, sources):
+        """-log(max(1 - sigmoid(logits), 1e-4)) [rows] of the concatenated sources
+        (clean_pufferl/core.py:229-242)."""
+        if mfma_disc_supported(self, _compute_dtype()):
+            return disc_mlp.adversarial_reward(self, sources)
+        logits = self.discriminate_rows(sources).float().reshape(-1)
+        prob = 1 / (1 + torch.exp(-logits))
+        return -torch.log(torch.maximum(1 - prob, torch.tensor(0.0001, device=logits.device)))
 
     def update_obs_rms(self, obs):
         self.obs_norm.update(obs)

@@ -116,6 +116,37 @@ def test_silu_grad_and_bias_grad(out_layout, pre_dtype):
     torch.testing.assert_close(db, p.grad.sum(1).reshape(-1), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("m", [777, 8192])  # 128 x 128 tiles; 256 x 256 tiles (>= 256 tiles)
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_relu_epilogues(dtype, m):
+    """BIAS_RELU (the discriminator's Linear + ReLU) and RELU_GRAD (its backward from the ReLU
+    output, bias-gradient column sums from the fp32 products) vs torch in fp32."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(6)
+    k, n = 512, 1024
+    x = torch.randn((m, k), device=DEV, generator=g).to(dtype)
+    w = (torch.randn((n, k), device=DEV, generator=g) / k ** 0.5).to(dtype)
+    b = torch.randn(n, device=DEV, generator=g) * 0.3
+    h = torch.empty((m, n), dtype=dtype, device=DEV)
+    N.twin_gemm(x, w, N.EPI_BIAS_RELU, h, (1, n), bias=b)
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    eps = 2.0 ** -8 if dtype == torch.float16 else 2.0 ** -5
+    torch.testing.assert_close(h.float(), ref.to(dtype).float(), rtol=eps, atol=1e-3)
+    assert 0.2 < float((h > 0).float().mean()) < 0.8
+    # backward: gin = (gr @ W^T-layout) * [h > 0]; W given as [n_in=n, n_out] for gr [m, n_out]
+    n_out = 256
+    gr = torch.randn((m, n_out), device=DEV, generator=g).to(dtype)
+    w2 = (torch.randn((n_out, n), device=DEV, generator=g) / n_out ** 0.5).to(dtype)
+    w2t = w2.t().contiguous()  # [n, n_out]
+    gin = torch.empty((m, n), dtype=dtype, device=DEV)
+    db = torch.empty(n, device=DEV)
+    N.twin_gemm(gr, w2t, N.EPI_RELU_GRAD, gin, (1, n), aux=h, bias_grad=db)
+    full = (gr.float() @ w2.float()) * (h.float() > 0)
+    torch.testing.assert_close(gin.float(), full.to(dtype).float(), rtol=eps, atol=1e-3)
+    torch.testing.assert_close(db, full.sum(0), rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("epi", ["bias_silu", "bias_f32", "silu_grad"])
 def test_large_ragged_256_tiles(epi):
     """Shapes large enough for the 256 x 256 tile configuration (>= 512 tiles), with ragged rows
