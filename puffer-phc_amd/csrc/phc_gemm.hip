@@ -121,38 +121,50 @@ template <typename OutT> __device__ __forceinline__ void gemm_store4(void *p, in
   }
 }
 
-// issue the global_load_lds of one R-row x 64-column operand tile (R / 8 wave-instructions over
-// the block's W waves)
-template <int R, int W>
+// issue the global_load_lds of one R-row x BK-column operand tile (R * BK / 512 wave-instructions
+// over the block's W waves).  BK = 64: LDS row r holds tile row r, its 16-B chunk c at slot
+// c ^ (r & 7).  BK = 32: LDS row R holds tile rows 2R (chunks 0-3) and 2R + 1 (chunks 4-7), slot
+// p ^ (R & 7); either way the 16 rows one ds_read_b128 fragment read touches hit 16 distinct
+// 16-B bank slots in each of its lane groups (checked exhaustively for both layouts).
+template <int R, int W, int BK>
 __device__ __forceinline__ void stage_tile(const char *base, int64_t ld, int64_t row0, int64_t rows, int k0,
                                            char *lds_tile, int wave, int lane) {
-  static_assert((R / 8) % W == 0, "tile rows must split evenly over the waves");
+  static_assert(BK == 64 || BK == 32, "BK 32 or 64");
+  constexpr int kInstr = R * BK / 512;
+  static_assert(kInstr % W == 0, "tile rows must split evenly over the waves");
 #pragma unroll
-  for (int i = 0; i < R / 8 / W; ++i) {
-    const int q0 = (i * W + wave) * 64;  // first 16-B chunk this wave-instruction fills
+  for (int i = 0; i < kInstr / W; ++i) {
+    const int q0 = (i * W + wave) * 64;  // first 16-B LDS slot this wave-instruction fills
     const int q = q0 + lane;
-    const int r = q >> 3, c = q & 7;
+    const int lr = q >> 3, sl = (q & 7) ^ (lr & 7);
+    const int r = BK == 64 ? lr : 2 * lr + (sl >> 2);
+    const int c = BK == 64 ? sl : (sl & 3);
     int64_t gr = row0 + r;
     gr = gr < rows ? gr : rows - 1;
-    const char *src = base + (gr * ld + k0 + ((c ^ (r & 7)) << 3)) * 2;
+    const char *src = base + (gr * ld + k0 + (c << 3)) * 2;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                      (lds_void *)(lds_tile + q0 * 16), 16, 0, 0);
   }
 }
 
-template <typename T>
+template <int BK, typename T>
 __device__ __forceinline__ void read_frag(const char *lds_tile, int row, int chunk, T &f) {
-  f = *reinterpret_cast<const T *>(lds_tile + row * 128 + ((chunk ^ (row & 7)) << 4));
+  if constexpr (BK == 64) {
+    f = *reinterpret_cast<const T *>(lds_tile + row * 128 + ((chunk ^ (row & 7)) << 4));
+  } else {
+    const int lr = row >> 1;
+    f = *reinterpret_cast<const T *>(lds_tile + lr * 128 + ((((row & 1) << 2) + chunk) ^ (lr & 7)) * 16);
+  }
 }
 
 // Tile geometry: BM x BN block tile, WGM x WGN waves, each owning a TM x TN = (BM / WGM) x
 // (BN / WGN) sub-tile of (TM / 16) x (TN / 16) MFMA blocks; STAGES operand buffers in LDS.
-template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_> struct Tile {
-  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, STAGES = STAGES_;
+template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_, int BK_ = 64> struct Tile {
+  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, STAGES = STAGES_, BK = BK_;
   static constexpr int kWaves = WGM * WGN, kThreads = kWaves * 64;
   static constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
-  static constexpr int kStageBytes = (BM + BN) * kGBK * 2;
-  static constexpr int kLoadsPerTile = (BM + BN) / 8 / kWaves;  // glds per thread per K-step
+  static constexpr int kStageBytes = (BM + BN) * BK * 2;
+  static constexpr int kLoadsPerTile = (BM + BN) * BK / 512 / kWaves;  // glds per thread per K-step
   static constexpr int kOpBytes = STAGES * kStageBytes;
   // epilogue: the fp32 LDS image (reusing the operand buffers) holds the whole tile, or passes of
   // every wave's next TM / kEpPasses rows (so half the accumulators die after the first pass)
@@ -163,20 +175,86 @@ template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_> struct Tile {
   static_assert(MI >= 1 && NI >= 1 && TM % 16 == 0 && TN % 16 == 0, "bad wave tile");
 };
 
+// first tile of XCD x when `total` tiles are split XCD-major over the 8 XCDs (bijective for any
+// count), and how many it gets
+__device__ __forceinline__ int xcd_first(int total, int x) {
+  const int q8 = total / 8, r8 = total % 8;
+  return x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+}
+__device__ __forceinline__ int xcd_count(int total, int x) { return total / 8 + (x < total % 8 ? 1 : 0); }
+
+// s_waitcnt vmcnt(n * L) for a run-time n <= NMAX (the immediate must be a constant)
+template <int L, int NMAX> __device__ __forceinline__ void wait_vmcnt_tiles(int n) {
+  static_assert(NMAX * L <= 63, "vmcnt range");
+  if (NMAX >= 3 && n >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * L) : "memory");
+  else if (NMAX >= 2 && n == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * L) : "memory");
+  else if (NMAX >= 1 && n == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// One K-step: issue the DMA of operand tile `next` into `wr` (when `issue`) and run the MFMAs of
+// the current one from `rd`.  The two LDS buffers are restrict parameters, so after inlining the
+// fragment reads and the LDS-DMA writes carry disjoint alias scopes and the compiler's wait
+// insertion does not drain the in-flight DMA before the first fragment read.  A K-step is BK / 32
+// MFMA sub-steps of 32; within it the (MI / 2) pairs of A fragments are walked as groups of
+// 2 x NI MFMAs, the fragments of group q + 1 read from LDS while the MFMAs of group q run (two
+// fragment register sets; B fragments re-read per sub-step).
+template <typename T, typename TL, typename Stage>
+__device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__restrict__ wr, bool issue,
+                                          const Stage &stage, int next, int wave, int lane,
+                                          f4 (&acc)[TL::MI][TL::NI]) {
+  constexpr int MI = TL::MI, NI = TL::NI, BK = TL::BK;
+  using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
+  const int wm = wave / TL::WGN, wn = wave % TL::WGN;
+  if (issue) stage(next, wr);
+  const char *ta = rd;
+  const char *tb = rd + TL::BM * BK * 2;
+  constexpr int GP = MI / 2, NS = BK / 32, NG = NS * GP;
+  static_assert(MI % 2 == 0, "A fragments are walked in pairs");
+  V8 fa[2][2], fb[2][NI];
+  auto load_b = [&](V8 *f, int s) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) read_frag<BK>(tb, wn * TL::TN + j * 16 + (lane & 15), s * 4 + (lane >> 4), f[j]);
+  };
+  auto load_a = [&](V8 *f, int s, int p) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+      read_frag<BK>(ta, wm * TL::TM + (2 * p + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), f[ii]);
+  };
+  load_b(fb[0], 0);
+  load_a(fa[0], 0, 0);
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const int s = q / GP, p = q % GP;
+    if (q + 1 < NG) {
+      const int s1 = (q + 1) / GP, p1 = (q + 1) % GP;
+      if (s1 != s) load_b(fb[s1 & 1], s1);
+      load_a(fa[(q + 1) & 1], s1, p1);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        f4 &c = acc[2 * p + ii][j];
+        if constexpr (std::is_same<T, _Float16>::value)
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
+        else
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
+      }
+  }
+}
+
+// One output tile: main loop + fused epilogue.  `wg` is the tile's linear index (n fastest within
+// an A panel, then m, then batch); smem holds the operand stages and, after the main loop, the
+// epilogue image.
 template <typename T, typename OutT, int EPI, typename TL>
-__global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
+__device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, int wg) {
   constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
   constexpr bool kGrad = EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD;  // aux read + column sums
   constexpr bool kBiasFwd = EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU || EPI == PHC_EPI_BIAS_RELU;
-  using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][A BM rows | B BN rows]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
-
-  // XCD-major renumbering (bijective for any grid size), then n fastest within an A panel
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int tn = wg % g.tiles_n;
   const int tm = (wg / g.tiles_n) % g.tiles_m;
   const int bt = wg / (g.tiles_n * g.tiles_m);
@@ -191,76 +269,36 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
-  auto stage = [&](int kt, int buf) {
-    char *st = smem + buf * TL::kStageBytes;
-    stage_tile<BM, TL::kWaves>(A, g.lda, m0, g.m, kt * kGBK, st, wave, lane);
-    stage_tile<BN, TL::kWaves>(B, g.ldb, n0, g.n, kt * kGBK, st + BM * 128, wave, lane);
+  const int kt_n = g.k / TL::BK;
+  auto stage = [&](int kt, char *st) {
+    stage_tile<BM, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
+    stage_tile<BN, TL::kWaves, TL::BK>(B, g.ldb, n0, g.n, kt * TL::BK, st + BM * TL::BK * 2, wave, lane);
   };
-  // one K-step (64) = 2 MFMA sub-steps of 32; within it the (MI / 2) pairs of A fragments
-  // are walked as groups of 2 x NI MFMAs, the fragments of group q + 1 read from LDS while the
-  // MFMAs of group q run (two fragment register sets; B fragments re-read per sub-step)
-  auto compute = [&](int buf) {
-    const char *ta = smem + buf * TL::kStageBytes;
-    const char *tb = ta + BM * 128;
-    constexpr int GP = MI / 2, NG = 2 * GP;
-    static_assert(MI % 2 == 0, "A fragments are walked in pairs");
-    V8 fa[2][2], fb[2][NI];
-    auto load_b = [&](V8 *f, int s) {
-#pragma unroll
-      for (int j = 0; j < NI; ++j) read_frag(tb, wn * TL::TN + j * 16 + (lane & 15), s * 4 + (lane >> 4), f[j]);
-    };
-    auto load_a = [&](V8 *f, int s, int p) {
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-        read_frag(ta, wm * TL::TM + (2 * p + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), f[ii]);
-    };
-    load_b(fb[0], 0);
-    load_a(fa[0], 0, 0);
-#pragma unroll
-    for (int q = 0; q < NG; ++q) {
-      const int s = q / GP, p = q % GP;
-      if (q + 1 < NG) {
-        const int s1 = (q + 1) / GP, p1 = (q + 1) % GP;
-        if (s1 != s) load_b(fb[s1 & 1], s1);
-        load_a(fa[(q + 1) & 1], s1, p1);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          f4 &c = acc[2 * p + ii][j];
-          if constexpr (std::is_same<T, _Float16>::value)
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
-          else
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
-        }
-    }
-  };
-
-  const int kt_n = g.k / kGBK;
   if constexpr (TL::STAGES == 2) {
-    stage(0, 0);
+    stage(0, smem);
     for (int kt = 0; kt < kt_n; ++kt) {
       __syncthreads();  // tile kt landed (vmcnt(0) + barrier); buffer (kt+1)&1 is no longer read
-      if (kt + 1 < kt_n) stage(kt + 1, (kt + 1) & 1);
-      compute(kt & 1);
+      gemm_step<T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt + 1 < kt_n,
+                       stage, kt + 1, wave, lane, acc);
     }
   } else {
-    static_assert(TL::STAGES == 3, "2 or 3 stages");
-    stage(0, 0);
-    if (kt_n > 1) stage(1, 1);
-    int buf = 0;
+    constexpr int S = TL::STAGES;
+#pragma unroll
+    for (int i = 0; i < S - 1; ++i)
+      if (i < kt_n) stage(i, smem + i * TL::kStageBytes);
+    int rd = 0;
     for (int kt = 0; kt < kt_n; ++kt) {
-      // this thread's part of tile kt has landed (tile kt + 1 may stay in flight); after the
-      // barrier every thread's part has, and every wave is done with tile kt - 1's buffer
-      if (kt + 1 < kt_n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TL::kLoadsPerTile) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // this thread's part of tile kt has landed (the younger tiles may stay in flight); after the
+      // barrier every thread's part has, and every wave is done with tile kt - 1's buffer, which
+      // the DMA of tile kt + S - 1 refills
+      const int younger = kt_n - 1 - kt < S - 2 ? kt_n - 1 - kt : S - 2;
+      wait_vmcnt_tiles<TL::kLoadsPerTile, S - 2>(younger);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (kt + 2 < kt_n) stage(kt + 2, buf == 0 ? 2 : buf - 1);
-      compute(buf);
-      buf = buf == 2 ? 0 : buf + 1;
+      const int wr = rd == 0 ? S - 1 : rd - 1;
+      gemm_step<T, TL>(smem + rd * TL::kStageBytes, smem + wr * TL::kStageBytes, kt + S - 1 < kt_n, stage,
+                       kt + S - 1, wave, lane, acc);
+      rd = rd == S - 1 ? 0 : rd + 1;
     }
   }
 
@@ -470,6 +508,14 @@ __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
         if (gcol + q < g.n) pr[gcol + q] = o[q];
     }
   }
+}
+
+// one tile per workgroup, XCD-major renumbering (bijective for any grid size)
+template <typename T, typename OutT, int EPI, typename TL>
+__global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][A BM rows | B BN rows]
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  twin_gemm_tile<T, OutT, EPI, TL>(g, smem, xcd_first(nwg, orig % 8) + orig / 8);
 }
 
 // ------------------------------------------------------------------ weight gradients (R21) --
@@ -763,7 +809,7 @@ static int gemm_config(int64_t m, int n, int batch) {
 
 static void gemm_tile_dims(int cfg, int *bm, int *bn) {
   *bm = cfg == kCfg128 ? 128 : 256;
-  *bn = cfg == kCfg256sq ? 256 : 128;
+  *bn = cfg == kCfg128 ? 128 : 256;
 }
 
 static phc_kernel_timer *g_gemm_timer = nullptr;  // bench.py measurement aid (phc_gemm_set_timer)
@@ -878,6 +924,7 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   PHC_REQUIRE(d->aux_dtype == PHC_DT_F32 || d->aux_dtype == d->dtype, "twin_gemm: aux must be f32 or the operand type");
   PHC_REQUIRE(!bias_grad || (grad_epi && workspace),
               "twin_gemm: bias_grad needs the SILU_GRAD / RELU_GRAD epilogue and a workspace");
+  hipStream_t st = as_stream(stream);
   const int cfg = gemm_config(d->m, d->n, d->batch);
   int bm, bn;
   gemm_tile_dims(cfg, &bm, &bn);
@@ -909,7 +956,6 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   g.tiles_n = (int)tiles_n;
   static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
   g.discard = discard ? 1 : 0;
-  hipStream_t st = as_stream(stream);
   g_ev0 = g_ev1 = nullptr;
   if (g_gemm_timer && g_gemm_timer->used < (int32_t)g_gemm_timer->start.size()) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

@@ -22,9 +22,15 @@ DIMS = [960, 2048, 1536, 1024, 1024, 512, 512]  # padded input width, then the s
 REPS = int(os.environ.get("REPS", "20"))
 
 
-def timeit(fn):
+SUMS = []
+
+
+def timeit(fn, out=None):
     for _ in range(3):
         fn()
+    if out is not None:  # checksum of one output, to compare library builds / tile configurations
+        torch.cuda.synchronize()
+        SUMS.append(float(out.double().sum()))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     s.record()
@@ -50,7 +56,7 @@ def main():
     z = torch.empty((2, M, DIMS[1]), dtype=dt, device=dev)
     pre = torch.empty((M, 2 * DIMS[1]), dtype=dt, device=dev)
     us = timeit(lambda: N.twin_gemm(x, w0, N.EPI_BIAS_SILU, z, (2, DIMS[1]), bias=b0, aux=pre,
-                                    aux_layout=N.SPLIT, out_layout=N.GROUPED))
+                                    aux_layout=N.SPLIT, out_layout=N.GROUPED), z)
     rows.append(("fwd L1", M, 2 * DIMS[1], DIMS[0], 1, us))
     for l in range(2, 7):
         k, n = DIMS[l - 1], DIMS[l]
@@ -60,10 +66,10 @@ def main():
         if l < 6:
             o = torch.empty((2, M, n), dtype=dt, device=dev)
             p = torch.empty((2, M, n), dtype=dt, device=dev)
-            us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS_SILU, o, (2, n), bias=b, aux=p))
+            us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS_SILU, o, (2, n), bias=b, aux=p), o)
         else:
             o = torch.empty((2, M, n), dtype=torch.float32, device=dev)
-            us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS, o, (2, n), bias=b))
+            us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS, o, (2, n), bias=b), o)
         rows.append((f"fwd L{l}", M, n, k, 2, us))
     # backward input gradients L6..L2: g [2, M, n_out] x W^T -> [2, M, n_in], SiLU' epilogue
     for l in range(6, 1, -1):
@@ -74,15 +80,15 @@ def main():
         db = torch.empty(2 * nin, device=dev)
         if l > 2:
             o = torch.empty((2, M, nin), dtype=dt, device=dev)
-            us = timeit(lambda: N.twin_gemm(gg, wt, N.EPI_SILU_GRAD, o, (2, nin), aux=p, bias_grad=db))
+            us = timeit(lambda: N.twin_gemm(gg, wt, N.EPI_SILU_GRAD, o, (2, nin), aux=p, bias_grad=db), o)
         else:
             o = torch.empty((M, 2 * nin), dtype=dt, device=dev)
             p = rnd(M, 2 * nin)
             us = timeit(lambda: N.twin_gemm(gg, wt, N.EPI_SILU_GRAD, o, (2, nin), aux=p, aux_layout=N.SPLIT,
-                                            out_layout=N.SPLIT, bias_grad=db))
+                                            out_layout=N.SPLIT, bias_grad=db), o)
         rows.append((f"dgrad L{l}", M, nin, nout, 2, us))
     # weight gradients (hipBLASLt, fp32 out): dW[b] = g[b]^T z[b]
-    for l in range(6, 0, -1):
+    for l in (range(6, 0, -1) if os.environ.get("WGRAD", "0") == "1" else []):
         nout, nin = DIMS[l], DIMS[l - 1]
         bt = 1 if l == 1 else 2
         gg = rnd(bt, M, nout * (2 if l == 1 else 1))
@@ -94,6 +100,7 @@ def main():
         total_us += us
         total_fl += fl
         print(f"{name:10s} m={m:6d} n={n:5d} k={k:5d} b={b} {us:8.1f} us {fl / us / 1e6:7.0f} TF/s", flush=True)
+    print("checksums", " ".join(f"{v:.6e}" for v in SUMS))
     print(f"TOTAL {total_us:.1f} us {total_fl / total_us / 1e6:.0f} TF/s  lib={os.environ.get('PHC_HIP_LIB', 'default')}")
 
 
