@@ -35,10 +35,22 @@
 namespace phc {
 
 constexpr int kGBK = 64;
+// experiment knobs (compile-time): MFMA priority (off), the B operand's DMA issued PHC_GEMM_SPLIT_DMA
+// eighths of a K-step after the A operand's (0 = together)
+#ifndef PHC_GEMM_PRIO
+#define PHC_GEMM_PRIO 0
+#endif
+#ifndef PHC_WGRAD_SPLIT
+#define PHC_WGRAD_SPLIT 2
+#endif
+#ifndef PHC_GEMM_SPLIT_DMA
+#define PHC_GEMM_SPLIT_DMA 2
+#endif
 using f4 = __attribute__((ext_vector_type(4))) float;
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using b8 = __attribute__((ext_vector_type(8))) __bf16;
 typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
 struct GemmArgs {
   const char *a, *b;
@@ -55,6 +67,7 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   int discard;
   int aux_half;  // aux in the operand type T instead of fp32
+  int nt;        // non-temporal epilogue traffic: 1 = out stores, 2 = aux stores, 4 = aux loads
 };
 
 // 4 consecutive aux values (fp32, or the operand type T when g.aux_half) at element offset off
@@ -75,7 +88,10 @@ template <typename T> __device__ __forceinline__ void aux_store4(const GemmArgs 
     const T h[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
     uint2 raw;
     __builtin_memcpy(&raw, h, sizeof(raw));
-    *reinterpret_cast<uint2 *>(static_cast<T *>(g.aux) + off) = raw;
+    if (g.nt & 2)
+      __builtin_nontemporal_store(__builtin_bit_cast(u2v, raw), reinterpret_cast<u2v *>(static_cast<T *>(g.aux) + off));
+    else
+      *reinterpret_cast<uint2 *>(static_cast<T *>(g.aux) + off) = raw;
   } else {
     *reinterpret_cast<float4 *>(static_cast<float *>(g.aux) + off) = float4{v[0], v[1], v[2], v[3]};
   }
@@ -110,14 +126,17 @@ template <typename OutT> __device__ __forceinline__ void gemm_store(void *p, int
   static_cast<OutT *>(p)[off] = (OutT)v;
 }
 
-template <typename OutT> __device__ __forceinline__ void gemm_store4(void *p, int64_t off, const float v[4]) {
+template <typename OutT> __device__ __forceinline__ void gemm_store4(void *p, int64_t off, const float v[4], bool nt) {
   if constexpr (sizeof(OutT) == 4) {
     *reinterpret_cast<float4 *>(static_cast<float *>(p) + off) = float4{v[0], v[1], v[2], v[3]};
   } else {
     OutT h[4] = {(OutT)v[0], (OutT)v[1], (OutT)v[2], (OutT)v[3]};
     uint2 raw;
     __builtin_memcpy(&raw, h, sizeof(raw));
-    *reinterpret_cast<uint2 *>(static_cast<OutT *>(p) + off) = raw;
+    if (nt)
+      __builtin_nontemporal_store(__builtin_bit_cast(u2v, raw), reinterpret_cast<u2v *>(static_cast<OutT *>(p) + off));
+    else
+      *reinterpret_cast<uint2 *>(static_cast<OutT *>(p) + off) = raw;
   }
 }
 
@@ -206,10 +225,11 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
   constexpr int MI = TL::MI, NI = TL::NI, BK = TL::BK;
   using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
-  if (issue) stage(next, wr);
+  constexpr int GP = MI / 2, NS = BK / 32, NG = NS * GP;
+  if (!PHC_GEMM_SPLIT_DMA && issue) stage(next, wr, 3);
+  if (PHC_GEMM_SPLIT_DMA && issue) stage(next, wr, 1);
   const char *ta = rd;
   const char *tb = rd + TL::BM * BK * 2;
-  constexpr int GP = MI / 2, NS = BK / 32, NG = NS * GP;
   static_assert(MI % 2 == 0, "A fragments are walked in pairs");
   V8 fa[2][2], fb[2][NI];
   auto load_b = [&](V8 *f, int s) {
@@ -231,7 +251,9 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
       if (s1 != s) load_b(fb[s1 & 1], s1);
       load_a(fa[(q + 1) & 1], s1, p1);
     }
+    if (PHC_GEMM_SPLIT_DMA && issue && q == (PHC_GEMM_SPLIT_DMA * NG / 8 < NG ? PHC_GEMM_SPLIT_DMA * NG / 8 : NG - 1)) stage(next, wr, 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
+    if (PHC_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
@@ -242,6 +264,10 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
         else
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
       }
+    if (PHC_GEMM_PRIO) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+    }
   }
 }
 
@@ -270,9 +296,9 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
     for (int j = 0; j < NI; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
   const int kt_n = g.k / TL::BK;
-  auto stage = [&](int kt, char *st) {
-    stage_tile<BM, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
-    stage_tile<BN, TL::kWaves, TL::BK>(B, g.ldb, n0, g.n, kt * TL::BK, st + BM * TL::BK * 2, wave, lane);
+  auto stage = [&](int kt, char *st, int parts = 3) {  // parts: 1 = A tile, 2 = B tile
+    if (parts & 1) stage_tile<BM, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
+    if (parts & 2) stage_tile<BN, TL::kWaves, TL::BK>(B, g.ldb, n0, g.n, kt * TL::BK, st + BM * TL::BK * 2, wave, lane);
   };
   if constexpr (TL::STAGES == 2) {
     stage(0, smem);
@@ -372,7 +398,9 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int64_t row = m0 + trow(pass, b * U + u);
-            raw[b & 1][u] = *reinterpret_cast<const uint2 *>(static_cast<const T *>(g.aux) + ab + row * as);
+            const T *src = static_cast<const T *>(g.aux) + ab + row * as;
+            raw[b & 1][u] = (g.nt & 4) ? __builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const u2v *>(src)))
+                                       : *reinterpret_cast<const uint2 *>(src);
           }
         }
       };
@@ -428,7 +456,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
               for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
             }
           }
-          gemm_store4<OutT>(g.out, ob + row * os, v);
+          gemm_store4<OutT>(g.out, ob + row * os, v, g.nt & 1);
         }
       }
       continue;
@@ -470,7 +498,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
         if constexpr (EPI == PHC_EPI_BIAS_SILU) {
           if (g.aux) aux_store4<T>(g, gemm_twin_off(g, g.aux_layout, row, lc), a);
         }
-        gemm_store4<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, lc), v);
+        gemm_store4<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, lc), v, g.nt & 1);
       } else {
         for (int q = 0; q < 4; ++q) {
           if (gcol + q >= g.n) break;
@@ -593,13 +621,11 @@ __device__ __forceinline__ void wgrad_step(const char *__restrict__ rd, char *__
   constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
   using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
-  if (issue) {
-    stage_tile_k<BM, TL::kWaves>(A, lda, row0, m0, am, wr, wave, lane);
-    stage_tile_k<BN, TL::kWaves>(B, ldb, row0, n0, bn, wr + BM * 128, wave, lane);
-  }
+  constexpr int GP = MI / 2, NG = 2 * GP;
+  if (issue) stage_tile_k<BM, TL::kWaves>(A, lda, row0, m0, am, wr, wave, lane);
+  if (!PHC_WGRAD_SPLIT && issue) stage_tile_k<BN, TL::kWaves>(B, ldb, row0, n0, bn, wr + BM * 128, wave, lane);
   const char *ta = rd;
   const char *tb = rd + BM * 128;
-  constexpr int GP = MI / 2, NG = 2 * GP;
   static_assert(MI % 2 == 0, "A fragments are walked in pairs");
   V8 fa[2][2], fb[2][NI];
   auto load_b = [&](V8 *f, int s) {
@@ -620,6 +646,8 @@ __device__ __forceinline__ void wgrad_step(const char *__restrict__ rd, char *__
       if (s1 != s) load_b(fb[s1 & 1], s1);
       load_a(fa[(q + 1) & 1], s1, p1);
     }
+    if (PHC_WGRAD_SPLIT && issue && q == (PHC_WGRAD_SPLIT * NG / 8 < NG ? PHC_WGRAD_SPLIT * NG / 8 : NG - 1))
+      stage_tile_k<BN, TL::kWaves>(B, ldb, row0, n0, bn, wr + BM * 128, wave, lane);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii)
@@ -956,6 +984,21 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   g.tiles_n = (int)tiles_n;
   static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
   g.discard = discard ? 1 : 0;
+  // Non-temporal epilogue traffic: an output of a whole PPO minibatch (tens to hundreds of MB,
+  // far past the 4 MB per-XCD L2) streams out without evicting the operand panels the other CUs
+  // are still re-reading; the pre-activation (written by the forward, read back once by the backward) always does.  Small
+  // outputs (the rollout's 4096-row layers) stay cached for the next layer.  Measured: -8 % on a
+  // minibatch's forward + input-gradient GEMMs (profiles/r02_gemm_experiments.txt).
+  static const int64_t nt_out_min = [] {
+    const char *e = getenv("PHC_GEMM_NT_OUT_MB");  // tuning aid
+    return (int64_t)(e ? atof(e) * 1048576.0 : 64.0 * 1048576.0);
+  }();
+  static const int nt_aux = [] {
+    const char *e = getenv("PHC_GEMM_NT_AUX");  // tuning aid: bit 1 = aux stores, bit 2 = aux loads
+    return e ? atoi(e) : 3;
+  }();
+  const int64_t out_bytes = d->m * (int64_t)d->batch * d->n * (d->out_dtype == PHC_DT_F32 ? 4 : 2);
+  g.nt = (out_bytes >= nt_out_min ? 1 : 0) | ((nt_aux & 1) ? 2 : 0) | ((nt_aux & 2) ? 4 : 0);
   g_ev0 = g_ev1 = nullptr;
   if (g_gemm_timer && g_gemm_timer->used < (int32_t)g_gemm_timer->start.size()) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

@@ -95,6 +95,24 @@ def main():
         zz = rnd(bt, M, nin)
         us = timeit(lambda: torch.bmm(gg.transpose(1, 2), zz, out_dtype=torch.float32))
         rows.append((f"wgrad L{l}", nout * (2 if l == 1 else 1), nin, M, bt, us))
+    if os.environ.get("WGRAD", "2") == "2":  # the grouped weight-gradient launch of layers 5..1
+        probs = []
+        for l in range(5, 0, -1):
+            nout, nin = DIMS[l], DIMS[l - 1]
+            if l == 1:
+                gg = rnd(M, 2 * nout, scale=0.1)
+                zz = rnd(M, nin)
+                d = [torch.zeros((nout, 934), device=dev) for _ in range(2)]
+                probs.append((gg, zz, d, nout, 934))
+            else:
+                gg = rnd(2, M, nout, scale=0.1)
+                zz = rnd(2, M, nin)
+                d = [torch.zeros((nout, nin), device=dev) for _ in range(2)]
+                probs.append((gg, zz, d, nout, nin))
+        us = timeit(lambda: N.weight_grad_group(probs, accumulate=False), probs[0][2][0])
+        fl = sum(2.0 * M * p_[0].shape[-1] * p_[1].shape[-1] * (2 if p_[0].dim() == 3 else 1) for p_ in probs)
+        rows.append(("wgrad grp", 1, 1, 1, 1, us))
+        total_fl += fl - 2.0
     for name, m, n, k, b, us in rows:
         fl = 2.0 * m * n * k * b
         total_us += us
