@@ -268,7 +268,8 @@ typedef struct phc_gemm_desc {
   int32_t twin_groups, twin_cols;
   int32_t aux_dtype; /* PHC_DT_F32, or dtype: the pre-activation kept in the operand type, as
                         torch.autocast's Linear output and SiLU's saved input are */
-  int32_t reserved;
+  int32_t max_workgroups; /* 0: one workgroup per output tile; else at most this many
+                             workgroups, each looping over tiles (persistent) */
 } phc_gemm_desc;
 size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_t n);
 int phc_twin_gemm(const phc_gemm_desc *desc, float *bias_grad, void *workspace, void *stream);

@@ -43,6 +43,9 @@ constexpr int kGBK = 64;
 #ifndef PHC_WGRAD_SPLIT
 #define PHC_WGRAD_SPLIT 2
 #endif
+#ifndef PHC_GEMM_SPLIT_A
+#define PHC_GEMM_SPLIT_A 0
+#endif
 #ifndef PHC_GEMM_SPLIT_DMA
 #define PHC_GEMM_SPLIT_DMA 2
 #endif
@@ -115,11 +118,19 @@ __device__ __forceinline__ float gemm_sigmoid(float a) {
 __device__ __forceinline__ float gemm_silu(float a) { return a * gemm_sigmoid(a); }
 
 // workgroup barrier for the epilogue's LDS hand-offs: waits for this wave's LDS operations only
-// (lgkmcnt), not for its global stores (__syncthreads' fence waits vmcnt(0)), so the stores of one
+// (lgkmcnt), not for its global stores (vmcnt), so the stores of one
 // image pass drain while the next pass runs, and past the end of the block while the CU's next
 // tile starts its main loop
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// workgroup barrier after which every wave's LDS-DMA (global_load_lds) writes have landed: each
+// wave drains its own DMA (vmcnt), then the barrier.  __syncthreads() is NOT enough: its fence
+// does not count LDS-DMA, and the compiler's own vmcnt for the DMA may land after the barrier
+// (seen in the persistent tile loop: waves read operand tiles other waves' DMA had not written).
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <typename OutT> __device__ __forceinline__ void gemm_store(void *p, int64_t off, float v) {
@@ -227,7 +238,8 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
   constexpr int GP = MI / 2, NS = BK / 32, NG = NS * GP;
   if (!PHC_GEMM_SPLIT_DMA && issue) stage(next, wr, 3);
-  if (PHC_GEMM_SPLIT_DMA && issue) stage(next, wr, 1);
+  if (PHC_GEMM_SPLIT_DMA && !PHC_GEMM_SPLIT_A && issue) stage(next, wr, 1);
+  if (PHC_GEMM_SPLIT_A && issue) stage(next, wr, 4);
   const char *ta = rd;
   const char *tb = rd + TL::BM * BK * 2;
   static_assert(MI % 2 == 0, "A fragments are walked in pairs");
@@ -251,6 +263,7 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
       if (s1 != s) load_b(fb[s1 & 1], s1);
       load_a(fa[(q + 1) & 1], s1, p1);
     }
+    if (PHC_GEMM_SPLIT_A && issue && q == PHC_GEMM_SPLIT_A * NG / 8) stage(next, wr, 8);
     if (PHC_GEMM_SPLIT_DMA && issue && q == (PHC_GEMM_SPLIT_DMA * NG / 8 < NG ? PHC_GEMM_SPLIT_DMA * NG / 8 : NG - 1)) stage(next, wr, 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
     if (PHC_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
@@ -296,14 +309,17 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
     for (int j = 0; j < NI; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
   const int kt_n = g.k / TL::BK;
-  auto stage = [&](int kt, char *st, int parts = 3) {  // parts: 1 = A tile, 2 = B tile
+  auto stage = [&](int kt, char *st, int parts = 3) {  // parts: 1 = A tile, 2 = B tile, 4 / 8 = A halves
     if (parts & 1) stage_tile<BM, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
+    if (parts & 4) stage_tile<BM / 2, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
+    if (parts & 8)
+      stage_tile<BM / 2, TL::kWaves, TL::BK>(A, g.lda, m0 + BM / 2, g.m, kt * TL::BK, st + BM / 2 * TL::BK * 2, wave, lane);
     if (parts & 2) stage_tile<BN, TL::kWaves, TL::BK>(B, g.ldb, n0, g.n, kt * TL::BK, st + BM * TL::BK * 2, wave, lane);
   };
   if constexpr (TL::STAGES == 2) {
     stage(0, smem);
     for (int kt = 0; kt < kt_n; ++kt) {
-      __syncthreads();  // tile kt landed (vmcnt(0) + barrier); buffer (kt+1)&1 is no longer read
+      dma_barrier();  // tile kt landed; buffer (kt+1)&1 is no longer read
       gemm_step<T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt + 1 < kt_n,
                        stage, kt + 1, wave, lane, acc);
     }
@@ -538,12 +554,25 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   }
 }
 
-// one tile per workgroup, XCD-major renumbering (bijective for any grid size)
+// One tile per workgroup, XCD-major renumbering (bijective for any grid size); or, with fewer
+// workgroups than tiles (phc_gemm_desc.max_workgroups), a persistent loop: step s hands tiles
+// [s * nwg, (s + 1) * nwg) out XCD-major, so the workgroups sharing an XCD's L2 walk neighbouring
+// tiles of the same A panels at every step.
 template <typename T, typename OutT, int EPI, typename TL>
 __global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][A BM rows | B BN rows]
   const int nwg = gridDim.x, orig = blockIdx.x;
-  twin_gemm_tile<T, OutT, EPI, TL>(g, smem, xcd_first(nwg, orig % 8) + orig / 8);
+  const int total = g.tiles_m * g.tiles_n * g.batch;
+  if (nwg >= total) {
+    twin_gemm_tile<T, OutT, EPI, TL>(g, smem, xcd_first(nwg, orig % 8) + orig / 8);
+    return;
+  }
+  const int x = orig % 8, l = orig / 8;
+  for (int base = 0; base < total; base += nwg) {
+    const int cnt = total - base < nwg ? total - base : nwg;
+    if (l < xcd_count(cnt, x)) twin_gemm_tile<T, OutT, EPI, TL>(g, smem, base + xcd_first(cnt, x) + l);
+    lds_barrier();  // the epilogue image is read out before the next tile's operands land
+  }
 }
 
 // ------------------------------------------------------------------ weight gradients (R21) --
@@ -691,7 +720,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad(WgradArgs g) {
   stage_tile_k<BM, TL::kWaves>(A, g.ldg, r0, m0, g.m, smem, wave, lane);
   stage_tile_k<BN, TL::kWaves>(B, g.ldz, r0, n0, g.n, smem + BM * 128, wave, lane);
   for (int kt = 0; kt < kt_n; ++kt) {
-    __syncthreads();  // tile kt landed; buffer (kt + 1) & 1 is no longer read
+    dma_barrier();  // tile kt landed; buffer (kt + 1) & 1 is no longer read
     char *cur = smem + (kt & 1) * TL::kStageBytes;
     char *nxt = smem + ((kt + 1) & 1) * TL::kStageBytes;
     wgrad_step<T, TL>(cur, nxt, kt + 1 < kt_n, A, g.ldg, g.m, B, g.ldz, g.n, r0 + (int64_t)(kt + 1) * kGBK, m0, n0,
@@ -777,7 +806,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad_group(WgradGroupArgs ga)
   stage_tile_k<BM, TL::kWaves>(A, lda, 0, m0, am, smem, wave, lane);
   stage_tile_k<BN, TL::kWaves>(B, ldb, 0, n0, bn, smem + BM * 128, wave, lane);
   for (int kt = 0; kt < kt_n; ++kt) {
-    __syncthreads();
+    dma_barrier();
     char *cur = smem + (kt & 1) * TL::kStageBytes;
     char *nxt = smem + ((kt + 1) & 1) * TL::kStageBytes;
     wgrad_step<T, TL>(cur, nxt, kt + 1 < kt_n, A, lda, am, B, ldb, bn, (int64_t)(kt + 1) * kGBK, m0, n0, wave,
@@ -958,8 +987,10 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   gemm_tile_dims(cfg, &bm, &bn);
   const int64_t tiles_m = (d->m + bm - 1) / bm;
   const int64_t tiles_n = (d->n + bn - 1) / bn;
-  const int64_t blocks = tiles_m * tiles_n * d->batch;
+  int64_t blocks = tiles_m * tiles_n * d->batch;
   PHC_REQUIRE(blocks < (1ll << 31), "twin_gemm: grid too large");
+  PHC_REQUIRE(d->max_workgroups >= 0, "twin_gemm: max_workgroups must be >= 0");
+  if (d->max_workgroups > 0 && d->max_workgroups < blocks) blocks = d->max_workgroups;
   GemmArgs g{};
   g.a = static_cast<const char *>(d->a);
   g.b = static_cast<const char *>(d->b);

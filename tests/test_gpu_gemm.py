@@ -253,3 +253,33 @@ def test_rejects_unpadded_k():
     out = torch.empty((64, 64), device=DEV)
     with pytest.raises(RuntimeError, match="multiple of 64"):
         N.twin_gemm(a, b, N.EPI_STORE, out, (1, 64))
+
+
+@pytest.mark.parametrize("epi", ["bias_silu", "silu_grad"])
+@pytest.mark.parametrize("max_wg", [7, 100, 256])
+def test_persistent_grid_matches_one_tile_per_workgroup(epi, max_wg):
+    """max_workgroups: a persistent grid looping over the tiles gives the one-tile-per-workgroup
+    result bit for bit (256 x 256 tiles, several tiles per workgroup, a ragged last step).  This
+    is the case that exposed LDS-DMA reads racing other waves' DMA when the K-step barrier relied
+    on __syncthreads (phc_gemm.hip dma_barrier)."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    m, n, k = 8192 + 77, 512, 1024
+    a = torch.randn((2, m, k), device=DEV, generator=g).half()
+    w = (torch.randn((2, n, k), device=DEV, generator=g) / k ** 0.5).half()
+    bias = torch.randn(2 * n, device=DEV, generator=g)
+    outs = []
+    for mwg in (0, max_wg):
+        out = torch.empty((2, m, n), dtype=torch.float16, device=DEV)
+        if epi == "bias_silu":
+            aux = torch.empty((2, m, n), dtype=torch.float16, device=DEV)
+            N.twin_gemm(a, w, N.EPI_BIAS_SILU, out, (2, n), bias=bias, aux=aux, max_workgroups=mwg)
+            outs.append((out, aux))
+        else:
+            aux = (torch.randn((2, m, n), device=DEV, generator=torch.Generator(device=DEV).manual_seed(5)) * 2).half()
+            db = torch.empty(2 * n, device=DEV)
+            N.twin_gemm(a, w, N.EPI_SILU_GRAD, out, (2, n), bias=bias, aux=aux, bias_grad=db, max_workgroups=mwg)
+            outs.append((out, db))
+    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=0, atol=0)
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=0, atol=0)

@@ -20,6 +20,7 @@ dt = torch.float16
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 DIMS = [960, 2048, 1536, 1024, 1024, 512, 512]  # padded input width, then the six layer widths
 REPS = int(os.environ.get("REPS", "20"))
+PER_TRUNK = os.environ.get("PER_TRUNK", "0") == "1"  # one launch per trunk (batch 1) instead of batched twins
 
 
 SUMS = []
@@ -63,7 +64,12 @@ def main():
         a = rnd(2, M, k)
         w = rnd(2, n, k, scale=k ** -0.5)
         b = torch.randn(2 * n, device=dev, generator=g)
-        if l < 6:
+        if l < 6 and PER_TRUNK:
+            o = torch.empty((2, M, n), dtype=dt, device=dev)
+            p = torch.empty((2, M, n), dtype=dt, device=dev)
+            us = timeit(lambda: [N.twin_gemm(a[t], w[t], N.EPI_BIAS_SILU, o[t], (1, n), bias=b[t * n:(t + 1) * n],
+                                             aux=p[t]) for t in range(2)], o)
+        elif l < 6:
             o = torch.empty((2, M, n), dtype=dt, device=dev)
             p = torch.empty((2, M, n), dtype=dt, device=dev)
             us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS_SILU, o, (2, n), bias=b, aux=p), o)
@@ -78,7 +84,11 @@ def main():
         wt = rnd(2, nin, nout, scale=nout ** -0.5)
         p = rnd(2, M, nin)
         db = torch.empty(2 * nin, device=dev)
-        if l > 2:
+        if l > 2 and PER_TRUNK:
+            o = torch.empty((2, M, nin), dtype=dt, device=dev)
+            us = timeit(lambda: [N.twin_gemm(gg[t], wt[t], N.EPI_SILU_GRAD, o[t], (1, nin), aux=p[t],
+                                             bias_grad=db[t * nin:(t + 1) * nin]) for t in range(2)], o)
+        elif l > 2:
             o = torch.empty((2, M, nin), dtype=dt, device=dev)
             us = timeit(lambda: N.twin_gemm(gg, wt, N.EPI_SILU_GRAD, o, (2, nin), aux=p, bias_grad=db), o)
         else:
