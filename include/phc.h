@@ -467,6 +467,21 @@ int phc_tail_ln_fwd(const phc_tail_ln_args *args, void *stream);
 int phc_tail_ln_bwd(const phc_tail_ln_args *args, const float *dh_actor, const float *dmu, const float *dvalue,
                     int32_t num_actions, void *dy, int32_t dtype, float *partial, void *stream);
 
+/* R19 + R21: the actor's mu head, nn.Linear(hidden, num_actions) in fp32
+ * (policies/phc_policy.py:40-61; its autograd in clean_pufferl/core.py:298-354), on the fp32-input
+ * MFMA (exact products, fp32 sums; the summation order differs from a library GEMM's):
+ *   fwd  : mu [rows, A] = h [rows, hidden] . w [A, hidden]^T + b [A]   (h, w 16-byte aligned, hidden % 16 == 0)
+ *   dgrad: dh [rows, hidden] = dmu [rows, A] . w
+ *   wgrad: partial [splits, A, hidden], partial[s] = dmu[rows_s]^T . h[rows_s] over the s-th of
+ *          `splits` row chunks of ceil(rows / splits) rows (sum over s = the weight gradient).
+ * A = num_actions, 1..80.  Replaces the three library GEMMs around phc_tail_ln_fwd / _bwd. */
+int phc_mu_head_fwd(const float *h, const float *w, const float *b, float *mu, int64_t rows, int32_t hidden,
+                    int32_t num_actions, void *stream);
+int phc_mu_head_dgrad(const float *dmu, const float *w, float *dh, int64_t rows, int32_t hidden, int32_t num_actions,
+                      void *stream);
+int phc_mu_head_wgrad(const float *dmu, const float *h, float *partial, int64_t rows, int32_t hidden,
+                      int32_t num_actions, int32_t splits, void *stream);
+
 /* R22: the AMP discriminator's logits head (puffer_phc/policies/discriminator_policy.py:72-79:
  * Linear(hidden, 1) after the second ReLU layer; the two wide layers run on phc_twin_gemm with the
  * BIAS_RELU / RELU_GRAD epilogues) on h [rows, width] f16 / bf16 (ldh, 16-byte aligned; width

@@ -190,6 +190,10 @@ _EXPORTS = {
     "phc_tail_layout": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     "phc_tail_blocks": (ctypes.c_int32, [c_i64]),
     "phc_tail_ln_fwd": (ctypes.c_int, [ctypes.POINTER(TailLnArgsC), c_vp]),
+    "phc_mu_head_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32, ctypes.c_int32, c_vp]),
+    "phc_mu_head_dgrad": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.c_int32, ctypes.c_int32, c_vp]),
+    "phc_mu_head_wgrad": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                          c_vp]),
     "phc_tail_ln_bwd": (ctypes.c_int, [ctypes.POINTER(TailLnArgsC), c_vp, c_vp, c_vp, ctypes.c_int32, c_vp,
                                         ctypes.c_int32, c_vp, c_vp]),
     "phc_ppo_loss_fwd": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int32,
@@ -825,6 +829,48 @@ class TailLN:
                                      A, dy.data_ptr(), DTYPE_CODE[dtype], part.data_ptr(), _stream()),
                "phc_tail_ln_bwd")
         return dy, part, lay
+
+
+# ------------------------------------------------------------- mu head --
+MU_HEAD_MAX_ACTIONS = 80
+
+
+def mu_head_fwd(h, w, b, out=None):
+    """mu [M, A] = h [M, H] @ w [A, H]^T + b in fp32 (phc_mu_head_fwd, fp32-input MFMA)."""
+    M, H = h.shape
+    A = w.shape[0]
+    f32 = torch.float32
+    if out is None:
+        out = torch.empty((M, A), dtype=f32, device=h.device)
+    _check(lib().phc_mu_head_fwd(_ptr(h, f32, (M, H), "h"), _ptr(w, f32, (A, H), "w"),
+                                 _ptr(b.reshape(-1), f32, (A,), "b"), _ptr(out, f32, (M, A), "mu"), M, H, A,
+                                 _stream()), "phc_mu_head_fwd")
+    return out
+
+
+def mu_head_dgrad(dmu, w, out=None):
+    """dh [M, H] = dmu [M, A] @ w [A, H] in fp32 (phc_mu_head_dgrad)."""
+    M, A = dmu.shape
+    H = w.shape[1]
+    f32 = torch.float32
+    if out is None:
+        out = torch.empty((M, H), dtype=f32, device=dmu.device)
+    _check(lib().phc_mu_head_dgrad(_ptr(dmu, f32, (M, A), "dmu"), _ptr(w, f32, (A, H), "w"),
+                                   _ptr(out, f32, (M, H), "dh"), M, H, A, _stream()), "phc_mu_head_dgrad")
+    return out
+
+
+def mu_head_wgrad_parts(dmu, h, splits=128):
+    """[splits, A, H] fp32 partials of dmu^T @ h over row chunks (phc_mu_head_wgrad); their sum
+    over dim 0 is the weight gradient (phc_reduce_into sums them straight into .grad)."""
+    M, A = dmu.shape
+    H = h.shape[1]
+    f32 = torch.float32
+    splits = max(1, min(int(splits), M))
+    part = torch.empty((splits, A, H), dtype=f32, device=dmu.device)
+    _check(lib().phc_mu_head_wgrad(_ptr(dmu, f32, (M, A), "dmu"), _ptr(h, f32, (M, H), "h"), part.data_ptr(), M, H,
+                                   A, splits, _stream()), "phc_mu_head_wgrad")
+    return part
 
 
 # ------------------------------------------------------- experience store --

@@ -1,0 +1,271 @@
+// phc_head.hip — the actor's mu head in fp32 on the fp32-input MFMA (R19 / R21).
+//
+// The reference's mu head is nn.Linear(512, num_actions) in fp32 (policies/phc_policy.py:40-61;
+// the PPO update runs it under torch autograd, clean_pufferl/core.py:298-354).  With num_actions
+// = 69 its three GEMMs per minibatch are skinny (N or K = 69), so they run here as three small
+// kernels on v_mfma_f32_16x16x4_f32 — exact fp32 products, fp32 accumulation, the f32 vector
+// rate — instead of library GEMMs:
+//   k_head_fwd   : mu[M, A]  = h[M, H] · W[A, H]^T + b          (one wave per 16 rows x 80 columns)
+//   k_head_dgrad : dh[M, H]  = dmu[M, A] · W[A, H]              (one wave per 16 rows x 128 columns)
+//   k_head_wgrad : part[s]   = dmu[rows_s]^T · h[rows_s]        (one wave per 80 x 32 outputs, rows
+//                  split into S chunks; the caller sums the S partials, e.g. phc_reduce_into)
+// Fragments come straight from global memory (the operands are L2-resident: W is 141 KB, the row
+// tiles are read once).  K is walked in chunks of 16 with a permuted order inside each chunk —
+// MFMA step t of chunk q feeds lane group g the index 16 q + 4 g + t on both operands — so every
+// lane reads 4 consecutive K values with one 16-B load where the operand is K-contiguous.  A is at
+// most 80 (5 blocks of 16).
+#include "phc_common.h"
+
+namespace phc {
+
+using hf4 = __attribute__((ext_vector_type(4))) float;
+constexpr int kHeadMaxA = 80;
+
+__device__ __forceinline__ hf4 head_mfma(float a, float b, hf4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// mu = h W^T + b.  Block = 4 waves = 64 rows; wave w: rows r0 + 16 w .. + 15, all 80 columns.
+__global__ __launch_bounds__(256) void k_head_fwd(const float *__restrict__ h, const float *__restrict__ w,
+                                                  const float *__restrict__ b, float *__restrict__ mu, int64_t M,
+                                                  int H, int A) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int64_t r0 = (int64_t)blockIdx.x * 64 + wave * 16;
+  if (r0 >= M) return;
+  int64_t hr = r0 + c;
+  hr = hr < M ? hr : M - 1;  // ragged last tile: clamp the read, mask the store
+  const float *hp = h + hr * H + 4 * g;
+  const float *wp[5];
+  bool wv[5];
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) {
+    const int a = 16 * nb + c;
+    wv[nb] = a < A;
+    wp[nb] = w + (int64_t)(wv[nb] ? a : 0) * H + 4 * g;
+  }
+  hf4 acc[5];
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) acc[nb] = hf4{0.0f, 0.0f, 0.0f, 0.0f};
+  // chunk k0's operands are loaded one chunk ahead of its MFMAs (two register sets)
+  float4 hv[2], wf[2][5];
+  auto load = [&](int k0, int b) {
+    hv[b] = *reinterpret_cast<const float4 *>(hp + k0);
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) wf[b][nb] = *reinterpret_cast<const float4 *>(wp[nb] + k0);
+  };
+  auto compute = [&](int b) {  // step-major: consecutive MFMAs write different accumulators
+    float4 wv4[5];
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) wv4[nb] = wv[nb] ? wf[b][nb] : float4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) acc[nb] = head_mfma(hv[b].x, wv4[nb].x, acc[nb]);
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) acc[nb] = head_mfma(hv[b].y, wv4[nb].y, acc[nb]);
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) acc[nb] = head_mfma(hv[b].z, wv4[nb].z, acc[nb]);
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) acc[nb] = head_mfma(hv[b].w, wv4[nb].w, acc[nb]);
+  };
+  load(0, 0);
+  for (int k0 = 0; k0 < H; k0 += 32) {  // H % 16 == 0: the second half-step may be absent
+    if (k0 + 16 < H) load(k0 + 16, 1);
+    compute(0);
+    if (k0 + 16 >= H) break;
+    if (k0 + 32 < H) load(k0 + 32, 0);
+    compute(1);
+  }
+  // lane: column a = 16 nb + c, rows r0 + 4 g + e
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) {
+    const int a = 16 * nb + c;
+    if (a >= A) continue;
+    const float bias = b[a];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t row = r0 + 4 * g + e;
+      if (row < M) mu[row * A + a] = acc[nb][e] + bias;
+    }
+  }
+}
+
+// dh = dmu W.  Block = 4 waves = 16 rows x 512 columns; wave w: columns 128 w .. + 127 (8 blocks),
+// blockIdx.y walks further 512-column panels when H > 512.  K = A in chunks of 16 (zero past A).
+__global__ __launch_bounds__(256) void k_head_dgrad(const float *__restrict__ dmu, const float *__restrict__ w,
+                                                    float *__restrict__ dh, int64_t M, int H, int A) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int64_t r0 = (int64_t)blockIdx.x * 16;
+  const int c0 = blockIdx.y * 512 + wave * 128;
+  if (c0 >= H) return;
+  int64_t ar = r0 + c;
+  ar = ar < M ? ar : M - 1;
+  const float *ap = dmu + ar * A;
+  hf4 acc[8];
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) acc[nb] = hf4{0.0f, 0.0f, 0.0f, 0.0f};
+  // the lane's whole dmu fragment (k = 16 q + 4 g + t, q < 5) up front; W one chunk ahead
+  // loads are unconditional (clamped addresses) and masked after they land: a select around a
+  // load makes the compiler branch and drain the load queue per element
+  float av[5][4];
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = 16 * q + 4 * g + t;
+      av[q][t] = ap[k < A ? k : A - 1];
+    }
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (16 * q + 4 * g + t >= A) av[q][t] = 0.0f;  // the matching W rows are zeroed too
+  int colc[8];
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) colc[nb] = c0 + 16 * nb + c < H ? 16 * nb : H - 1 - c0 - c;
+  float bw[2][4][8];
+  auto load = [&](int q, int b) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = 16 * q + 4 * g + t;
+      const float *wr = w + (int64_t)(k < A ? k : A - 1) * H + c0 + c;
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) bw[b][t][nb] = wr[colc[nb]];
+    }
+  };
+  auto compute = [&](int q, int b) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) acc[nb] = head_mfma(av[q][t], bw[b][t][nb], acc[nb]);
+  };
+  const int nq = (A + 15) / 16;
+  load(0, 0);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    if (q >= nq) break;
+    if (q + 1 < nq) load(q + 1, (q + 1) & 1);
+    compute(q, q & 1);
+  }
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) {
+    const int col = c0 + 16 * nb + c;
+    if (col >= H) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t row = r0 + 4 * g + e;
+      if (row < M) dh[row * H + col] = acc[nb][e];
+    }
+  }
+}
+
+// part[s] = dmu[rows_s]^T h[rows_s] for the s-th chunk of rows_per_split rows (the last chunk
+// ragged).  Block (blockIdx.x = column panel of 128, blockIdx.y = s) = 4 waves; wave w: all 80
+// output rows (a) x columns 128 x + 32 w .. + 31 (2 blocks).  K = rows in chunks of 16.
+__global__ __launch_bounds__(256) void k_head_wgrad(const float *__restrict__ dmu, const float *__restrict__ h,
+                                                    float *__restrict__ part, int64_t M, int H, int A,
+                                                    int64_t rows_per_split) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int c0 = blockIdx.x * 128 + wave * 32;
+  const int64_t s = blockIdx.y, rb = s * rows_per_split;
+  const int64_t re = rb + rows_per_split < M ? rb + rows_per_split : M;
+  hf4 acc[5][2];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = hf4{0.0f, 0.0f, 0.0f, 0.0f};
+  const bool colv[2] = {c0 + c < H, c0 + 16 + c < H};
+  float av[2][4][5], bv[2][4][2];  // one 16-row chunk's fragments, loaded a chunk ahead
+  int ac[5];  // clamped dmu columns (masked after the load), see k_head_dgrad
+#pragma unroll
+  for (int i = 0; i < 5; ++i) ac[i] = 16 * i + c < A ? 16 * i + c : A - 1;
+  const int hc[2] = {colv[0] ? c0 + c : H - 1, colv[1] ? c0 + 16 + c : H - 1};
+  auto load = [&](int64_t k0, int b) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int64_t row = k0 + 4 * g + t;
+      const bool rv = row < re;
+      const float *arow = dmu + (rv ? row : rb) * A;
+      const float *hrow = h + (rv ? row : rb) * H;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) av[b][t][i] = arow[ac[i]];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[b][t][j] = hrow[hc[j]];
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        if (!rv || 16 * i + c >= A) av[b][t][i] = 0.0f;
+    }
+  };
+  auto compute = [&](int b) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = head_mfma(av[b][t][i], bv[b][t][j], acc[i][j]);
+  };
+  if (rb < re) load(rb, 0);
+  for (int64_t k0 = rb; k0 < re; k0 += 32) {
+    if (k0 + 16 < re) load(k0 + 16, 1);
+    compute(0);
+    if (k0 + 16 >= re) break;
+    if (k0 + 32 < re) load(k0 + 32, 0);
+    compute(1);
+  }
+  // lane: output row a = 16 i + 4 g + e, column c0 + 16 j + c
+  float *out = part + s * (int64_t)A * H;
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int a = 16 * i + 4 * g + e;
+      if (a >= A) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (colv[j]) out[(int64_t)a * H + c0 + 16 * j + c] = acc[i][j][e];
+    }
+}
+
+static int check_head(const void *x, const void *w, int64_t M, int H, int A) {
+  PHC_REQUIRE(x && w, "mu_head: null operand");
+  PHC_REQUIRE(M > 0 && H > 0 && A >= 1 && A <= kHeadMaxA, "mu_head: bad shape (rows %lld, hidden %d, actions %d <= %d)",
+              (long long)M, H, A, kHeadMaxA);
+  return PHC_OK;
+}
+
+}  // namespace phc
+
+using namespace phc;
+
+extern "C" int phc_mu_head_fwd(const float *h, const float *w, const float *b, float *mu, int64_t rows, int32_t hidden,
+                               int32_t num_actions, void *stream) {
+  if (int rc = check_head(h, w, rows, hidden, num_actions)) return rc;
+  PHC_REQUIRE(b && mu, "mu_head_fwd: null bias / output");
+  PHC_REQUIRE(hidden % 16 == 0, "mu_head_fwd: hidden must be a multiple of 16");
+  PHC_REQUIRE((reinterpret_cast<uintptr_t>(h) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
+              "mu_head_fwd: h and w must be 16-byte aligned");
+  const int64_t blocks = (rows + 63) / 64;
+  hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), h, w, b, mu, rows,
+                     (int)hidden, (int)num_actions);
+  return check_launch("mu_head_fwd");
+}
+
+extern "C" int phc_mu_head_dgrad(const float *dmu, const float *w, float *dh, int64_t rows, int32_t hidden,
+                                 int32_t num_actions, void *stream) {
+  if (int rc = check_head(dmu, w, rows, hidden, num_actions)) return rc;
+  PHC_REQUIRE(dh, "mu_head_dgrad: null output");
+  const dim3 grid((unsigned)((rows + 15) / 16), (unsigned)((hidden + 511) / 512));
+  hipLaunchKernelGGL(k_head_dgrad, grid, dim3(256), 0, as_stream(stream), dmu, w, dh, rows, (int)hidden,
+                     (int)num_actions);
+  return check_launch("mu_head_dgrad");
+}
+
+extern "C" int phc_mu_head_wgrad(const float *dmu, const float *h, float *partial, int64_t rows, int32_t hidden,
+                                 int32_t num_actions, int32_t splits, void *stream) {
+  if (int rc = check_head(dmu, h, rows, hidden, num_actions)) return rc;
+  PHC_REQUIRE(partial, "mu_head_wgrad: null partials");
+  PHC_REQUIRE(splits >= 1 && splits <= 65535, "mu_head_wgrad: 1..65535 splits");
+  const int64_t per = (rows + splits - 1) / splits;
+  const dim3 grid((unsigned)((hidden + 127) / 128), (unsigned)splits);
+  hipLaunchKernelGGL(k_head_wgrad, grid, dim3(256), 0, as_stream(stream), dmu, h, partial, rows, (int)hidden,
+                     (int)num_actions, per);
+  return check_launch("mu_head_wgrad");
+}

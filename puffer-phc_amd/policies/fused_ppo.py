@@ -1,21 +1,37 @@
 """The PPO minibatch as one autograd node on the device (R19 + R21).
 
 forward: MFMA twin trunks (twin_mlp.mfma_trunk_forward) -> phc_tail_ln_fwd (LayerNorm + SiLU of
-both trunks, the critic's value head) -> the fp32 mu head GEMM -> the PPO objective kernels
-(phc_ppo_loss_fwd).  backward: phc_ppo_loss_bwd (d mu, d value) -> d h_a = dmu W_mu and the split-K
-W_mu gradient (fp32 GEMMs) -> phc_tail_ln_bwd (LayerNorm + SiLU backward of both trunks; dy in the
-trunk's operand type; every remaining tail gradient as per-block column sums) -> the trunk
-backward.  Same math as PHCPolicy.forward_train + ppo_objective (reference:
+both trunks, the critic's value head) -> the fp32 mu head (phc_mu_head_fwd) -> the PPO objective
+kernels (phc_ppo_loss_fwd).  backward: phc_ppo_loss_bwd (d mu, d value) -> d h_a = dmu W_mu and the
+split-K W_mu gradient (phc_mu_head_dgrad / _wgrad, fp32-input MFMA) -> phc_tail_ln_bwd (LayerNorm +
+SiLU backward of both trunks; dy in the trunk's operand type; every remaining tail gradient as
+per-block column sums) -> the trunk backward.  Same math as PHCPolicy.forward_train + ppo_objective (reference:
 policies/phc_policy.py:16-61, clean_pufferl/core.py:298-352) without the ~30 elementwise, fill,
 copy and reduction launches autograd runs between those pieces; the unfused path stays for fp32
 storage and other shapes."""
+
+import os
 
 import torch
 
 from .. import _native as N
 from . import twin_mlp
-from .twin_mlp import (_compute_dtype, _use_mfma, _weight_grad, _weight_grad_parts, direct_grads_bound,
-                       mfma_trunk_backward, mfma_trunk_forward)
+from .twin_mlp import _compute_dtype, _use_mfma, direct_grads_bound, mfma_trunk_backward, mfma_trunk_forward
+
+
+MU_WGRAD_SPLITS = int(os.environ.get("PHC_MU_WGRAD_SPLITS", "128"))  # row chunks of the mu-head weight gradient
+# forward / input gradient of the mu head on phc_mu_head_fwd / _dgrad (1) or the library GEMMs (0):
+# the fp32-MFMA kernels read W once per 16-row wave and measured 49 / 54 us against the library's
+# 36 / 36 us per 32768-row minibatch (tools/mu_head_probe.py); the weight gradient runs on
+# phc_mu_head_wgrad either way (39 us + its partial sum riding in phc_reduce_into, library 140 us)
+MU_HEAD_KERNELS = os.environ.get("PHC_MU_HEAD_KERNELS", "0") == "1"
+
+
+def _aligned(w):
+    """w, or a 16-byte aligned copy (phc_mu_head_fwd reads w with 16-B loads; a parameter may be a
+    view into a flat buffer at any 4-byte offset)."""
+    w = w.contiguous()
+    return w if w.data_ptr() % 16 == 0 else w.clone(memory_format=torch.contiguous_format)
 
 
 class FusedPPOLossFn(torch.autograd.Function):
@@ -32,7 +48,10 @@ class FusedPPOLossFn(torch.autograd.Function):
         with torch.no_grad(), torch.autocast("cuda", enabled=False):
             tail = N.TailLN(y, (la_w, la_b), (lc_w, lc_b), eps, v_w, v_b)
             h_a, value = tail.forward()
-            mu = torch.addmm(mu_b, h_a, mu_w.t())  # fp32 head, as HeadLinearFn
+            if MU_HEAD_KERNELS:
+                mu = N.mu_head_fwd(h_a, _aligned(mu_w), mu_b)  # fp32 head, as HeadLinearFn
+            else:
+                mu = torch.addmm(mu_b, h_a, mu_w.t())
             stats, row_coef = N.ppo_loss_fwd(mu, log_sigma, actions, old_logprob, adv, adv_ms, value, old_value,
                                              returns, coefs)
         ctx.saved, ctx.tail, ctx.params, ctx.n_trunk = saved, tail, params, n_trunk
@@ -49,7 +68,10 @@ class FusedPPOLossFn(torch.autograd.Function):
         direct = direct_grads_bound(params)
         with torch.no_grad(), torch.autocast("cuda", enabled=False):
             gmu, gv = N.ppo_loss_bwd(mu, log_sigma, actions, row_coef, g_loss.float().contiguous(), coefs)
-            dh_a = torch.mm(gmu, mu_w.detach())
+            if MU_HEAD_KERNELS:
+                dh_a = N.mu_head_dgrad(gmu, mu_w.detach().contiguous())
+            else:
+                dh_a = torch.mm(gmu, mu_w.detach())
             dy, part, lay = tail.backward(dh_a, gmu, gv, saved.xc.dtype)
             sums = part.sum(0)
             A, H = gmu.shape[1], tail.H
@@ -62,7 +84,7 @@ class FusedPPOLossFn(torch.autograd.Function):
                          (seg("b_value", 1), v_b)]
             db6 = seg("b6", 2 * H)
             if direct:
-                jobs = [(_weight_grad_parts(gmu[None], tail.h_actor[None])[0], mu_w.grad)]
+                jobs = [(N.mu_head_wgrad_parts(gmu, tail.h_actor, MU_WGRAD_SPLITS), mu_w.grad)]
                 jobs += [(s.view(1, -1), p.grad) for s, p in tail_srcs]
                 if twin_mlp.GRAD_READY is not None:  # data parallel: the tail's all-reduce starts now
                     N.reduce_into(jobs, accumulate=True)
@@ -72,7 +94,7 @@ class FusedPPOLossFn(torch.autograd.Function):
                 mfma_trunk_backward(saved, dy, db6, params[:n], True, extra_jobs=jobs)
                 grads = [None] * len(params)
             else:
-                g_mu_w = _weight_grad(gmu[None], tail.h_actor[None])[0]
+                g_mu_w = N.mu_head_wgrad_parts(gmu, tail.h_actor, MU_WGRAD_SPLITS).sum(0)
                 tg = {id(p): s.reshape(p.shape).clone() for s, p in tail_srcs}
                 tg[id(mu_w)] = g_mu_w
                 trunk = mfma_trunk_backward(saved, dy, db6.clone(), params[:n], False)

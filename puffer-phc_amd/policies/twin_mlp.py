@@ -591,6 +591,11 @@ def _row_sum(g):
     return g.float().reshape(S, M // S, -1).sum(1).sum(0)
 
 
+def _head_kernels(x, w):
+    """phc_mu_head_* serve an fp32 device head with at most 80 outputs and width % 16 == 0."""
+    return x.is_cuda and w.shape[0] <= N.MU_HEAD_MAX_ACTIONS and w.shape[1] % 16 == 0 and x.dtype == torch.float32
+
+
 class HeadLinearFn(torch.autograd.Function):
     """nn.Linear with few outputs (the actor's mu head 512 -> 69, the critic's value head 512 -> 1)
     with a split-K weight gradient and a chunked bias gradient: torch's backward for these shapes
@@ -599,11 +604,15 @@ class HeadLinearFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b):
-        # float32 storage in every precision mode: the heads are < 1 % of the FLOPs, and the
-        # odd-width (69, 1) half-precision GEMMs cost more in hipBLASLt solution lookup than math
+        # float32 storage in every precision mode: the heads are < 1 % of the FLOPs; on the device
+        # the three GEMMs run on the fp32-input MFMA kernels of phc_head.hip (phc_mu_head_*)
         with torch.autocast("cuda", enabled=False):
-            xc = x.float()
-            y = torch.mm(xc, w.t()) + b
+            xc = x.float().contiguous()
+            wc = w.detach().float().contiguous()
+            if _head_kernels(xc, wc):
+                y = N.mu_head_fwd(xc, wc if wc.data_ptr() % 16 == 0 else wc.clone(), b.detach().float().contiguous())
+            else:
+                y = torch.mm(xc, w.t()) + b
         ctx.save_for_backward(xc, w)
         ctx.x_dtype = x.dtype
         return y
@@ -613,8 +622,13 @@ class HeadLinearFn(torch.autograd.Function):
         xc, wc = ctx.saved_tensors
         with torch.autocast("cuda", enabled=False):
             g = gy.to(xc.dtype).contiguous()
-            gx = torch.mm(g, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
-            gw = _weight_grad(g[None], xc[None])[0]
+            wd = wc.detach().float().contiguous()
+            if _head_kernels(xc, wd):
+                gx = N.mu_head_dgrad(g, wd).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+                gw = N.mu_head_wgrad_parts(g, xc, 128).sum(0)
+            else:
+                gx = torch.mm(g, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+                gw = _weight_grad(g[None], xc[None])[0]
             gb = _row_sum(g)
         return gx, gw, gb
 
