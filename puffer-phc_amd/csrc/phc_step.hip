@@ -14,6 +14,10 @@
 
 #include <vector>
 
+#ifndef PHC_ENV_ABLATE
+#define PHC_ENV_ABLATE 0
+#endif
+
 namespace phc {
 
 struct StepConsts {
@@ -330,6 +334,10 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   const bool valid = env < e.n;
   const int b = lane < kBodies ? lane : 0;
   const int64_t ei = valid ? env : 0;
+#if PHC_ENV_ABLATE == 1  // measurement build: launch + dispatch floor
+  if (valid && lane == 0) e.rew[ei] = 0.0f;
+  return;
+#endif
 
   // per-env scalars (broadcast loads: every lane of the half-wave reads the same word)
   const int prog = (int)e.progress[ei] + 1;
@@ -370,7 +378,14 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
     e.reset[ei] = o.reset;
     e.term[ei] = o.terminated;
   }
+#if PHC_ENV_ABLATE == 2  // measurement build: no observation math (the rows still feed a store)
+  if (valid && lane < kBodies) {
+    const BodyRec r1 = blend_body(rows1.a, rows1.c, bl1.b, &off1);
+    e.obs[ei * kObs + lane] = r1.p.x + r1.r.w + r1.v.y + r1.av.z + s.p.x;
+  }
+#else
   env_obs_ref(e, ei, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
+#endif
 
   if (e.stats) {
     if (lane == 0) {
