@@ -317,7 +317,7 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None):
     M = xc.shape[0]
     grads = [None] * (2 * L)
     jobs = list(extra_jobs) if (direct and extra_jobs) else []
-    grouped = GRAD_READY is None and GROUPED_WGRAD and M % 64 == 0 and L <= N.WGRAD_GROUP_MAX
+    grouped = (GRAD_READY is None or not DP_PER_LAYER) and GROUPED_WGRAD and M % 64 == 0 and L <= N.WGRAD_GROUP_MAX
     problems = {}
 
     def put_bias(l, db):
@@ -329,7 +329,8 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None):
             jobs.extend([(db[:n].view(1, n), ba.grad), (db[n:].view(1, n), bc.grad)])
 
     def put(l, dW_parts, db):
-        """dW_parts: ([parts, 2n, k] or [2, parts, n, k] partials, layer-1 flag), db [2n]."""
+        """dW_parts: ([parts, 2n, k] or [2, parts, n, k] partials, layer-1 flag), db [2n]
+        (per-layer path: without data parallelism, or with DP_PER_LAYER)."""
         if not direct:
             grads[2 * l], grads[2 * l + 1] = dW_parts, db
             return
@@ -408,6 +409,10 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None):
         if direct:
             if jobs:
                 N.reduce_into(jobs, accumulate=True)
+            if grouped and GRAD_READY is not None:
+                # data parallel on the grouped path: every trunk gradient is final now; their
+                # all-reduce (one contiguous span of the flat buffer, last layer first) starts
+                GRAD_READY([p for l in range(L - 1, -1, -1) for p in params[4 * l:4 * l + 4]])
             return None
     out = []
     for l in range(L):
@@ -547,6 +552,11 @@ PRE_HALF = os.environ.get("PHC_PRE_HALF", "1") == "1"
 GRAD_READY = None
 # one grouped weight-gradient launch per backward (False: per-layer split-K library GEMMs)
 GROUPED_WGRAD = True
+# data parallel: per-layer split-K weight gradients, each layer's all-reduce started as soon as
+# its gradient lands (1), or the single-GPU grouped launch with every trunk span's all-reduce
+# started after it (0, default: the grouped launch fills the 256 CUs exactly once and RCCL's
+# kernels do not take CUs from the backward's GEMMs)
+DP_PER_LAYER = os.environ.get("PHC_DP_PER_LAYER", "0") == "1"
 
 
 def _use_mfma(weights, dtype):
