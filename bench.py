@@ -252,8 +252,11 @@ class Runner:
             return None
         return int(c.skipped_steps)
 
+    _gpu_phases = None
+
     def mark(self):
         self._skip0 = self.skipped()
+        self._gpu_phases = [] if self.args.mode == "ppo" else None
         if self.args.mode == "ppo":
             p = self.info.profile
             self._p0 = {k: getattr(p, k).elapsed for k in ("evaluate", "env", "eval_forward", "train",
@@ -275,12 +278,41 @@ class Runner:
             self.env.send(actions)
             return a.envs
         g0 = self.info.global_step
+        ev = self._phase_events() if self._gpu_phases is not None else None
+        if ev:
+            ev[0].record()
         self.cp.evaluate(self.components, self.info)
+        if ev:
+            ev[1].record()
         self.policy.policy.update_obs_rms(self.components.experience.obs)
         if self.args.amp:
             self.policy.policy.update_amp_obs_rms(self.components.experience.amp_obs)
+        if ev:
+            ev[2].record()
         self.cp.train(self.components, self.info, self.util)
+        if ev:
+            ev[3].record()
+            self._gpu_phases.append(ev)
         return self.info.global_step - g0
+
+    @staticmethod
+    def _phase_events():
+        return [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+    def gpu_phase_ms(self):
+        """GPU-timeline time per timed step between events recorded on the stream at the phase
+        boundaries (evaluate | obs-RMS update | train): what the GPU spent from the first launch
+        of a phase to the last, idle gaps included — unlike the host timers, no phase absorbs
+        another's GPU work through a synchronising call."""
+        if not self._gpu_phases:
+            return None
+        n = len(self._gpu_phases)
+        tot = {"evaluate": 0.0, "rms_update": 0.0, "train": 0.0}
+        for e in self._gpu_phases:
+            tot["evaluate"] += e[0].elapsed_time(e[1])
+            tot["rms_update"] += e[1].elapsed_time(e[2])
+            tot["train"] += e[2].elapsed_time(e[3])
+        return {k: v / n for k, v in tot.items()}
 
 
 def main():
@@ -377,7 +409,12 @@ def main():
                                                "fp32 accumulate + outputs"}[args.precision]
                        if args.mode != "env" else None,
                        "optimizer_steps_skipped_by_loss_scaler": skipped,
-                       "phase_ms_per_step": runner.phase_ms(args.steps)},
+                       "phase_gpu_ms_per_step": runner.gpu_phase_ms(),
+                       "phase_host_wall_ms_per_step": runner.phase_ms(args.steps),
+                       "phase_note": "phase_gpu_ms: GPU-timeline time between stream events at the phase "
+                                     "boundaries; phase_host_wall_ms: clean_pufferl's host Profile timers, "
+                                     "where train_misc includes host waits on GPU work launched by other "
+                                     "phases (the per-epoch stat readback)" if args.mode == "ppo" else None},
             "cpu_baseline": cpu,
         }
         env_roof = {"bound": "hbm", "kernel": "phc_env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,

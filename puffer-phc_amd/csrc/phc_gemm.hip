@@ -43,6 +43,12 @@ constexpr int kGBK = 64;
 #ifndef PHC_WGRAD_SPLIT
 #define PHC_WGRAD_SPLIT 2
 #endif
+#ifndef PHC_GEMM_EPI_VW
+#define PHC_GEMM_EPI_VW 8  // output columns per thread in the epilogue for f16 / bf16 outputs (4 or 8)
+#endif
+#ifndef PHC_GEMM_GRAD_U8
+#define PHC_GEMM_GRAD_U8 2
+#endif
 #ifndef PHC_GEMM_SPLIT_A
 #define PHC_GEMM_SPLIT_A 0
 #endif
@@ -54,6 +60,7 @@ using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using b8 = __attribute__((ext_vector_type(8))) __bf16;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
 struct GemmArgs {
   const char *a, *b;
@@ -150,6 +157,43 @@ template <typename OutT> __device__ __forceinline__ void gemm_store4(void *p, in
       *reinterpret_cast<uint2 *>(static_cast<OutT *>(p) + off) = raw;
   }
 }
+
+// VW consecutive values at element offset off: fp32 as float4s, f16 / bf16 packed (16 B for VW 8)
+template <typename OutT, int VW>
+__device__ __forceinline__ void gemm_store_v(void *p, int64_t off, const float v[VW], bool nt) {
+  if constexpr (sizeof(OutT) == 4 || VW == 4) {
+#pragma unroll
+    for (int h = 0; h < VW / 4; ++h) gemm_store4<OutT>(p, off + 4 * h, v + 4 * h, nt);
+  } else {
+    OutT h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) h[q] = (OutT)v[q];
+    uint4 raw;
+    __builtin_memcpy(&raw, h, sizeof(raw));
+    if (nt)
+      __builtin_nontemporal_store(__builtin_bit_cast(u4v, raw), reinterpret_cast<u4v *>(static_cast<OutT *>(p) + off));
+    else
+      *reinterpret_cast<uint4 *>(static_cast<OutT *>(p) + off) = raw;
+  }
+}
+
+template <typename T, int VW> __device__ __forceinline__ void aux_store_v(const GemmArgs &g, int64_t off, const float v[VW]) {
+  if (VW == 8 && g.aux_half) {
+    T h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) h[q] = (T)v[q];
+    uint4 raw;
+    __builtin_memcpy(&raw, h, sizeof(raw));
+    if (g.nt & 2)
+      __builtin_nontemporal_store(__builtin_bit_cast(u4v, raw), reinterpret_cast<u4v *>(static_cast<T *>(g.aux) + off));
+    else
+      *reinterpret_cast<uint4 *>(static_cast<T *>(g.aux) + off) = raw;
+  } else {
+#pragma unroll
+    for (int h = 0; h < VW / 4; ++h) aux_store4<T>(g, off + 4 * h, v + 4 * h);
+  }
+}
+
 
 // issue the global_load_lds of one R-row x BK-column operand tile (R * BK / 512 wave-instructions
 // over the block's W waves).  BK = 64: LDS row r holds tile row r, its 16-B chunk c at slot
@@ -356,23 +400,32 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   // ---- epilogue.  The accumulators (lane: column lane & 15, rows 4 * (lane >> 4) + e of each
   // 16 x 16 block) go through LDS as an fp32 [rows][BN] image, 16-column groups XOR-swizzled by
   // (row >> 2) & 3 so both the scattered writes and the row reads are conflict-free; pass p holds
-  // rows [p * kEpWaveRows, (p + 1) * kEpWaveRows) of every wave row.  Then each thread owns 4
-  // consecutive columns of every kRowGroups-th image row: 16-B loads / stores, BN * 4
-  // contiguous bytes per row.
-  constexpr int kColThreads = BN / 4, kRowGroups = TL::kThreads / kColThreads;
+  // rows [p * kEpWaveRows, (p + 1) * kEpWaveRows) of every wave row.  Then each thread owns VW
+  // consecutive columns of every kRowGroups-th image row — 8 for a half-precision output, so every
+  // global store (and the input gradient's pre-activation load) moves 16 B per lane: the store
+  // tail of a tile is issue-bound, and halving its instruction count is what shortens it — and
+  // BN * sizeof(OutT) contiguous bytes per row.
+  constexpr int VW = sizeof(OutT) == 2 ? PHC_GEMM_EPI_VW : 4;
+  static_assert(VW == 4 || VW == 8, "4 or 8 columns per thread");
+  constexpr int kColThreads = BN / VW, kRowGroups = TL::kThreads / kColThreads;
   constexpr int WR = TL::kEpWaveRows, IT = TL::kEpRows / kRowGroups;
   float *ep = reinterpret_cast<float *>(smem);
-  const int c4 = (tid % kColThreads) * 4, rg = tid / kColThreads;
-  const int gcol = n0 + c4;
-  const bool vec = gcol + 3 < g.n && g.tc % 4 == 0;
+  const int cv = (tid % kColThreads) * VW, rg = tid / kColThreads;
+  const int gcol = n0 + cv;
+  const bool vec = gcol + VW - 1 < g.n && g.tc % VW == 0;
   const bool full = vec && m0 + BM <= g.m;
-  float bias4[4] = {0.0f, 0.0f, 0.0f, 0.0f}, csum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float biasv[VW], csum[VW];
+#pragma unroll
+  for (int q = 0; q < VW; ++q) {
+    biasv[q] = 0.0f;
+    csum[q] = 0.0f;
+  }
   if (EPI != PHC_EPI_STORE && g.bias) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (gcol + q < g.n) bias4[q] = g.bias[bt * g.n + gcol + q];
+    for (int q = 0; q < VW; ++q)
+      if (gcol + q < g.n) biasv[q] = g.bias[bt * g.n + gcol + q];
   }
-  // element offsets of this thread's 4 columns: base + row * stride in either layout
+  // element offsets of this thread's VW columns: base + row * stride in either layout
   const int lc = bt * g.n + gcol;
   const int grp = lc / g.tc, jc = lc - grp * g.tc;
   auto lin = [&](int layout, int64_t &base, int64_t &stride) {
@@ -387,6 +440,16 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
     const int r = rg + kRowGroups * it;
     return (r / WR) * TL::TM + p * WR + r % WR;
   };
+  // the VW image values of image row r at this thread's columns
+  auto read_image = [&](int r, float v[VW]) {
+#pragma unroll
+    for (int h = 0; h < VW / 4; ++h) {
+      const float4 t = *reinterpret_cast<const float4 *>(&ep[r * BN + ((cv + 4 * h) ^ (((r >> 2) & 3) << 4))]);
+      v[4 * h] = t.x; v[4 * h + 1] = t.y; v[4 * h + 2] = t.z; v[4 * h + 3] = t.w;
+    }
+  };
+  using RawV = typename std::conditional<VW == 8, uint4, uint2>::type;  // VW half-precision values
+  using RawN = typename std::conditional<VW == 8, u4v, u2v>::type;
 #pragma unroll
   for (int pass = 0; pass < TL::kEpPasses; ++pass) {
     lds_barrier();  // operand tiles / the previous pass's image are no longer read
@@ -402,77 +465,81 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
         }
     lds_barrier();
     if (full) {
-      // whole tile in range, 4 whole columns per thread: offsets are base + row * stride, rows
+      // whole tile in range, VW whole columns per thread: offsets are base + row * stride, rows
       // in batches of U; a half-precision aux is software-pipelined (batch b + 1's loads in
       // flight while batch b is processed), an fp32 one loaded per batch
-      constexpr int U = 4;
+      constexpr int U = (kGrad && VW == 8) ? PHC_GEMM_GRAD_U8 : 4;  // 16-B aux rows in flight per batch
       static_assert(IT % U == 0, "row batches");
       const bool pipe = kGrad && g.aux_half;
-      uint2 raw[2][kGrad ? U : 1];
+      RawV raw[2][kGrad ? U : 1];
       auto load_raw = [&](int b) {
         if constexpr (kGrad) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int64_t row = m0 + trow(pass, b * U + u);
             const T *src = static_cast<const T *>(g.aux) + ab + row * as;
-            raw[b & 1][u] = (g.nt & 4) ? __builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const u2v *>(src)))
-                                       : *reinterpret_cast<const uint2 *>(src);
+            raw[b & 1][u] = (g.nt & 4) ? __builtin_bit_cast(RawV, __builtin_nontemporal_load(reinterpret_cast<const RawN *>(src)))
+                                       : *reinterpret_cast<const RawV *>(src);
           }
         }
       };
       if (pipe) load_raw(0);
 #pragma unroll
       for (int i0 = 0; i0 < IT; i0 += U) {
-        float4 av[U];
+        float av[U][VW];
         if constexpr (kGrad) {
           if (pipe) {
             if (i0 + U < IT) load_raw(i0 / U + 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-              T h[4];
+              T h[VW];
               __builtin_memcpy(h, &raw[(i0 / U) & 1][u], sizeof(h));
-              av[u] = float4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+#pragma unroll
+              for (int q = 0; q < VW; ++q) av[u][q] = (float)h[q];
             }
           } else {
 #pragma unroll
-            for (int u = 0; u < U; ++u) av[u] = aux_load4<T>(g, ab + (m0 + trow(pass, i0 + u)) * as);
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+              for (int h = 0; h < VW / 4; ++h) {
+                const float4 a4 = aux_load4<T>(g, ab + (m0 + trow(pass, i0 + u)) * as + 4 * h);
+                av[u][4 * h] = a4.x; av[u][4 * h + 1] = a4.y; av[u][4 * h + 2] = a4.z; av[u][4 * h + 3] = a4.w;
+              }
           }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int r = rg + kRowGroups * (i0 + u);
           const int64_t row = m0 + trow(pass, i0 + u);
-          const float4 t = *reinterpret_cast<const float4 *>(&ep[r * BN + (c4 ^ (((r >> 2) & 3) << 4))]);
-          float v[4] = {t.x, t.y, t.z, t.w};
+          float v[VW];
+          read_image(r, v);
           if constexpr (EPI == PHC_EPI_SILU_GRAD) {
-            const float a[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float x = a[q] + bias4[q];
+            for (int q = 0; q < VW; ++q) {
+              const float x = av[u][q] + biasv[q];
               const float sg = gemm_sigmoid(x);
               v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
               csum[q] += v[q];
             }
           } else if constexpr (EPI == PHC_EPI_RELU_GRAD) {
-            const float a[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              v[q] = a[q] + bias4[q] > 0.0f ? v[q] : 0.0f;
+            for (int q = 0; q < VW; ++q) {
+              v[q] = av[u][q] + biasv[q] > 0.0f ? v[q] : 0.0f;
               csum[q] += v[q];
             }
           } else if constexpr (kBiasFwd) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] += bias4[q];
+            for (int q = 0; q < VW; ++q) v[q] += biasv[q];
             if constexpr (EPI == PHC_EPI_BIAS_SILU) {
-              if (g.aux) aux_store4<T>(g, ab + row * as, v);
+              if (g.aux) aux_store_v<T, VW>(g, ab + row * as, v);
 #pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = gemm_silu(v[q]);
+              for (int q = 0; q < VW; ++q) v[q] = gemm_silu(v[q]);
             } else if constexpr (EPI == PHC_EPI_BIAS_RELU) {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
+              for (int q = 0; q < VW; ++q) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
             }
           }
-          gemm_store4<OutT>(g.out, ob + row * os, v, g.nt & 1);
+          gemm_store_v<OutT, VW>(g.out, ob + row * os, v, g.nt & 1);
         }
       }
       continue;
@@ -481,42 +548,46 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
       const int r = rg + kRowGroups * it;
       const int64_t row = m0 + trow(pass, it);
       if (row >= g.m) continue;
-      const float4 t = *reinterpret_cast<const float4 *>(&ep[r * BN + (c4 ^ (((r >> 2) & 3) << 4))]);
-      float v[4] = {t.x, t.y, t.z, t.w};
-      float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      float v[VW], a[VW];
+      read_image(r, v);
+#pragma unroll
+      for (int q = 0; q < VW; ++q) a[q] = 0.0f;
       if constexpr (kGrad) {
         if (vec) {
-          const float4 av = aux_load4<T>(g, gemm_twin_off(g, g.aux_layout, row, lc));
-          a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
+#pragma unroll
+          for (int h = 0; h < VW / 4; ++h) {
+            const float4 a4 = aux_load4<T>(g, gemm_twin_off(g, g.aux_layout, row, lc) + 4 * h);
+            a[4 * h] = a4.x; a[4 * h + 1] = a4.y; a[4 * h + 2] = a4.z; a[4 * h + 3] = a4.w;
+          }
         } else {
-          for (int q = 0; q < 4; ++q)
+          for (int q = 0; q < VW; ++q)
             if (gcol + q < g.n) a[q] = aux_load1<T>(g, gemm_twin_off(g, g.aux_layout, row, lc + q));
         }
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < VW; ++q) {
         if constexpr (kBiasFwd) {
-          v[q] += bias4[q];
+          v[q] += biasv[q];
           a[q] = v[q];
           if constexpr (EPI == PHC_EPI_BIAS_SILU) v[q] = gemm_silu(v[q]);
           if constexpr (EPI == PHC_EPI_BIAS_RELU) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
         } else if constexpr (EPI == PHC_EPI_SILU_GRAD) {
-          const float x = a[q] + bias4[q];
+          const float x = a[q] + biasv[q];
           const float sg = gemm_sigmoid(x);
           v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
           csum[q] += gcol + q < g.n ? v[q] : 0.0f;
         } else if constexpr (EPI == PHC_EPI_RELU_GRAD) {
-          v[q] = a[q] + bias4[q] > 0.0f ? v[q] : 0.0f;
+          v[q] = a[q] + biasv[q] > 0.0f ? v[q] : 0.0f;
           csum[q] += gcol + q < g.n ? v[q] : 0.0f;
         }
       }
       if (vec) {
         if constexpr (EPI == PHC_EPI_BIAS_SILU) {
-          if (g.aux) aux_store4<T>(g, gemm_twin_off(g, g.aux_layout, row, lc), a);
+          if (g.aux) aux_store_v<T, VW>(g, gemm_twin_off(g, g.aux_layout, row, lc), a);
         }
-        gemm_store4<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, lc), v, g.nt & 1);
+        gemm_store_v<OutT, VW>(g.out, gemm_twin_off(g, g.out_layout, row, lc), v, g.nt & 1);
       } else {
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < VW; ++q) {
           if (gcol + q >= g.n) break;
           if constexpr (EPI == PHC_EPI_BIAS_SILU) {
             if (g.aux) aux_store1<T>(g, gemm_twin_off(g, g.aux_layout, row, lc + q), a[q]);
@@ -529,26 +600,32 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   if constexpr (kGrad) {
     if (!g.partial) return;
     // column sums over the tile's rows: row groups inside a wave by shuffle, the waves by LDS
-    if constexpr (kColThreads == 32) {
+    if constexpr (kColThreads < 64) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) csum[q] += __shfl_xor(csum[q], 32, 64);
+      for (int o = kColThreads; o < 64; o <<= 1)
+#pragma unroll
+        for (int q = 0; q < VW; ++q) csum[q] += __shfl_xor(csum[q], o, 64);
     }
-    constexpr int kWaveRows = kColThreads >= 64 ? 1 : 64 / kColThreads;  // rows one wave spans
     lds_barrier();  // the epilogue image is no longer read
-    if (lane < 64 / kWaveRows) {
-      const int wc = (kColThreads >= 64 ? (tid % kColThreads) : lane) * 4;
+    constexpr int kSlots = kColThreads >= 64 ? kRowGroups : TL::kWaves;
+    if (kColThreads >= 64 || lane < kColThreads) {
+      const int wc = (kColThreads >= 64 ? (tid % kColThreads) : lane) * VW;
       const int slot = kColThreads >= 64 ? (tid / kColThreads) : wave;
-      *reinterpret_cast<float4 *>(&ep[slot * BN + wc]) = float4{csum[0], csum[1], csum[2], csum[3]};
+#pragma unroll
+      for (int h = 0; h < VW / 4; ++h)
+        *reinterpret_cast<float4 *>(&ep[slot * BN + wc + 4 * h]) =
+            float4{csum[4 * h], csum[4 * h + 1], csum[4 * h + 2], csum[4 * h + 3]};
     }
     lds_barrier();
-    constexpr int kSlots = kColThreads >= 64 ? kRowGroups : TL::kWaves;
     if (tid < kColThreads) {
-      float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      float o[VW];
+#pragma unroll
+      for (int q = 0; q < VW; ++q) o[q] = 0.0f;
       for (int w = 0; w < kSlots; ++w)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] += ep[w * BN + c4 + q];
+        for (int q = 0; q < VW; ++q) o[q] += ep[w * BN + cv + q];
       float *pr = g.partial + (int64_t)tm * (g.batch * g.n) + bt * g.n;
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < VW; ++q)
         if (gcol + q < g.n) pr[gcol + q] = o[q];
     }
   }
