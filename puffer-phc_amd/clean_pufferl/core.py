@@ -13,6 +13,7 @@ Differences from the reference that do not change the math:
 """
 
 import contextlib
+import os
 from collections import defaultdict
 
 import numpy as np
@@ -54,6 +55,9 @@ def _l2_init_reg(named_params, initial_params, need_grad):
 
 
 _NUMEL_CACHE = {}
+# fused minibatch backward stores every gradient (one writer per parameter) instead of adding it,
+# so the flat gradient buffer is not zeroed per minibatch (PHC_STORE_GRADS=0: zero + accumulate)
+STORE_GRADS = os.environ.get("PHC_STORE_GRADS", "1") == "1"
 
 _AUTOCAST = {"fp16": torch.float16, "bf16": torch.bfloat16}
 
@@ -401,7 +405,12 @@ def train(components, info, utilization=None):
                             ms = torch.tensor([0.0, 1.0], dtype=torch.float32, device=obs.device)
                         if tail_coefs is None:
                             tail_coefs = ppo_coefs(cfg, pol.soft_bound)
-                        loss, st = fused_ppo_loss(pol, obs, atn, log_probs, adv, ms, val, ret, tail_coefs)
+                        # every gradient of this backward has one writer that stores it: the flat
+                        # buffer need not be zeroed first (AMP adds the discriminator's on top)
+                        store_grads = STORE_GRADS and not info.use_amp_obs and isinstance(components.optimizer,
+                                                                                          FlatAdam)
+                        loss, st = fused_ppo_loss(pol, obs, atn, log_probs, adv, ms, val, ret, tail_coefs,
+                                                  store_grads=store_grads)
                     elif fused_obj:
                         mu, newvalue = pol.forward_train(obs)
                     else:
@@ -444,8 +453,7 @@ def train(components, info, utilization=None):
                             v_loss = ((newvalue - ret) ** 2).mean()
                         entropy_loss = entropy.mean()
                         loss = pg_loss - cfg.ent_coef * entropy_loss + v_loss * cfg.vf_coef
-                    disc_loss = torch.zeros((), device=cfg.device)
-                    disc_acc = (torch.zeros((), device=cfg.device), torch.zeros((), device=cfg.device))
+                    disc_loss = disc_acc = None  # zeros only where the logging row needs them (below)
                     if info.use_amp_obs:
                         # agent rows, replay rows and demo rows through the discriminator in one
                         # pass (core.py:336-344 calls it twice; rows are independent)
@@ -476,7 +484,8 @@ def train(components, info, utilization=None):
                     if cfg.l2_reg_coef > 0:
                         loss = loss + l2 * cfg.l2_reg_coef
                 with profile.learn:
-                    flat.zero()
+                    if not (fused_mb and store_grads):
+                        flat.zero()
                     opt, scaler = components.optimizer, components.scaler
                     if isinstance(opt, FlatAdam):
                         flat.overlap_begin()  # data parallel: per-layer all-reduces during the backward
@@ -504,6 +513,9 @@ def train(components, info, utilization=None):
                         continue
                     if l2 is None:
                         l2 = components.optimizer.norms[2]
+                    if disc_loss is None:
+                        disc_loss = torch.zeros((), device=cfg.device)
+                        disc_acc = (disc_loss, disc_loss)
                     acc += torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl,
                                         approx_kl, clipfrac, gnorm, l2.detach(), disc_loss.detach(),
                                         (mbl.detach() if mbl is not None else torch.zeros((), device=cfg.device)),

@@ -41,7 +41,7 @@ class FusedPPOLossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weights, cfg, data, n_trunk, *params):
-        eps, log_sigma, coefs = cfg
+        eps, log_sigma, coefs, ctx.store_grads = cfg
         y, saved = mfma_trunk_forward(x, weights, True)
         la_w, la_b, lc_w, lc_b, mu_w, mu_b, v_w, v_b = [p.detach() for p in params[n_trunk:]]
         actions, old_logprob, adv, adv_ms, old_value, returns = data
@@ -73,25 +73,30 @@ class FusedPPOLossFn(torch.autograd.Function):
             else:
                 dh_a = torch.mm(gmu, mu_w.detach())
             dy, part, lay = tail.backward(dh_a, gmu, gv, saved.xc.dtype)
-            sums = part.sum(0)
             A, H = gmu.shape[1], tail.H
+            # direct mode: the tail's per-block partial rows go to phc_reduce_into as [parts, 1, w]
+            # sources (summed in the same launch that writes them into .grad); otherwise summed here
+            sums = None if direct else part.sum(0)
 
             def seg(key, width):
-                return sums[lay[key]:lay[key] + width]
+                o = lay[key]
+                return part[:, None, o:o + width] if direct else sums[o:o + width]
 
-            tail_srcs = [(seg("gamma", H), la_w), (seg("beta", H), la_b), (seg("gamma", 2 * H)[H:], lc_w),
-                         (seg("beta", 2 * H)[H:], lc_b), (seg("b_mu", A), mu_b), (seg("w_value", H), v_w),
-                         (seg("b_value", 1), v_b)]
-            db6 = seg("b6", 2 * H)
+            tail_srcs = [(seg("gamma", 2 * H), (la_w, lc_w)), (seg("beta", 2 * H), (la_b, lc_b)),
+                         (seg("b_mu", A), (mu_b,)), (seg("w_value", H), (v_w,)), (seg("b_value", 1), (v_b,))]
+            tail_srcs = [(src[..., k * p.numel():(k + 1) * p.numel()], p) for src, ps in tail_srcs
+                         for k, p in enumerate(ps)]
+            db6 = part[:, lay["b6"]:lay["b6"] + 2 * H] if direct else sums[lay["b6"]:lay["b6"] + 2 * H]
             if direct:
                 jobs = [(N.mu_head_wgrad_parts(gmu, tail.h_actor, MU_WGRAD_SPLITS), mu_w.grad)]
-                jobs += [(s.view(1, -1), p.grad) for s, p in tail_srcs]
+                jobs += [(s, p.grad) for s, p in tail_srcs]
+                store = ctx.store_grads
                 if twin_mlp.GRAD_READY is not None:  # data parallel: the tail's all-reduce starts now
-                    N.reduce_into(jobs, accumulate=True)
+                    N.reduce_into(jobs, accumulate=not store)
                     twin_mlp.GRAD_READY(params[n:])
                     jobs = None
                 # single-GPU: the tail's sums ride along with the trunk's final reduce launch
-                mfma_trunk_backward(saved, dy, db6, params[:n], True, extra_jobs=jobs)
+                mfma_trunk_backward(saved, dy, db6, params[:n], True, extra_jobs=jobs, store=store)
                 grads = [None] * len(params)
             else:
                 g_mu_w = N.mu_head_wgrad_parts(gmu, tail.h_actor, MU_WGRAD_SPLITS).sum(0)
@@ -116,9 +121,12 @@ def fused_ppo_supported(policy, obs):
             and policy.mu[0].weight.shape[0] <= N.TAIL_MAX_ACTIONS)
 
 
-def fused_ppo_loss(policy, obs, actions, old_logprob, adv, adv_mean_std, old_value, returns, coefs):
+def fused_ppo_loss(policy, obs, actions, old_logprob, adv, adv_mean_std, old_value, returns, coefs,
+                   store_grads=False):
     """(loss, stats [7]: pg, v, entropy, old_approx_kl, approx_kl, clipfrac, bound) of one
-    minibatch; the backward writes every policy gradient."""
+    minibatch; the backward writes every policy gradient.  store_grads: with the gradients bound
+    to a flat buffer (direct mode), the backward stores them instead of adding to them, so the
+    buffer need not be zeroed first (every parameter of the policy has exactly one writer)."""
     h = policy._head
     la, lc = policy.actor_mlp[h], policy.critic_mlp[h]
     vh, mh = policy.critic_mlp[h + 2], policy.mu[0]
@@ -127,5 +135,5 @@ def fused_ppo_loss(policy, obs, actions, old_logprob, adv, adv_mean_std, old_val
     f = lambda t: t.detach().float().contiguous().reshape(-1)  # noqa: E731
     data = (actions.detach().float().contiguous(), f(old_logprob), f(adv), adv_mean_std.detach().float().contiguous(),
             f(old_value), f(returns))
-    cfg = (la.eps, policy.sigma.detach().float().contiguous().reshape(-1), coefs)
+    cfg = (la.eps, policy.sigma.detach().float().contiguous().reshape(-1), coefs, bool(store_grads))
     return FusedPPOLossFn.apply(obs, policy._twin, cfg, data, len(trunk), *trunk, *tail)

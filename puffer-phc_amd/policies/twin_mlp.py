@@ -298,7 +298,7 @@ def _grouped_subset(problems, device, rest=False):
     return sel
 
 
-def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None):
+def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None, store=False):
     """Backward of mfma_trunk_forward from g = d loss / d (last layer output) [2, M, n] in the
     operand dtype and db = its fp32 column sums [2n] (the last layer's bias gradient; in direct
     mode also [parts, 2n] partial rows, summed into the bias gradients).  Every
@@ -310,7 +310,9 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None):
     backward continues.  direct: the gradients are summed straight into the parameters' bound
     .grad views and None is returned; otherwise the per-parameter gradient list (trunk params
     order).  extra_jobs: (src, dst) accumulate jobs of the caller, flushed with the trunk's own
-    bias-gradient sums in one phc_reduce_into launch (direct mode)."""
+    bias-gradient sums in one phc_reduce_into launch (direct mode).  store (direct mode): every
+    gradient is written, not added — each parameter has exactly one writer (its job or its
+    grouped tile), so the caller need not zero the gradient buffer first."""
     L, K0 = saved.L, saved.K0
     xc, WT, pres, zs = saved.xc, saved.wt, saved.pres, saved.zs
     dt = xc.dtype
@@ -342,7 +344,7 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None):
             jobs.extend([(dW_parts[0], wa.grad), (dW_parts[1], wc.grad)])
         put_bias(l, db)
         if GRAD_READY is not None:  # data parallel: this layer's gradients now, then its all-reduce
-            N.reduce_into(jobs, accumulate=True)
+            N.reduce_into(jobs, accumulate=not store)
             jobs.clear()
             GRAD_READY(params[4 * l:4 * l + 4])
 
@@ -405,10 +407,11 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None):
                     jobs.extend(pairs)  # summed with the bias jobs below
                 else:
                     N.reduce_into(pairs, accumulate=False)
-            N.weight_grad_group([problems[l][3] for l in _grouped_subset(problems, xc.device)], accumulate=direct)
+            N.weight_grad_group([problems[l][3] for l in _grouped_subset(problems, xc.device)],
+                                accumulate=direct and not store)
         if direct:
             if jobs:
-                N.reduce_into(jobs, accumulate=True)
+                N.reduce_into(jobs, accumulate=not store)
             if grouped and GRAD_READY is not None:
                 # data parallel on the grouped path: every trunk gradient is final now; their
                 # all-reduce (one contiguous span of the flat buffer, last layer first) starts

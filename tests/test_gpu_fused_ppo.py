@@ -167,3 +167,53 @@ def test_fused_minibatch_matches_unfused(direct):
     names = [n for n, q in policy.named_parameters() if q.requires_grad]
     for n, a, b in zip(names, gf, gu):
         assert _rel(a, b) < 2e-3, n
+
+
+@pytest.mark.parametrize("rows", [2048, 32768])  # split-K weight gradients; the grouped launch
+def test_store_grads_writes_every_gradient(rows):
+    """fused_ppo_loss(store_grads=True) into a flat buffer pre-filled with NaN gives, bit for bit,
+    the gradients of the zero-then-accumulate backward: every parameter has exactly one writer
+    (clean_pufferl.core then skips the per-minibatch zeroing of the 68 MB buffer)."""
+    from puffer_phc_amd.clean_pufferl.ppo_loss import ppo_coefs
+    from puffer_phc_amd.config import TrainConfig
+    from puffer_phc_amd.distributed import FlatGrads
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+    from puffer_phc_amd.policies.fused_ppo import fused_ppo_loss
+
+    torch.manual_seed(0)
+    policy = Policy(PHCPolicy(_Env())).to(DEV)
+    pol = policy.policy
+    cfg = TrainConfig()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    obs = torch.randn((rows, 934), device=DEV, generator=g)
+    atn = 0.1 * torch.randn((rows, 69), device=DEV, generator=g)
+    old_lp = torch.randn(rows, device=DEV, generator=g) + 200.0  # ratios ~0: finite objective
+    adv, val, ret = (torch.randn(rows, device=DEV, generator=g) for _ in range(3))
+    ms = torch.tensor([0.0, 1.0], device=DEV)
+    params = [q for q in policy.parameters() if q.requires_grad]
+    fg = FlatGrads(params, order=pol.grad_ready_order())
+    out = []
+    for store in (False, True):
+        if store:
+            fg.flat.fill_(float("nan"))
+        else:
+            fg.zero()
+        with torch.autocast("cuda", dtype=torch.float16):
+            xh = pol.obs_half_input(obs)
+            loss, _ = fused_ppo_loss(pol, xh, atn, old_lp, adv, ms, val, ret, ppo_coefs(cfg, pol.soft_bound),
+                                     store_grads=store)
+        (loss * 64.0).backward()
+        torch.cuda.synchronize()
+        out.append(fg.flat.detach().clone())
+    names = []
+    for n_, q in policy.named_parameters():
+        if q.requires_grad:
+            names.append((n_, q))
+    bad = []
+    for n_, q in names:
+        lo, hi = fg._range[id(q)]
+        a, b = out[0][lo:hi], out[1][lo:hi]
+        if not torch.equal(a, b):
+            bad.append((n_, int((~torch.isfinite(b)).sum()), float((a - b).abs().nan_to_num(1e30).max())))
+    assert torch.isfinite(out[0]).all()
+    assert not bad, bad
