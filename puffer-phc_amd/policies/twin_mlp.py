@@ -298,6 +298,20 @@ def _grouped_subset(problems, device, rest=False):
     return sel
 
 
+def _mfma_wgrad_parts(g, z):
+    """Split-K partials [B, S, n, k] of dW[b] = g[b]^T z[b] for the MFMA path's per-layer weight
+    gradients: the transposed-read kernel (phc_weight_grad) when the rows split into 64-row
+    chunks, else the library GEMMs (_weight_grad_parts: ragged row counts, e.g. 1000-row tests)."""
+    B, M, n = g.shape
+    if M % 64 or n % 8 or z.shape[2] % 8:
+        return _weight_grad_parts(g, z)
+    S = _wgrad_splits(_wgrad_tiles(g, z), M, g.device)
+    gg = g if B > 1 else g[0]
+    zz = z if z.shape[0] > 1 else z[0]
+    part = N.weight_grad(gg, zz, S)  # [S, B, n, k]
+    return part.transpose(0, 1)
+
+
 def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None, store=False):
     """Backward of mfma_trunk_forward from g = d loss / d (last layer output) [2, M, n] in the
     operand dtype and db = its fp32 column sums [2n] (the last layer's bias gradient; in direct
@@ -369,7 +383,7 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None, store=Fal
                 else:
                     grads[2 * l], grads[2 * l + 1] = W, db
             else:
-                put(l, _weight_grad_parts(g, zs[l - 1]) if direct else _weight_grad(g, zs[l - 1]), db)
+                put(l, _mfma_wgrad_parts(g, zs[l - 1]) if direct else _mfma_wgrad_parts(g, zs[l - 1]).sum(1), db)
             k = WT[l - 1].shape[1]
             db = torch.empty(2 * k, dtype=torch.float32, device=g.device)
             if l > 1:
@@ -387,9 +401,9 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None, store=Fal
                     else:
                         grads[0], grads[1] = W, db
                 elif direct:
-                    put(0, _weight_grad_parts(gp[None], xc[None])[0], db)
+                    put(0, _mfma_wgrad_parts(gp[None], xc[None])[0], db)
                 else:
-                    put(0, _weight_grad(gp[None], xc[None])[0][:, :K0], db)
+                    put(0, _mfma_wgrad_parts(gp[None], xc[None])[0].sum(0)[:, :K0], db)
             g = gp
         if grouped:
             for l in _grouped_subset(problems, xc.device, rest=True):
