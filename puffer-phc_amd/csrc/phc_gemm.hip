@@ -281,9 +281,12 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
   using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
   constexpr int GP = MI / 2, NS = BK / 32, NG = NS * GP;
-  if (!PHC_GEMM_SPLIT_DMA && issue) stage(next, wr, 3);
-  if (PHC_GEMM_SPLIT_DMA && !PHC_GEMM_SPLIT_A && issue) stage(next, wr, 1);
-  if (PHC_GEMM_SPLIT_A && issue) stage(next, wr, 4);
+  // the B operand's DMA a quarter K-step after A's on 256 x 256 tiles (measured: -4 % on the
+  // minibatch GEMMs); on the short K-steps of 128 x 128 tiles the late B tile is exposed (+25 %)
+  constexpr int SPLIT = TL::BM >= 256 ? PHC_GEMM_SPLIT_DMA : 0;
+  if (!SPLIT && issue) stage(next, wr, 3);
+  if (SPLIT && !PHC_GEMM_SPLIT_A && issue) stage(next, wr, 1);
+  if (SPLIT && PHC_GEMM_SPLIT_A && issue) stage(next, wr, 4);
   const char *ta = rd;
   const char *tb = rd + TL::BM * BK * 2;
   static_assert(MI % 2 == 0, "A fragments are walked in pairs");
@@ -307,8 +310,8 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
       if (s1 != s) load_b(fb[s1 & 1], s1);
       load_a(fa[(q + 1) & 1], s1, p1);
     }
-    if (PHC_GEMM_SPLIT_A && issue && q == PHC_GEMM_SPLIT_A * NG / 8) stage(next, wr, 8);
-    if (PHC_GEMM_SPLIT_DMA && issue && q == (PHC_GEMM_SPLIT_DMA * NG / 8 < NG ? PHC_GEMM_SPLIT_DMA * NG / 8 : NG - 1)) stage(next, wr, 2);
+    if (SPLIT && PHC_GEMM_SPLIT_A && issue && q == PHC_GEMM_SPLIT_A * NG / 8) stage(next, wr, 8);
+    if (SPLIT && issue && q == (SPLIT * NG / 8 < NG ? SPLIT * NG / 8 : NG - 1)) stage(next, wr, 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
     if (PHC_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
