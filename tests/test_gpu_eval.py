@@ -51,6 +51,26 @@ def test_eval_low_noise_all_succeed(golden):
     assert np.all(rbm["played_steps"] >= 1) and np.all(rbm["played_steps"] <= rbm["motion_length"])
 
 
+def test_eval_metrics_recomputed_from_recorded_positions(golden):
+    """The eval metrics are compute_metrics_lite over exactly the frames the reference keeps
+    (scripts/train.py:150-201: per motion the first motion_num_steps - 1 steps of body_pos /
+    body_pos_gt), and the per-step MPJPE extra is the mean joint distance of those two arrays
+    (humanoid_phc.py:159-169).  Recomputed here with independent loops."""
+    env, stats, res, n, steps = _run(golden, 0.02)
+    pred, gt = stats.pred_pos_all[:n], stats.gt_pos_all[:n]
+    lens = stats.results_by_motion["motion_length"]
+    assert [p.shape[0] for p in pred] == [int(x) - 1 for x in lens]
+    frames = []
+    for p, g in zip(pred, gt):
+        for t in range(p.shape[0]):
+            frames.append(np.mean([np.linalg.norm(p[t, j] - g[t, j]) for j in range(p.shape[1])]) * 1000.0)
+    np.testing.assert_allclose(res["eval/mpjpe_all"], np.mean(frames), rtol=1e-6)
+    # the per-step MPJPE means of the batches (mpjpe_all, reported live) come from the same arrays
+    means = [float(x) for b in stats.mpjpe_all for x in b][:n]
+    np.testing.assert_allclose(means, [np.mean(np.linalg.norm(p - g, axis=2)) for p, g in zip(pred, gt)],
+                               rtol=1e-5)
+
+
 def test_eval_high_noise_reports_failures(golden):
     env, stats, res, n, steps = _run(golden, 0.6)
     succ = stats.results_by_motion["success"]

@@ -49,3 +49,39 @@ def test_velocity_and_acceleration_errors():
     np.testing.assert_allclose(compute_error_accel(gt, pred), 0.0, atol=1e-12)
     pred[:, :, 1] = 0.1 * t[:, None] ** 2     # constant acceleration 0.2 / frame^2
     np.testing.assert_allclose(compute_error_accel(gt, pred), 0.2, rtol=1e-9)
+
+
+def test_hand_worked_vectors():
+    """compute_metrics_lite's published definitions on a 3-frame, 2-joint motion worked out by hand
+    (metres in, millimetres out; smpl_sim.smpllib.smpl_eval, called at scripts/train.py:197-198):
+      gt   : joint 0 at the origin, joint 1 at (1, 0, 0) m in every frame;
+      pred : joint 1 displaced by (0, 0.003, 0.004) m (5 mm) in frame 1 only.
+    mpjpe_g per frame = mean over joints = (0, 2.5, 0) mm; root-relative (joint 0 is the root and
+    undisplaced) the same; velocity error: frames 0->1 and 1->2 each move joint 1 by 5 mm ->
+    mean over joints 2.5 mm; acceleration error: joint 1's second difference 2 x 5 mm = 10 mm ->
+    mean over joints 5 mm."""
+    gt = np.zeros((3, 2, 3))
+    gt[:, 1, 0] = 1.0
+    pred = gt.copy()
+    pred[1, 1] += [0.0, 0.003, 0.004]
+    m = compute_metrics_lite([pred], [gt])
+    np.testing.assert_allclose(m["mpjpe_g"], [0.0, 2.5, 0.0], atol=1e-9)
+    np.testing.assert_allclose(m["mpjpe_l"], [0.0, 2.5, 0.0], atol=1e-9)
+    np.testing.assert_allclose(m["vel_dist"], [2.5, 2.5], atol=1e-9)
+    np.testing.assert_allclose(m["accel_dist"], [5.0], atol=1e-9)
+    # frames 0 and 2 are exact, so their Procrustes error is 0; frame 1 is a non-similar
+    # distortion of a 2-point set, which a similarity transform of 2 points always absorbs
+    np.testing.assert_allclose(m["mpjpe_pa"], 0.0, atol=1e-9)
+
+
+def test_procrustes_does_not_reflect():
+    """The published p_mpjpe corrects the SVD's rotation to det = +1 (sign_det): a mirrored pose
+    is not aligned away (a reflection would give 0)."""
+    rng = np.random.default_rng(3)
+    gt = rng.normal(size=(4, 24, 3))
+    mirrored = gt * np.array([-1.0, 1.0, 1.0])
+    assert np.all(p_mpjpe(mirrored, gt) > 0.05)
+    # a proper rotation of the same pose is aligned away
+    c, s = np.cos(0.4), np.sin(0.4)
+    rot = gt @ np.array([[1, 0, 0], [0, c, -s], [0, s, c]]).T
+    np.testing.assert_allclose(p_mpjpe(rot, gt), 0.0, atol=1e-9)
