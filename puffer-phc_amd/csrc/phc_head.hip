@@ -16,10 +16,13 @@
 // most 80 (5 blocks of 16).
 #include "phc_common.h"
 
+#include <algorithm>
+
 namespace phc {
 
 using hf4 = __attribute__((ext_vector_type(4))) float;
 constexpr int kHeadMaxA = 80;
+constexpr size_t kHeadLdsMax = 160 * 1024;  // LDS per workgroup (MI355X: 160 KB per CU)
 
 __device__ __forceinline__ hf4 head_mfma(float a, float b, hf4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -224,6 +227,86 @@ __global__ __launch_bounds__(256) void k_head_wgrad(const float *__restrict__ dm
     }
 }
 
+// ---- W staged in LDS once per workgroup (persistent over row tiles) ------------------------------
+// Forward: W as [A][H + 4] fp32 in LDS (row stride 16 B off a multiple of 256 B, so the 16 lanes of
+// a ds_read_b128 group, 16 consecutive rows a at the same k, hit 16 distinct 16-B bank slots);
+// every wave then reads its B fragments from LDS instead of re-reading W from L2 per 16 rows.
+constexpr int kHeadFwdWaves = 8;  // LDS-staged forward: 2 waves per SIMD
+
+__global__ __launch_bounds__(kHeadFwdWaves * 64) void k_head_fwd_lds(const float *__restrict__ h, const float *__restrict__ w,
+                                                      const float *__restrict__ b, float *__restrict__ mu, int64_t M,
+                                                      int H, int A) {
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [A][H + 4]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int ld = H + 4;
+  for (int i = threadIdx.x; i < A * (H / 4); i += blockDim.x) {
+    const int a = i / (H / 4), k4 = i - a * (H / 4);
+    *reinterpret_cast<float4 *>(&wl[a * ld + 4 * k4]) = *reinterpret_cast<const float4 *>(w + (int64_t)a * H + 4 * k4);
+  }
+  __syncthreads();
+  int arow[5];
+  bool av[5];
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) {
+    av[nb] = 16 * nb + c < A;
+    arow[nb] = (av[nb] ? 16 * nb + c : 0) * ld + 4 * g;
+  }
+  float bias[5];
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) bias[nb] = av[nb] ? b[16 * nb + c] : 0.0f;
+  const int64_t tiles = (M + 15) / 16;
+  for (int64_t t = (int64_t)blockIdx.x * kHeadFwdWaves + wave; t < tiles; t += (int64_t)gridDim.x * kHeadFwdWaves) {
+    const int64_t r0 = t * 16;
+    int64_t hr = r0 + c;
+    hr = hr < M ? hr : M - 1;
+    const float *hp = h + hr * H + 4 * g;
+    hf4 acc[5];
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) acc[nb] = hf4{0.0f, 0.0f, 0.0f, 0.0f};
+    float4 hv[2];
+    hv[0] = *reinterpret_cast<const float4 *>(hp);
+    for (int k0 = 0; k0 < H; k0 += 32) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int kk = k0 + 16 * half;
+        if (kk >= H) break;
+        if (kk + 16 < H) hv[half ^ 1] = *reinterpret_cast<const float4 *>(hp + kk + 16);
+        float4 wv[5];
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) {
+          wv[nb] = *reinterpret_cast<const float4 *>(&wl[arow[nb] + kk]);
+          if (!av[nb]) wv[nb] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+        const float4 x = hv[half];
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) acc[nb] = head_mfma(x.x, wv[nb].x, acc[nb]);
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) acc[nb] = head_mfma(x.y, wv[nb].y, acc[nb]);
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) acc[nb] = head_mfma(x.z, wv[nb].z, acc[nb]);
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) acc[nb] = head_mfma(x.w, wv[nb].w, acc[nb]);
+      }
+    }
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) {
+      const int a = 16 * nb + c;
+      if (a >= A) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = r0 + 4 * g + e;
+        if (row < M) mu[row * A + a] = acc[nb][e] + bias[nb];
+      }
+    }
+  }
+}
+
+static int head_cus() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return cus;
+}
+
 static int check_head(const void *x, const void *w, int64_t M, int H, int A) {
   PHC_REQUIRE(x && w, "mu_head: null operand");
   PHC_REQUIRE(M > 0 && H > 0 && A >= 1 && A <= kHeadMaxA, "mu_head: bad shape (rows %lld, hidden %d, actions %d <= %d)",
@@ -242,9 +325,23 @@ extern "C" int phc_mu_head_fwd(const float *h, const float *w, const float *b, f
   PHC_REQUIRE(hidden % 16 == 0, "mu_head_fwd: hidden must be a multiple of 16");
   PHC_REQUIRE((reinterpret_cast<uintptr_t>(h) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
               "mu_head_fwd: h and w must be 16-byte aligned");
-  const int64_t blocks = (rows + 63) / 64;
-  hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), h, w, b, mu, rows,
-                     (int)hidden, (int)num_actions);
+  const size_t lds = (size_t)num_actions * (hidden + 4) * sizeof(float);
+  if (lds <= kHeadLdsMax) {  // W staged in LDS, persistent over 16-row tiles
+    static bool attr = [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_head_fwd_lds),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHeadLdsMax);
+      return true;
+    }();
+    (void)attr;
+    const int64_t tiles = (rows + 15) / 16;
+    const int64_t blocks = std::min<int64_t>((tiles + kHeadFwdWaves - 1) / kHeadFwdWaves, head_cus());
+    hipLaunchKernelGGL(k_head_fwd_lds, dim3((unsigned)blocks), dim3(kHeadFwdWaves * 64), lds, as_stream(stream), h, w, b, mu, rows,
+                       (int)hidden, (int)num_actions);
+  } else {
+    const int64_t blocks = (rows + 63) / 64;
+    hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), h, w, b, mu, rows,
+                       (int)hidden, (int)num_actions);
+  }
   return check_launch("mu_head_fwd");
 }
 
