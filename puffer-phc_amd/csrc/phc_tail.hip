@@ -100,16 +100,21 @@ __global__ __launch_bounds__(kFwdThreads) void k_tail_ln_fwd(phc_tail_ln_args a)
     const int64_t row = r0 + q / 2;
     if (row < M) t_load_row(a.trunk_out + ((int64_t)(q % 2) * M + row) * kTH, lane, x[t]);
   }
+  // task q = wave + kWaves t belongs to trunk q % 2 = wave % 2 (kWaves even): one parameter load
+  // per wave, before any store (the stores of h_actor could alias the parameter views)
+  static_assert(kWaves % 2 == 0, "a wave's tasks share one trunk");
+  const int grp = wave % 2;
+  float gm[kTC][4], bt[kTC][4], wv[kTC][4];
+  t_load_param(a.ln_gamma[grp], lane, gm);
+  t_load_param(a.ln_beta[grp], lane, bt);
+  if (grp == 1) t_load_param(a.w_value, lane, wv);
+  const float bv = grp == 1 ? a.b_value[0] : 0.0f;
 #pragma unroll
   for (int t = 0; t < kTasks; ++t) {
     const int q = wave + kWaves * t;
-    const int grp = q % 2;
     const int64_t row = r0 + q / 2;
     if (row >= M) continue;
     const LnStat st = t_ln_stat(x[t], a.ln_eps);
-    float gm[kTC][4], bt[kTC][4];
-    t_load_param(a.ln_gamma[grp], lane, gm);
-    t_load_param(a.ln_beta[grp], lane, bt);
     float h[kTC][4];
 #pragma unroll
     for (int k = 0; k < kTC; ++k)
@@ -124,14 +129,12 @@ __global__ __launch_bounds__(kFwdThreads) void k_tail_ln_fwd(phc_tail_ln_args a)
         *reinterpret_cast<float4 *>(a.h_actor + row * kTH + 4 * (lane + 64 * k)) =
             float4{h[k][0], h[k][1], h[k][2], h[k][3]};
     } else {
-      float wv[kTC][4];
-      t_load_param(a.w_value, lane, wv);
       float s = 0.0f;
 #pragma unroll
       for (int k = 0; k < kTC; ++k)
         s += h[k][0] * wv[k][0] + h[k][1] * wv[k][1] + h[k][2] * wv[k][2] + h[k][3] * wv[k][3];
       s = t_wave_sum(s);
-      if (lane == 0) a.value[row] = s + a.b_value[0];
+      if (lane == 0) a.value[row] = s + bv;
     }
   }
 }

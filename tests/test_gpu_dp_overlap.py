@@ -1,7 +1,8 @@
 """Data-parallel fused minibatch (policies/fused_ppo.py + distributed.FlatGrads overlap): two
 ranks on one GPU over gloo (needs an MI355X), full PHCPolicy widths, 32768-row minibatches per
 rank.  Each rank runs the fused PPO minibatch on its own data with the all-reduces started from
-the backward (twin_mlp.GRAD_READY) — on the grouped weight-gradient path (default: every trunk
+the backward (twin_mlp.GRAD_READY) and the gradients stored into a NaN-filled buffer (store_grads,
+as the trainer runs it) — on the grouped weight-gradient path (default: every trunk
 span after the grouped launch) and on the per-layer path (PHC_DP_PER_LAYER).  Checks:
   * the reduced flat gradient equals the mean of the two ranks' local gradients (fp32 a + b
     summed in either order is the same number: exact up to the final division, tol 1e-6);
@@ -75,10 +76,13 @@ def _worker(rank, world, port, out_dir, per_layer):
 
         def backward(batch, overlap):
             obs, atn, old_lp, adv, val, ret = batch
-            fg.zero()
+            if overlap:  # as clean_pufferl.core.train runs it: gradients stored, the buffer not zeroed
+                fg.flat.fill_(float("nan"))
+            else:
+                fg.zero()
             with torch.autocast("cuda", dtype=torch.float16):
                 xh = pol.obs_half_input(obs)
-                loss, _ = fused_ppo_loss(pol, xh, atn, old_lp, adv, ms, val, ret, coefs)
+                loss, _ = fused_ppo_loss(pol, xh, atn, old_lp, adv, ms, val, ret, coefs, store_grads=overlap)
             if overlap:
                 fg.overlap_begin()
             (loss * 64.0).backward()
