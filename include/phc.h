@@ -181,6 +181,33 @@ int phc_actions_to_pd(const float *actions, float *pd_target, int64_t n, const f
 int phc_physics_replay(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
                        float pos_sigma, float force_scale, uint64_t seed, uint64_t counter, void *stream);
 
+/* N3: articulated-body physics step, replacing `gym.simulate(sim)` x control_freq_inv
+ * (puffer_phc/envs/humanoid_phc.py:129-134; sim params envs/isaacgym_env.py:6-42; PD drives
+ * humanoid_phc.py:274-281; ground plane :255-262).  Featherstone ABA over the 24-body tree (6-DoF
+ * root, 23 ball joints), implicit joint-space PD to pd_target [N,69] (exp-map targets, stiffness /
+ * damping x kp_scale / kd_scale), penalty ground contact with capped viscous friction,
+ * control_freq_inv x substeps semi-implicit Euler substeps of sim_dt / substeps.  Reads the root
+ * record of rigid_body_state and dof_state, writes rigid_body_state [N,24,13], root_state (if set),
+ * dof_state [N,69,2] and dof_force [N,69] (the applied PD torques of the last substep).
+ * body_model: device float [PHC_NUM_BODIES][PHC_BODY_MODEL_STRIDE] (layout in phc_physics.hip,
+ * packed by puffer-phc_amd/physics.py from assets/smpl_body_model.json). */
+#define PHC_BODY_MODEL_STRIDE 64
+typedef struct phc_physics_params {
+  float sim_dt;             /* 1/60 (isaacgym_env.py:38) */
+  int32_t control_freq_inv; /* 2 */
+  int32_t substeps;         /* semi-implicit Euler substeps per sim step */
+  int32_t tree_depth;       /* deepest body level of the model (root = 0), 1..15 */
+  float kp_scale, kd_scale; /* EnvConfig kp_scale / kd_scale */
+  float contact_stiffness;  /* N/m per contact point */
+  float contact_damping;    /* N s/m per contact point */
+  float friction;           /* Coulomb coefficient (ground plane friction 1.0) */
+  float friction_damping;   /* N s/m: tangential force = -min(friction_damping, mu fn / |vt|) vt */
+  float gravity;            /* m/s^2 along z (-9.81) */
+  float reserved;
+} phc_physics_params;
+int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const float *body_model,
+                     const phc_physics_params *p, void *stream);
+
 /* R3-R5: load-time FK + velocities (poselib_skeleton.py:518-619, 1230-1251; motion_lib.py:119-140)
  * for `num_motions` clips packed back to back.  quat_global f64 [F,24,4], root_trans f64 [F,3],
  * starts/counts int64 [num_motions], fps float [num_motions].  Writes lib frames/local_rot/

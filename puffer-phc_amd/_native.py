@@ -58,6 +58,14 @@ class StepParamsC(ctypes.Structure):
                 ("auto_reset", ctypes.c_int32), ("reset_at_start", ctypes.c_int32), ("seed", ctypes.c_uint64)]
 
 
+class PhysicsParamsC(ctypes.Structure):
+    _fields_ = [("sim_dt", ctypes.c_float), ("control_freq_inv", ctypes.c_int32), ("substeps", ctypes.c_int32),
+                ("tree_depth", ctypes.c_int32), ("kp_scale", ctypes.c_float), ("kd_scale", ctypes.c_float),
+                ("contact_stiffness", ctypes.c_float), ("contact_damping", ctypes.c_float),
+                ("friction", ctypes.c_float), ("friction_damping", ctypes.c_float), ("gravity", ctypes.c_float),
+                ("reserved", ctypes.c_float)]
+
+
 class RowFieldC(ctypes.Structure):
     _fields_ = [("src", c_vp), ("dst", c_vp), ("row_elems", c_i64), ("kind", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
@@ -209,6 +217,8 @@ _EXPORTS = {
     "phc_physics_replay": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                            ctypes.POINTER(StepParamsC), ctypes.c_float, ctypes.c_float,
                                            ctypes.c_uint64, ctypes.c_uint64, c_vp]),
+    "phc_physics_step": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), c_vp, c_vp, ctypes.POINTER(PhysicsParamsC),
+                                         c_vp]),
     "phc_fk_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_fk_motions": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
                                        ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -925,6 +935,30 @@ def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):
                                     float(pos_sigma), float(force_scale), ctypes.c_uint64(seed),
                                     ctypes.c_uint64(counter), _stream()),
            "phc_physics_replay")
+
+
+BODY_MODEL_STRIDE = 64
+
+
+def physics_env_struct(rigid_body_state, dof_state, dof_force, root_state=None):
+    """An env struct carrying only the buffers phc_physics_step touches (standalone use / tests)."""
+    n = rigid_body_state.shape[0]
+    e = EnvBuffersC()
+    e.num_envs = n
+    e.rigid_body_state = _ptr(rigid_body_state, torch.float32, (n, NUM_BODIES, BODY_STRIDE), "rigid_body_state")
+    e.root_state = _ptr(root_state, torch.float32, (n, BODY_STRIDE), "root_state", nullable=True)
+    e.dof_state = _ptr(dof_state, torch.float32, (n, NUM_DOF, 2), "dof_state")
+    e.dof_force = _ptr(dof_force, torch.float32, (n, NUM_DOF), "dof_force")
+    return e
+
+
+def physics_step(env_c, pd_target, body_model, params):
+    """N3 articulated-body step (phc_physics_step) over the env buffers of env_c."""
+    n = int(env_c.num_envs)
+    _check(lib().phc_physics_step(ctypes.byref(env_c), _ptr(pd_target, torch.float32, (n, NUM_DOF), "pd_target"),
+                                  _ptr(body_model, torch.float32, (NUM_BODIES, BODY_MODEL_STRIDE), "body_model"),
+                                  ctypes.byref(params), _stream()),
+           "phc_physics_step")
 
 
 def actions_to_pd(actions, pd_out, offset, scale, frozen):

@@ -107,7 +107,10 @@ class EnvConfig(DeviceConfig):
     num_amp_obs_steps: int = 10
     amp_root_height_obs: bool = True
 
-    # physics stand-in (this build only): replayed reference states + gaussian noise
+    # physics: "replay" = the stand-in of BASELINE configs[1] (replayed reference states + gaussian
+    # noise); "articulated" = the N3 articulated-body step (physics.ArticulatedPhysics)
+    physics: Literal["replay", "articulated"] = "replay"
+    physics_substeps: int = 8
     replay_pos_sigma: float = 0.02
     replay_force_scale: float = 50.0
     seed: int = 0

@@ -1,0 +1,462 @@
+// phc_physics.hip — N3: the articulated-body physics step (replaces gym.simulate x control_freq_inv,
+// puffer_phc/envs/humanoid_phc.py:129-134).
+//
+// Model: the SMPL humanoid of assets/smpl_humanoid.xml as a 24-body tree — a 6-DoF floating root and
+// 23 ball joints (the MJCF's three hinges per body, stiffness / damping / armature per axis) — with
+// one collision geom per body (sphere / capsule / box) against the ground plane.  Per substep:
+//   1. forward kinematics, outward: world pose and body-coordinate twist of every body;
+//   2. gravity + penalty ground contact (normal: stiffness x depth - damping x normal velocity,
+//      clamped >= 0; tangential: -min(friction_damping, mu fn / |vt|) vt) as body-coordinate wrenches;
+//      implicit PD torques tau = kp (target - e) - (kd + dt kp) qd, e = rotation vector of the joint;
+//   3. Featherstone's articulated-body algorithm: inward pass of articulated inertias / bias forces
+//      (the joint-space diagonal carries armature + dt kd + dt^2 kp, the implicit-PD term), the
+//      floating root's 6x6 solve, outward pass of accelerations;
+//   4. semi-implicit Euler: velocities, then joint / root rotations (quaternions) and root position.
+// The CPU restatement is oracle/physics_oracle.py (generic 6x6 matrices, float64).
+//
+// Decomposition (MI355X): one 32-lane half-wave per env, lane b = body b (24 of 32 lanes), 8 envs
+// per 256-thread workgroup, as k_env_step.  The tree passes run level-synchronously (depth 8 for
+// SMPL): at level L the lanes of that level read their parent's (outward) or children's (inward)
+// record from the env's LDS slots and write their own; a workgroup barrier separates levels.  All
+// per-body state stays in registers across the substeps; HBM is touched once per env step (read the
+// root record, dof_state and targets; write the 24 rigid-body records, dof_state, dof_force).  The
+// kernel is VALU-latency bound (about 3k VALU instructions per body per substep).
+//
+// Body model row (floats, PHC_BODY_MODEL_STRIDE = 64):
+//   0 parent  1 level  2 num_children  3..5 children  6..8 joint offset (parent coords)  9 mass
+//   10..12 com  13..18 inertia about the com (xx yy zz xy xz yz)  19..21 kp  22..24 kd  25..27 armature
+//   28 num_points  32..63 contact points (x y z radius) x 8
+#include "phc_common.h"
+
+namespace phc {
+
+constexpr int kModel = PHC_BODY_MODEL_STRIDE;
+constexpr int kSlot = 27;  // LDS floats per body: A(6, sym) B(9) M(6, sym) f(6)
+constexpr int kMaxPoints = 8;
+
+struct PhysConsts {
+  float dt;
+  int nsub;
+  int depth;
+  float kp_scale, kd_scale, kn, cn, mu, ct, g;
+};
+
+struct M3 {
+  float m[9];  // row-major
+};
+
+__device__ __forceinline__ M3 m3_quat(float x, float y, float z, float w) {
+  return {{1.0f - 2.0f * (y * y + z * z), 2.0f * (x * y - z * w), 2.0f * (x * z + y * w),
+           2.0f * (x * y + z * w), 1.0f - 2.0f * (x * x + z * z), 2.0f * (y * z - x * w),
+           2.0f * (x * z - y * w), 2.0f * (y * z + x * w), 1.0f - 2.0f * (x * x + y * y)}};
+}
+__device__ __forceinline__ M3 m3_mul(const M3 &a, const M3 &b) {
+  M3 o;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) o.m[3 * i + j] = a.m[3 * i] * b.m[j] + a.m[3 * i + 1] * b.m[3 + j] + a.m[3 * i + 2] * b.m[6 + j];
+  return o;
+}
+__device__ __forceinline__ M3 m3_mul_t(const M3 &a, const M3 &b) {  // a b^T
+  M3 o;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      o.m[3 * i + j] = a.m[3 * i] * b.m[3 * j] + a.m[3 * i + 1] * b.m[3 * j + 1] + a.m[3 * i + 2] * b.m[3 * j + 2];
+  return o;
+}
+__device__ __forceinline__ M3 m3_t(const M3 &a) {
+  return {{a.m[0], a.m[3], a.m[6], a.m[1], a.m[4], a.m[7], a.m[2], a.m[5], a.m[8]}};
+}
+__device__ __forceinline__ M3 m3_add(const M3 &a, const M3 &b) {
+  M3 o;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) o.m[i] = a.m[i] + b.m[i];
+  return o;
+}
+__device__ __forceinline__ M3 m3_sub(const M3 &a, const M3 &b) {
+  M3 o;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) o.m[i] = a.m[i] - b.m[i];
+  return o;
+}
+__device__ __forceinline__ M3 m3_skew(v3 r) { return {{0.0f, -r.z, r.y, r.z, 0.0f, -r.x, -r.y, r.x, 0.0f}}; }
+__device__ __forceinline__ v3 m3_v(const M3 &a, v3 v) {
+  return {a.m[0] * v.x + a.m[1] * v.y + a.m[2] * v.z, a.m[3] * v.x + a.m[4] * v.y + a.m[5] * v.z,
+          a.m[6] * v.x + a.m[7] * v.y + a.m[8] * v.z};
+}
+__device__ __forceinline__ v3 m3_tv(const M3 &a, v3 v) {  // a^T v
+  return {a.m[0] * v.x + a.m[3] * v.y + a.m[6] * v.z, a.m[1] * v.x + a.m[4] * v.y + a.m[7] * v.z,
+          a.m[2] * v.x + a.m[5] * v.y + a.m[8] * v.z};
+}
+__device__ __forceinline__ M3 m3_inv(const M3 &a) {  // adjugate / determinant
+  const float *m = a.m;
+  const float c0 = m[4] * m[8] - m[5] * m[7], c1 = m[5] * m[6] - m[3] * m[8], c2 = m[3] * m[7] - m[4] * m[6];
+  const float id = 1.0f / (m[0] * c0 + m[1] * c1 + m[2] * c2);
+  return {{c0 * id, (m[2] * m[7] - m[1] * m[8]) * id, (m[1] * m[5] - m[2] * m[4]) * id, c1 * id,
+           (m[0] * m[8] - m[2] * m[6]) * id, (m[2] * m[3] - m[0] * m[5]) * id, c2 * id,
+           (m[1] * m[6] - m[0] * m[7]) * id, (m[0] * m[4] - m[1] * m[3]) * id}};
+}
+__device__ __forceinline__ v3 cross3(v3 a, v3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+__device__ __forceinline__ v3 vscale(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+
+__device__ __forceinline__ q4 qmul_std(q4 a, q4 b) {
+  return {a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x,
+          a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+__device__ __forceinline__ q4 qnormalize(q4 q) {
+  const float s = rsqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  return {q.x * s, q.y * s, q.z * s, q.w * s};
+}
+__device__ __forceinline__ q4 quat_from_rotvec(v3 e) {
+  const float th = sqrtf(e.x * e.x + e.y * e.y + e.z * e.z);
+  const float s = th > 1e-8f ? sinf(0.5f * th) / th : 0.5f - th * th / 48.0f;
+  return {e.x * s, e.y * s, e.z * s, cosf(0.5f * th)};
+}
+__device__ __forceinline__ v3 rotvec_of(q4 q) {
+  if (q.w < 0.0f) q = {-q.x, -q.y, -q.z, -q.w};
+  const float sn = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
+  const float th = 2.0f * atan2f(sn, q.w);
+  const float k = sn > 1e-8f ? th / sn : 2.0f / fmaxf(q.w, 1e-30f);
+  return {q.x * k, q.y * k, q.z * k};
+}
+
+// symmetric 3x3 (xx yy zz xy xz yz) <-> full
+__device__ __forceinline__ M3 sym_full(const float *s) { return {{s[0], s[3], s[4], s[3], s[1], s[5], s[4], s[5], s[2]}}; }
+__device__ __forceinline__ void full_sym(const M3 &a, float *s) {
+  s[0] = a.m[0]; s[1] = a.m[4]; s[2] = a.m[8];
+  s[3] = 0.5f * (a.m[1] + a.m[3]); s[4] = 0.5f * (a.m[2] + a.m[6]); s[5] = 0.5f * (a.m[5] + a.m[7]);
+}
+
+struct PhysView {
+  int64_t n;
+  float *rb;
+  float *root;
+  float *dof_state;
+  float *dof_force;
+};
+
+__global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float *__restrict__ model,
+                                                         const float *__restrict__ target, PhysConsts c) {
+  __shared__ float slots[kEnvsPerBlock][kBodies][kSlot];
+  const int lane = threadIdx.x % kGroup, sub = threadIdx.x / kGroup;
+  const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + sub;
+  const bool act = env < e.n && lane < kBodies;
+  const int b = lane < kBodies ? lane : 0;
+  const int64_t ev = env < e.n ? env : e.n - 1;
+  float(*S)[kSlot] = slots[sub];
+
+  // ---- this lane's body (indices clamped: a corrupt model cannot address outside the slots)
+  const float *md = model + b * kModel;
+  const int parent = min(max((int)md[0], 0), kBodies - 1);
+  const int level = act ? (int)md[1] : -1;
+  const int nch = min(max((int)md[2], 0), 3);
+  int ch[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) ch[k] = min(max((int)md[3 + k], 0), kBodies - 1);
+  const v3 off = {md[6], md[7], md[8]};
+  const float mass = md[9];
+  const v3 com = {md[10], md[11], md[12]};
+  v3 kp = {md[19] * c.kp_scale, md[20] * c.kp_scale, md[21] * c.kp_scale};
+  v3 kd = {md[22] * c.kd_scale, md[23] * c.kd_scale, md[24] * c.kd_scale};
+  const float dt = c.dt;
+  const v3 dext = {md[25] + dt * kd.x + dt * dt * kp.x, md[26] + dt * kd.y + dt * dt * kp.y,
+                   md[27] + dt * kd.z + dt * dt * kp.z};
+  const int npts = min(max((int)md[28], 0), kMaxPoints);
+  // spatial inertia about the body origin: [[A0, B0], [B0^T, m 1]], A0 = Ic + m C C^T, B0 = m C
+  M3 A0, B0;
+  {
+    const M3 C = m3_skew(com);
+    const M3 Ic = sym_full(md + 13), CC = m3_mul_t(C, C);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      A0.m[i] = Ic.m[i] + mass * CC.m[i];
+      B0.m[i] = mass * C.m[i];
+    }
+  }
+
+  // ---- state: root (lane 0) in body coordinates, joints (lanes >= 1)
+  q4 r = {0.0f, 0.0f, 0.0f, 1.0f};
+  v3 om = {0.0f, 0.0f, 0.0f}, tgt = {0.0f, 0.0f, 0.0f};
+  v3 p0 = {0.0f, 0.0f, 0.0f}, w0 = {0.0f, 0.0f, 0.0f}, v0 = {0.0f, 0.0f, 0.0f};
+  q4 q0 = {0.0f, 0.0f, 0.0f, 1.0f};
+  if (act && b == 0) {
+    const float *s = e.rb + ev * kBodies * kRec;
+    p0 = {s[0], s[1], s[2]};
+    q0 = qnormalize(q4{s[3], s[4], s[5], s[6]});
+    const M3 R0 = m3_quat(q0.x, q0.y, q0.z, q0.w);
+    v0 = m3_tv(R0, v3{s[7], s[8], s[9]});
+    w0 = m3_tv(R0, v3{s[10], s[11], s[12]});
+  } else if (act) {
+    const float *d = e.dof_state + (ev * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+    r = quat_from_rotvec(v3{d[0], d[2], d[4]});
+    om = {d[1], d[3], d[5]};
+    const float *t = target + ev * PHC_NUM_DOF + 3 * (b - 1);
+    tgt = {t[0], t[1], t[2]};
+  }
+
+  q4 Q = {0.0f, 0.0f, 0.0f, 1.0f};
+  M3 R = m3_quat(0.0f, 0.0f, 0.0f, 1.0f);
+  v3 P = {0.0f, 0.0f, 0.0f}, w = P, v = P;
+  // outward pass: world quaternion / rotation / origin and body twist of every body
+  auto kinematics = [&]() {
+    for (int L = 0; L <= c.depth; ++L) {
+      if (level == L) {
+        if (b == 0) {
+          Q = q0; P = p0; w = w0; v = v0;
+        } else {
+          const float *ps = S[parent];
+          const q4 Qp = {ps[0], ps[1], ps[2], ps[3]};
+          const v3 Pp = {ps[4], ps[5], ps[6]}, wp = {ps[7], ps[8], ps[9]}, vp = {ps[10], ps[11], ps[12]};
+          Q = qmul_std(Qp, r);
+          P = vadd(Pp, m3_v(m3_quat(Qp.x, Qp.y, Qp.z, Qp.w), off));
+          const M3 E = m3_quat(r.x, r.y, r.z, r.w);
+          w = vadd(m3_tv(E, wp), om);
+          v = m3_tv(E, vsub(vp, cross3(off, wp)));
+        }
+        R = m3_quat(Q.x, Q.y, Q.z, Q.w);
+        float *s = S[b];
+        s[0] = Q.x; s[1] = Q.y; s[2] = Q.z; s[3] = Q.w;
+        s[4] = P.x; s[5] = P.y; s[6] = P.z;
+        s[7] = w.x; s[8] = w.y; s[9] = w.z;
+        s[10] = v.x; s[11] = v.y; s[12] = v.z;
+      }
+      __syncthreads();
+    }
+  };
+
+  v3 applied = {0.0f, 0.0f, 0.0f};
+  for (int it = 0; it < c.nsub; ++it) {
+    kinematics();
+    // ---- external wrench (body coordinates, about the origin): gravity and ground contact
+    v3 fn_ = {0.0f, 0.0f, 0.0f}, ff = {0.0f, 0.0f, 0.0f};
+    v3 tau = {0.0f, 0.0f, 0.0f}, cw = {0.0f, 0.0f, 0.0f}, cv = {0.0f, 0.0f, 0.0f};
+    {
+      const v3 F = m3_tv(R, v3{0.0f, 0.0f, mass * c.g});
+      fn_ = cross3(com, F);
+      ff = F;
+      const v3 zb = {R.m[6], R.m[7], R.m[8]};  // R^T z
+      for (int k = 0; k < npts; ++k) {
+        const float *pt = md + 32 + 4 * k;
+        const v3 cp = {pt[0], pt[1], pt[2]};
+        const float rho = pt[3];
+        const float d = rho - (P.z + R.m[6] * cp.x + R.m[7] * cp.y + R.m[8] * cp.z);
+        if (d > 0.0f) {
+          const v3 a = vsub(cp, vscale(zb, rho));
+          const v3 vw = m3_v(R, vadd(v, cross3(w, a)));
+          const float fn = fmaxf(0.0f, c.kn * d - c.cn * vw.z);
+          const float vt = sqrtf(vw.x * vw.x + vw.y * vw.y);
+          const float kt = fminf(c.ct, c.mu * fn / fmaxf(vt, 1e-12f));
+          const v3 Fb = m3_tv(R, v3{-kt * vw.x, -kt * vw.y, fn});
+          fn_ = vadd(fn_, cross3(a, Fb));
+          ff = vadd(ff, Fb);
+        }
+      }
+      if (b > 0) {
+        const v3 ej = rotvec_of(r);
+        tau = {kp.x * (tgt.x - ej.x) - (kd.x + dt * kp.x) * om.x, kp.y * (tgt.y - ej.y) - (kd.y + dt * kp.y) * om.y,
+               kp.z * (tgt.z - ej.z) - (kd.z + dt * kp.z) * om.z};
+        cw = cross3(w, om);
+        cv = cross3(v, om);
+      }
+    }
+    // ---- bias force p = V x* (I V) - f_ext; articulated inertia starts as the body's own
+    M3 A = A0, B = B0, M = {{mass, 0.0f, 0.0f, 0.0f, mass, 0.0f, 0.0f, 0.0f, mass}};
+    v3 pt_, pb_;
+    {
+      const v3 h = vadd(m3_v(A0, w), m3_v(B0, v));
+      const v3 l = vadd(m3_tv(B0, w), vscale(v, mass));
+      pt_ = vsub(vadd(cross3(w, h), cross3(v, l)), fn_);
+      pb_ = vsub(cross3(w, l), ff);
+    }
+    M3 Dinv = {};
+    v3 u = {0.0f, 0.0f, 0.0f};
+    auto gather_children = [&]() {
+      for (int k = 0; k < nch; ++k) {
+        const float *s = S[ch[k]];
+        const M3 As = sym_full(s), Ms = sym_full(s + 15);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+          A.m[i] += As.m[i];
+          B.m[i] += s[6 + i];
+          M.m[i] += Ms.m[i];
+        }
+        pt_ = vadd(pt_, v3{s[21], s[22], s[23]});
+        pb_ = vadd(pb_, v3{s[24], s[25], s[26]});
+      }
+    };
+    // ---- inward pass
+    for (int L = c.depth; L >= 1; --L) {
+      if (level == L) {
+        gather_children();
+        M3 D = A;
+        D.m[0] += dext.x; D.m[4] += dext.y; D.m[8] += dext.z;
+        Dinv = m3_inv(D);
+        u = vsub(tau, pt_);
+        const M3 K = m3_mul(Dinv, A), Lm = m3_mul(Dinv, B);
+        const M3 Aa = m3_sub(A, m3_mul(A, K));
+        const M3 Ba = m3_sub(B, m3_mul(A, Lm));
+        const M3 Ma = m3_sub(M, m3_mul(m3_t(B), Lm));
+        const v3 y = m3_v(Dinv, u);
+        const v3 pat = vadd(vadd(pt_, vadd(m3_v(Aa, cw), m3_v(Ba, cv))), m3_v(A, y));
+        const v3 pab = vadd(vadd(pb_, vadd(m3_tv(Ba, cw), m3_v(Ma, cv))), m3_tv(B, y));
+        // to parent coordinates: rotate by E, then shift by the joint offset
+        const M3 E = m3_quat(r.x, r.y, r.z, r.w);
+        const M3 Ar = m3_mul_t(m3_mul(E, Aa), E), Br = m3_mul_t(m3_mul(E, Ba), E), Mr = m3_mul_t(m3_mul(E, Ma), E);
+        const M3 Rx = m3_skew(off);
+        const M3 BR = m3_mul(Br, Rx), RBt = m3_mul_t(Rx, Br), RM = m3_mul(Rx, Mr);
+        const M3 Ap = m3_sub(m3_add(m3_sub(Ar, BR), RBt), m3_mul(RM, Rx));
+        const M3 Bp = m3_add(Br, RM);
+        const v3 Fp = m3_v(E, pab);
+        const v3 Np = vadd(m3_v(E, pat), cross3(off, Fp));
+        float *s = S[b];
+        full_sym(Ap, s);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) s[6 + i] = Bp.m[i];
+        full_sym(Mr, s + 15);
+        s[21] = Np.x; s[22] = Np.y; s[23] = Np.z;
+        s[24] = Fp.x; s[25] = Fp.y; s[26] = Fp.z;
+      }
+      __syncthreads();
+    }
+    // ---- floating root: a0 = -IA^-1 pA (6x6 Cholesky on lane 0)
+    v3 aw = {0.0f, 0.0f, 0.0f}, av = {0.0f, 0.0f, 0.0f};
+    if (level == 0) {
+      gather_children();
+      float G[6][6], rhs[6];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          G[i][j] = A.m[3 * i + j];
+          G[i][3 + j] = B.m[3 * i + j];
+          G[3 + i][j] = B.m[3 * j + i];
+          G[3 + i][3 + j] = M.m[3 * i + j];
+        }
+      rhs[0] = -pt_.x; rhs[1] = -pt_.y; rhs[2] = -pt_.z; rhs[3] = -pb_.x; rhs[4] = -pb_.y; rhs[5] = -pb_.z;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        float d = G[j][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) d -= G[j][k] * G[j][k];
+        const float ljj = sqrtf(fmaxf(d, 1e-20f)), il = 1.0f / ljj;
+        G[j][j] = ljj;
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+          float s = G[i][j];
+#pragma unroll
+          for (int k = 0; k < j; ++k) s -= G[i][k] * G[j][k];
+          G[i][j] = s * il;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {  // L y = rhs
+        float s = rhs[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) s -= G[i][k] * rhs[k];
+        rhs[i] = s / G[i][i];
+      }
+#pragma unroll
+      for (int i = 5; i >= 0; --i) {  // L^T x = y
+        float s = rhs[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; ++k) s -= G[k][i] * rhs[k];
+        rhs[i] = s / G[i][i];
+      }
+      aw = {rhs[0], rhs[1], rhs[2]};
+      av = {rhs[3], rhs[4], rhs[5]};
+      float *s = S[0];
+      s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
+    }
+    __syncthreads();
+    // ---- outward pass: accelerations and joint accelerations
+    v3 qdd = {0.0f, 0.0f, 0.0f};
+    for (int L = 1; L <= c.depth; ++L) {
+      if (level == L) {
+        const float *ps = S[parent];
+        const v3 apw = {ps[0], ps[1], ps[2]}, apv = {ps[3], ps[4], ps[5]};
+        const M3 E = m3_quat(r.x, r.y, r.z, r.w);
+        aw = vadd(m3_tv(E, apw), cw);
+        av = vadd(m3_tv(E, vsub(apv, cross3(off, apw))), cv);
+        const v3 ua = vadd(m3_v(A, aw), m3_v(B, av));  // U^T a' (A symmetric)
+        qdd = m3_v(Dinv, vsub(u, ua));
+        aw = vadd(aw, qdd);
+        float *s = S[b];
+        s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
+      }
+      __syncthreads();
+    }
+    // ---- semi-implicit Euler
+    if (act && b > 0) {
+      applied = {tau.x - dt * (kd.x + dt * kp.x) * qdd.x, tau.y - dt * (kd.y + dt * kp.y) * qdd.y,
+                 tau.z - dt * (kd.z + dt * kp.z) * qdd.z};
+      om = vadd(om, vscale(qdd, dt));
+      r = qnormalize(qmul_std(r, quat_from_rotvec(vscale(om, dt))));
+    } else if (act) {
+      w0 = vadd(w0, vscale(aw, dt));
+      v0 = vadd(v0, vscale(av, dt));
+      p0 = vadd(p0, vscale(m3_v(R, v0), dt));
+      q0 = qnormalize(qmul_std(q0, quat_from_rotvec(vscale(w0, dt))));
+    }
+  }
+  kinematics();
+  if (!act) return;  // no barrier follows
+  {
+    const v3 vw = m3_v(R, v), ww = m3_v(R, w);
+    float *o = e.rb + (env * kBodies + b) * kRec;
+    o[0] = P.x; o[1] = P.y; o[2] = P.z;
+    o[3] = Q.x; o[4] = Q.y; o[5] = Q.z; o[6] = Q.w;
+    o[7] = vw.x; o[8] = vw.y; o[9] = vw.z;
+    o[10] = ww.x; o[11] = ww.y; o[12] = ww.z;
+    if (b == 0 && e.root) {
+      float *rt = e.root + env * kRec;
+#pragma unroll
+      for (int k = 0; k < kRec; ++k) rt[k] = o[k];
+    }
+  }
+  if (b > 0) {
+    const v3 ej = rotvec_of(r);
+    float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+    d[0] = ej.x; d[1] = om.x; d[2] = ej.y; d[3] = om.y; d[4] = ej.z; d[5] = om.z;
+    float *f = e.dof_force + env * PHC_NUM_DOF + 3 * (b - 1);
+    f[0] = applied.x; f[1] = applied.y; f[2] = applied.z;
+  }
+}
+
+}  // namespace phc
+
+using namespace phc;
+
+extern "C" int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const float *body_model,
+                                const phc_physics_params *p, void *stream) {
+  PHC_REQUIRE(env && env->num_envs > 0, "physics_step: num_envs must be > 0");
+  PHC_REQUIRE(env->rigid_body_state && env->dof_state && env->dof_force, "physics_step: null env buffer");
+  PHC_REQUIRE(pd_target && body_model && p, "physics_step: null target / model / params");
+  PHC_REQUIRE(p->sim_dt > 0.0f && p->control_freq_inv >= 1 && p->substeps >= 1 && p->substeps <= 1024 &&
+                  p->control_freq_inv <= 64,
+              "physics_step: bad time stepping (sim_dt %g, control_freq_inv %d, substeps %d)", (double)p->sim_dt,
+              p->control_freq_inv, p->substeps);
+  PHC_REQUIRE(p->tree_depth >= 1 && p->tree_depth <= 15, "physics_step: tree_depth must be 1..15");
+  PHC_REQUIRE(p->contact_stiffness >= 0.0f && p->contact_damping >= 0.0f && p->friction >= 0.0f &&
+                  p->friction_damping >= 0.0f,
+              "physics_step: contact coefficients must be >= 0");
+  PhysConsts c;
+  c.dt = p->sim_dt / (float)p->substeps;
+  c.nsub = p->control_freq_inv * p->substeps;
+  c.depth = p->tree_depth;
+  c.kp_scale = p->kp_scale;
+  c.kd_scale = p->kd_scale;
+  c.kn = p->contact_stiffness;
+  c.cn = p->contact_damping;
+  c.mu = p->friction;
+  c.ct = p->friction_damping;
+  c.g = p->gravity;
+  const PhysView v = {env->num_envs, env->rigid_body_state, env->root_state, env->dof_state,
+                       const_cast<float *>(env->dof_force)};  // read-only for the env step, written here
+  const int64_t blocks = (env->num_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  hipLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kBlock), 0, as_stream(stream), v, body_model,
+                     pd_target, c);
+  return check_launch("physics_step");
+}

@@ -2,8 +2,10 @@
 
 Per step (HumanoidPHC.step, :105-172) the env launches, on the current HIP stream:
   phc_actions_to_pd  (R13)  action -> PD target
-  physics            stand-in: `ReplayPhysics` (BASELINE configs[1], "physics stubbed with
-                     replayed rigid-body states"); a real simulator writes the same buffers
+  physics            `ReplayPhysics` (BASELINE configs[1], "physics stubbed with replayed rigid-body
+                     states"; the default) or `physics.ArticulatedPhysics` (N3, cfg.physics =
+                     "articulated": phc_physics_step, the articulated-body PD step); both write the
+                     same buffers
   phc_env_step       (R6,R7,R9-R12,R14) progress, reward(t), reset(t), obs(t+dt) and the
                      PufferEnv bookkeeping, fused in one kernel
 and `reset_done()` / `reset(env_ids)` (R15) re-initialises terminated envs from the motion
@@ -73,6 +75,11 @@ class HumanoidPHC:
         self._config_env()
         self._define_gym_spaces()
         self._setup_env_buffers()
+        if physics is None and cfg.physics == "articulated":
+            from ..physics import ArticulatedPhysics, PhysicsConfig
+
+            physics = ArticulatedPhysics(PhysicsConfig(substeps=cfg.physics_substeps, kp_scale=cfg.kp_scale,
+                                                       kd_scale=cfg.kd_scale), device=self.device)
         self.physics = physics or ReplayPhysics(cfg.replay_pos_sigma, cfg.replay_force_scale, cfg.seed)
         self._rng_seed = int(cfg.seed) * 7919 + 17
         self._rng_counter = 0

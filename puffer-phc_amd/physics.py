@@ -1,0 +1,127 @@
+"""N3: the articulated-body physics step on the HIP path (phc_physics_step), a drop-in for the
+reference's `gym.simulate(sim)` x control_freq_inv (puffer_phc/envs/humanoid_phc.py:129-134).
+
+`BodyModel` packs the SMPL humanoid's physical model (assets/smpl_body_model.json, extracted from the
+reference's assets/smpl_humanoid.xml by tools/make_body_model.py) into the device table the kernel
+reads; `ArticulatedPhysics` is the physics object `HumanoidPHC` steps after writing its PD targets,
+in place of the replay stand-in (`HumanoidPHC(cfg, physics=ArticulatedPhysics(cfg))`).  The
+simulator's settings follow the reference where it states them (sim_dt 1/60 and control_freq_inv 2,
+envs/isaacgym_env.py:6-42; PD gains x kp_scale / kd_scale, humanoid_phc.py:274-281; ground friction
+1, :255-262); the contact model and the substep count are this solver's own (PhysX's TGS solver is a
+closed binary) and documented in DESIGN.md §8.
+"""
+
+import json
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native
+
+MODEL_JSON = os.path.join(os.path.dirname(__file__), "assets", "smpl_body_model.json")
+MAX_POINTS = 8
+
+
+@dataclass
+class PhysicsConfig:
+    sim_dt: float = 1.0 / 60.0
+    control_freq_inv: int = 2
+    substeps: int = 8
+    kp_scale: float = 1.0
+    kd_scale: float = 1.0
+    contact_stiffness: float = 5.0e4
+    contact_damping: float = 1.0e3
+    friction: float = 1.0
+    friction_damping: float = 1.0e3
+    gravity: float = -9.81
+
+
+def contact_points(shape):
+    """Contact points (x, y, z, radius) of one geom in body coordinates: a sphere's centre, a
+    capsule's two end-sphere centres, a box's 8 corners (radius 0)."""
+    if shape["type"] == "sphere":
+        return [list(shape["center"]) + [shape["radius"]]]
+    if shape["type"] == "capsule":
+        return [list(shape["p0"]) + [shape["radius"]], list(shape["p1"]) + [shape["radius"]]]
+    if shape["type"] == "box":
+        c, h = np.asarray(shape["center"]), np.asarray(shape["half"])
+        return [list(c + h * np.array([sx, sy, sz])) + [0.0] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]
+    raise ValueError(f"unsupported geom type {shape['type']!r}")
+
+
+class BodyModel:
+    """The [24, 64] float32 body table of phc_physics.hip (row layout documented there)."""
+
+    def __init__(self, path=MODEL_JSON, device="cuda"):
+        with open(path) as f:
+            d = json.load(f)
+        bodies = d["bodies"]
+        n = len(bodies)
+        if n != _native.NUM_BODIES:
+            raise ValueError(f"body model has {n} bodies, the kernels are built for {_native.NUM_BODIES}")
+        level = [0] * n
+        children = [[] for _ in range(n)]
+        for i, b in enumerate(bodies):
+            p = b["parent"]
+            if i == 0:
+                if p != -1:
+                    raise ValueError("body 0 must be the root")
+                continue
+            if not 0 <= p < i:
+                raise ValueError(f"body {i}: parent {p} must precede it")
+            level[i] = level[p] + 1
+            children[p].append(i)
+        if max(len(c) for c in children) > 3:
+            raise ValueError("at most 3 children per body")
+        self.depth = max(level)
+        if not 1 <= self.depth <= 15:
+            raise ValueError(f"tree depth {self.depth} outside 1..15")
+        t = np.zeros((n, _native.BODY_MODEL_STRIDE), dtype=np.float32)
+        for i, b in enumerate(bodies):
+            I = np.asarray(b["inertia"])
+            pts = contact_points(b["shape"])
+            if len(pts) > MAX_POINTS:
+                raise ValueError(f"body {i}: more than {MAX_POINTS} contact points")
+            t[i, 0] = max(b["parent"], 0)
+            t[i, 1] = level[i]
+            t[i, 2] = len(children[i])
+            t[i, 3:3 + len(children[i])] = children[i]
+            t[i, 6:9] = b["offset"]
+            t[i, 9] = b["mass"]
+            t[i, 10:13] = b["com"]
+            t[i, 13:19] = [I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]]
+            t[i, 19:22] = b["kp"]
+            t[i, 22:25] = b["kd"]
+            t[i, 25:28] = b["armature"]
+            t[i, 28] = len(pts)
+            t[i, 32:32 + 4 * len(pts)] = np.asarray(pts, dtype=np.float32).reshape(-1)
+        self.names = [b["name"] for b in bodies]
+        self.total_mass = float(sum(b["mass"] for b in bodies))
+        self.host = t
+        self.table = torch.from_numpy(t).to(device)
+
+
+class ArticulatedPhysics:
+    """Physics object for HumanoidPHC: one phc_physics_step launch per env step (control_freq_inv
+    sim steps of `substeps` substeps) on the env's rigid-body / dof buffers and PD targets."""
+
+    def __init__(self, config=None, kp_scale=None, kd_scale=None, model=None, device="cuda"):
+        self.config = config or PhysicsConfig()
+        if kp_scale is not None:
+            self.config.kp_scale = kp_scale
+        if kd_scale is not None:
+            self.config.kd_scale = kd_scale
+        self.model = model or BodyModel(device=device)
+        self.params = self._params()
+
+    def _params(self):
+        c = self.config
+        return _native.PhysicsParamsC(float(c.sim_dt), int(c.control_freq_inv), int(c.substeps), int(self.model.depth),
+                                      float(c.kp_scale), float(c.kd_scale), float(c.contact_stiffness),
+                                      float(c.contact_damping), float(c.friction), float(c.friction_damping),
+                                      float(c.gravity), 0.0)
+
+    def step(self, env):
+        _native.physics_step(env._env_c, env.pd_target, self.model.table, self.params)
