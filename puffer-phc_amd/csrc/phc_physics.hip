@@ -30,7 +30,16 @@
 
 namespace phc {
 
+#ifndef PHC_PHYS_EPB
+#define PHC_PHYS_EPB 2  // envs per workgroup (half-waves): one wave per workgroup (measured: 8 -> 750 us, 4 -> 711 us, 2 -> 631 us per 4096-env step)
+#endif
+#ifndef PHC_PHYS_WAVES_PER_SIMD
+#define PHC_PHYS_WAVES_PER_SIMD 1  // occupancy hint to the register allocator
+#endif
+
 constexpr int kModel = PHC_BODY_MODEL_STRIDE;
+constexpr int kPhysEnvs = PHC_PHYS_EPB;
+constexpr int kPhysBlock = kPhysEnvs * kGroup;
 constexpr int kSlot = 27;  // LDS floats per body: A(6, sym) B(9) M(6, sym) f(6)
 constexpr int kMaxPoints = 8;
 
@@ -115,6 +124,15 @@ __device__ __forceinline__ q4 quat_from_rotvec(v3 e) {
   const float s = th > 1e-8f ? sinf(0.5f * th) / th : 0.5f - th * th / 48.0f;
   return {e.x * s, e.y * s, e.z * s, cosf(0.5f * th)};
 }
+// exp of a substep's rotation increment (|e| = |omega| dt, small): series to theta^4 below 0.25 rad
+// (truncation < 3e-9, below fp32 rounding), the exact form above
+__device__ __forceinline__ q4 quat_exp_increment(v3 e) {
+  const float t2 = e.x * e.x + e.y * e.y + e.z * e.z;
+  if (t2 > 0.0625f) return quat_from_rotvec(e);
+  const float s = 0.5f - t2 * (1.0f / 48.0f) + t2 * t2 * (1.0f / 3840.0f);
+  const float c = 1.0f - t2 * 0.125f + t2 * t2 * (1.0f / 384.0f);
+  return {e.x * s, e.y * s, e.z * s, c};
+}
 __device__ __forceinline__ v3 rotvec_of(q4 q) {
   if (q.w < 0.0f) q = {-q.x, -q.y, -q.z, -q.w};
   const float sn = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
@@ -138,44 +156,73 @@ struct PhysView {
   float *dof_force;
 };
 
-__global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float *__restrict__ model,
-                                                         const float *__restrict__ target, PhysConsts c) {
-  __shared__ float slots[kEnvsPerBlock][kBodies][kSlot];
+// Per-block LDS: the body table with the derived constants (row stride 65 floats: lanes b = 0..23
+// reading the same field hit 24 distinct banks), per env the tree-pass slots (FK record 13 / inward
+// contribution 27 / acceleration 6 floats) and each body's outward-pass operands K = D^-1 A,
+// L = D^-1 B, y = D^-1 u (21 floats), so they do not occupy registers between the passes.
+constexpr int kTab = 65;
+enum : int {
+  T_PARENT = 0, T_LEVEL = 1, T_NCH = 2, T_CH = 3, T_OFF = 6, T_MASS = 9, T_COM = 10, T_A0 = 13 /* 9, full */,
+  T_KP = 22, T_KD = 25, T_DEXT = 28, T_NPTS = 31, T_PTS = 32 /* 32 */
+};
+constexpr int kOut = 21;
+
+__device__ __forceinline__ v3 ld3(const float *p) { return {p[0], p[1], p[2]}; }
+__device__ __forceinline__ M3 ld9(const float *p) {
+  M3 o;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) o.m[i] = p[i];
+  return o;
+}
+
+__global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics_step(
+    PhysView e, const float *__restrict__ model, const float *__restrict__ target, PhysConsts c) {
+  __shared__ float tab[kBodies * kTab];
+  __shared__ float slots[kPhysEnvs][kBodies][kSlot];
+  __shared__ float outw[kPhysEnvs][kBodies][kOut];
   const int lane = threadIdx.x % kGroup, sub = threadIdx.x / kGroup;
-  const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + sub;
+  const int64_t env = (int64_t)blockIdx.x * kPhysEnvs + sub;
   const bool act = env < e.n && lane < kBodies;
   const int b = lane < kBodies ? lane : 0;
   const int64_t ev = env < e.n ? env : e.n - 1;
   float(*S)[kSlot] = slots[sub];
-
-  // ---- this lane's body (indices clamped: a corrupt model cannot address outside the slots)
-  const float *md = model + b * kModel;
-  const int parent = min(max((int)md[0], 0), kBodies - 1);
-  const int level = act ? (int)md[1] : -1;
-  const int nch = min(max((int)md[2], 0), 3);
-  int ch[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) ch[k] = min(max((int)md[3 + k], 0), kBodies - 1);
-  const v3 off = {md[6], md[7], md[8]};
-  const float mass = md[9];
-  const v3 com = {md[10], md[11], md[12]};
-  v3 kp = {md[19] * c.kp_scale, md[20] * c.kp_scale, md[21] * c.kp_scale};
-  v3 kd = {md[22] * c.kd_scale, md[23] * c.kd_scale, md[24] * c.kd_scale};
+  float(*O)[kOut] = outw[sub];
   const float dt = c.dt;
-  const v3 dext = {md[25] + dt * kd.x + dt * dt * kp.x, md[26] + dt * kd.y + dt * dt * kp.y,
-                   md[27] + dt * kd.z + dt * dt * kp.z};
-  const int npts = min(max((int)md[28], 0), kMaxPoints);
-  // spatial inertia about the body origin: [[A0, B0], [B0^T, m 1]], A0 = Ic + m C C^T, B0 = m C
-  M3 A0, B0;
-  {
-    const M3 C = m3_skew(com);
-    const M3 Ic = sym_full(md + 13), CC = m3_mul_t(C, C);
+
+  // ---- body table (indices clamped: a corrupt model cannot address outside the slots)
+  if (threadIdx.x < kBodies) {
+    const float *md = model + threadIdx.x * kModel;
+    float *t = tab + threadIdx.x * kTab;
+    t[T_PARENT] = (float)min(max((int)md[0], 0), kBodies - 1);
+    t[T_LEVEL] = md[1];
+    t[T_NCH] = (float)min(max((int)md[2], 0), 3);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      A0.m[i] = Ic.m[i] + mass * CC.m[i];
-      B0.m[i] = mass * C.m[i];
+    for (int k = 0; k < 3; ++k) t[T_CH + k] = (float)min(max((int)md[3 + k], 0), kBodies - 1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[T_OFF + k] = md[6 + k];
+    const float mass = md[9];
+    t[T_MASS] = mass;
+    const v3 com = ld3(md + 10);
+    t[T_COM] = com.x; t[T_COM + 1] = com.y; t[T_COM + 2] = com.z;
+    // spatial inertia about the origin: [[A0, m C], [m C^T, m 1]], A0 = Ic + m C C^T
+    const M3 C = m3_skew(com), Ic = sym_full(md + 13), CC = m3_mul_t(C, C);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t[T_A0 + i] = Ic.m[i] + mass * CC.m[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float kp = md[19 + k] * c.kp_scale, kd = md[22 + k] * c.kd_scale;
+      t[T_KP + k] = kp;
+      t[T_KD + k] = kd;
+      t[T_DEXT + k] = md[25 + k] + dt * kd + dt * dt * kp;
     }
+    const int npts = min(max((int)md[28], 0), kMaxPoints);
+    t[T_NPTS] = (float)npts;
+    for (int k = 0; k < 4 * kMaxPoints; ++k) t[T_PTS + k] = md[32 + k];
   }
+  __syncthreads();
+  const float *T = tab + b * kTab;
+  const int parent = (int)T[T_PARENT];
+  const int level = act ? (int)T[T_LEVEL] : -1;
 
   // ---- state: root (lane 0) in body coordinates, joints (lanes >= 1)
   q4 r = {0.0f, 0.0f, 0.0f, 1.0f};
@@ -198,9 +245,8 @@ __global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float
   }
 
   q4 Q = {0.0f, 0.0f, 0.0f, 1.0f};
-  M3 R = m3_quat(0.0f, 0.0f, 0.0f, 1.0f);
   v3 P = {0.0f, 0.0f, 0.0f}, w = P, v = P;
-  // outward pass: world quaternion / rotation / origin and body twist of every body
+  // outward pass: world quaternion / origin and body twist of every body
   auto kinematics = [&]() {
     for (int L = 0; L <= c.depth; ++L) {
       if (level == L) {
@@ -209,14 +255,13 @@ __global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float
         } else {
           const float *ps = S[parent];
           const q4 Qp = {ps[0], ps[1], ps[2], ps[3]};
-          const v3 Pp = {ps[4], ps[5], ps[6]}, wp = {ps[7], ps[8], ps[9]}, vp = {ps[10], ps[11], ps[12]};
+          const v3 wp = ld3(ps + 7), off = ld3(T + T_OFF);
           Q = qmul_std(Qp, r);
-          P = vadd(Pp, m3_v(m3_quat(Qp.x, Qp.y, Qp.z, Qp.w), off));
+          P = vadd(ld3(ps + 4), m3_v(m3_quat(Qp.x, Qp.y, Qp.z, Qp.w), off));
           const M3 E = m3_quat(r.x, r.y, r.z, r.w);
           w = vadd(m3_tv(E, wp), om);
-          v = m3_tv(E, vsub(vp, cross3(off, wp)));
+          v = m3_tv(E, vsub(ld3(ps + 10), cross3(off, wp)));
         }
-        R = m3_quat(Q.x, Q.y, Q.z, Q.w);
         float *s = S[b];
         s[0] = Q.x; s[1] = Q.y; s[2] = Q.z; s[3] = Q.w;
         s[4] = P.x; s[5] = P.y; s[6] = P.z;
@@ -230,17 +275,19 @@ __global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float
   v3 applied = {0.0f, 0.0f, 0.0f};
   for (int it = 0; it < c.nsub; ++it) {
     kinematics();
-    // ---- external wrench (body coordinates, about the origin): gravity and ground contact
-    v3 fn_ = {0.0f, 0.0f, 0.0f}, ff = {0.0f, 0.0f, 0.0f};
-    v3 tau = {0.0f, 0.0f, 0.0f}, cw = {0.0f, 0.0f, 0.0f}, cv = {0.0f, 0.0f, 0.0f};
+    // ---- bias force pA = V x* (I V) - f_ext (gravity + ground contact), body coordinates
+    v3 pt_, pb_, tau = {0.0f, 0.0f, 0.0f}, cw = {0.0f, 0.0f, 0.0f}, cv = {0.0f, 0.0f, 0.0f};
     {
+      const M3 R = m3_quat(Q.x, Q.y, Q.z, Q.w);
+      const float mass = T[T_MASS];
+      const v3 com = ld3(T + T_COM);
       const v3 F = m3_tv(R, v3{0.0f, 0.0f, mass * c.g});
-      fn_ = cross3(com, F);
-      ff = F;
+      v3 fn_ = cross3(com, F), ff = F;
       const v3 zb = {R.m[6], R.m[7], R.m[8]};  // R^T z
+      const int npts = (int)T[T_NPTS];
       for (int k = 0; k < npts; ++k) {
-        const float *pt = md + 32 + 4 * k;
-        const v3 cp = {pt[0], pt[1], pt[2]};
+        const float *pt = T + T_PTS + 4 * k;
+        const v3 cp = ld3(pt);
         const float rho = pt[3];
         const float d = rho - (P.z + R.m[6] * cp.x + R.m[7] * cp.y + R.m[8] * cp.z);
         if (d > 0.0f) {
@@ -254,28 +301,28 @@ __global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float
           ff = vadd(ff, Fb);
         }
       }
+      // I V = [A0 w + m com x v; m (v - com x w)]
+      const v3 h = vadd(m3_v(ld9(T + T_A0), w), vscale(cross3(com, v), mass));
+      const v3 l = vscale(vsub(v, cross3(com, w)), mass);
+      pt_ = vsub(vadd(cross3(w, h), cross3(v, l)), fn_);
+      pb_ = vsub(cross3(w, l), ff);
       if (b > 0) {
-        const v3 ej = rotvec_of(r);
+        const v3 ej = rotvec_of(r), kp = ld3(T + T_KP), kd = ld3(T + T_KD);
         tau = {kp.x * (tgt.x - ej.x) - (kd.x + dt * kp.x) * om.x, kp.y * (tgt.y - ej.y) - (kd.y + dt * kp.y) * om.y,
                kp.z * (tgt.z - ej.z) - (kd.z + dt * kp.z) * om.z};
         cw = cross3(w, om);
         cv = cross3(v, om);
       }
     }
-    // ---- bias force p = V x* (I V) - f_ext; articulated inertia starts as the body's own
-    M3 A = A0, B = B0, M = {{mass, 0.0f, 0.0f, 0.0f, mass, 0.0f, 0.0f, 0.0f, mass}};
-    v3 pt_, pb_;
-    {
-      const v3 h = vadd(m3_v(A0, w), m3_v(B0, v));
-      const v3 l = vadd(m3_tv(B0, w), vscale(v, mass));
-      pt_ = vsub(vadd(cross3(w, h), cross3(v, l)), fn_);
-      pb_ = vsub(cross3(w, l), ff);
-    }
-    M3 Dinv = {};
-    v3 u = {0.0f, 0.0f, 0.0f};
-    auto gather_children = [&]() {
+    // articulated inertia [[A, B], [B^T, M]]: the body's own plus its children's contributions
+    auto gather = [&](M3 &A, M3 &B, M3 &M) {
+      const float mass = T[T_MASS];
+      A = ld9(T + T_A0);
+      B = m3_skew(vscale(ld3(T + T_COM), mass));
+      M = {{mass, 0.0f, 0.0f, 0.0f, mass, 0.0f, 0.0f, 0.0f, mass}};
+      const int nch = (int)T[T_NCH];
       for (int k = 0; k < nch; ++k) {
-        const float *s = S[ch[k]];
+        const float *s = S[(int)T[T_CH + k]];
         const M3 As = sym_full(s), Ms = sym_full(s + 15);
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
@@ -283,31 +330,47 @@ __global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float
           B.m[i] += s[6 + i];
           M.m[i] += Ms.m[i];
         }
-        pt_ = vadd(pt_, v3{s[21], s[22], s[23]});
-        pb_ = vadd(pb_, v3{s[24], s[25], s[26]});
+        pt_ = vadd(pt_, ld3(s + 21));
+        pb_ = vadd(pb_, ld3(s + 24));
       }
     };
     // ---- inward pass
     for (int L = c.depth; L >= 1; --L) {
       if (level == L) {
-        gather_children();
-        M3 D = A;
-        D.m[0] += dext.x; D.m[4] += dext.y; D.m[8] += dext.z;
-        Dinv = m3_inv(D);
-        u = vsub(tau, pt_);
-        const M3 K = m3_mul(Dinv, A), Lm = m3_mul(Dinv, B);
-        const M3 Aa = m3_sub(A, m3_mul(A, K));
+        M3 A, B, M;
+        gather(A, B, M);
+        M3 Ka, Lm;
+        v3 y;
+        {
+          M3 D = A;
+          const v3 dx = ld3(T + T_DEXT);
+          D.m[0] += dx.x; D.m[4] += dx.y; D.m[8] += dx.z;
+          const M3 Dinv = m3_inv(D);
+          Ka = m3_mul(Dinv, A);
+          Lm = m3_mul(Dinv, B);
+          y = m3_v(Dinv, vsub(tau, pt_));
+        }
+        float *o = O[b];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+          o[i] = Ka.m[i];
+          o[9 + i] = Lm.m[i];
+        }
+        o[18] = y.x; o[19] = y.y; o[20] = y.z;
+        // Ia = I^A - U D^-1 U^T, pa = pA + Ia c + U D^-1 u  (U = [A; B^T])
+        const M3 Aa = m3_sub(A, m3_mul(A, Ka));
         const M3 Ba = m3_sub(B, m3_mul(A, Lm));
         const M3 Ma = m3_sub(M, m3_mul(m3_t(B), Lm));
-        const v3 y = m3_v(Dinv, u);
         const v3 pat = vadd(vadd(pt_, vadd(m3_v(Aa, cw), m3_v(Ba, cv))), m3_v(A, y));
         const v3 pab = vadd(vadd(pb_, vadd(m3_tv(Ba, cw), m3_v(Ma, cv))), m3_tv(B, y));
         // to parent coordinates: rotate by E, then shift by the joint offset
         const M3 E = m3_quat(r.x, r.y, r.z, r.w);
-        const M3 Ar = m3_mul_t(m3_mul(E, Aa), E), Br = m3_mul_t(m3_mul(E, Ba), E), Mr = m3_mul_t(m3_mul(E, Ma), E);
+        const v3 off = ld3(T + T_OFF);
         const M3 Rx = m3_skew(off);
-        const M3 BR = m3_mul(Br, Rx), RBt = m3_mul_t(Rx, Br), RM = m3_mul(Rx, Mr);
-        const M3 Ap = m3_sub(m3_add(m3_sub(Ar, BR), RBt), m3_mul(RM, Rx));
+        const M3 Br = m3_mul_t(m3_mul(E, Ba), E), Mr = m3_mul_t(m3_mul(E, Ma), E);
+        const M3 RM = m3_mul(Rx, Mr);
+        const M3 Ap = m3_sub(m3_add(m3_sub(m3_mul_t(m3_mul(E, Aa), E), m3_mul(Br, Rx)), m3_mul_t(Rx, Br)),
+                             m3_mul(RM, Rx));
         const M3 Bp = m3_add(Br, RM);
         const v3 Fp = m3_v(E, pab);
         const v3 Np = vadd(m3_v(E, pat), cross3(off, Fp));
@@ -324,7 +387,8 @@ __global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float
     // ---- floating root: a0 = -IA^-1 pA (6x6 Cholesky on lane 0)
     v3 aw = {0.0f, 0.0f, 0.0f}, av = {0.0f, 0.0f, 0.0f};
     if (level == 0) {
-      gather_children();
+      M3 A, B, M;
+      gather(A, B, M);
       float G[6][6], rhs[6];
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -371,17 +435,17 @@ __global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float
       s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
     }
     __syncthreads();
-    // ---- outward pass: accelerations and joint accelerations
+    // ---- outward pass: a' = X a_parent + c, qdd = y - K a'_w - L a'_v, a = a' + [qdd; 0]
     v3 qdd = {0.0f, 0.0f, 0.0f};
     for (int L = 1; L <= c.depth; ++L) {
       if (level == L) {
         const float *ps = S[parent];
-        const v3 apw = {ps[0], ps[1], ps[2]}, apv = {ps[3], ps[4], ps[5]};
+        const v3 apw = ld3(ps);
         const M3 E = m3_quat(r.x, r.y, r.z, r.w);
         aw = vadd(m3_tv(E, apw), cw);
-        av = vadd(m3_tv(E, vsub(apv, cross3(off, apw))), cv);
-        const v3 ua = vadd(m3_v(A, aw), m3_v(B, av));  // U^T a' (A symmetric)
-        qdd = m3_v(Dinv, vsub(u, ua));
+        av = vadd(m3_tv(E, vsub(ld3(ps + 3), cross3(ld3(T + T_OFF), apw))), cv);
+        const float *o = O[b];
+        qdd = vsub(vsub(ld3(o + 18), m3_v(ld9(o), aw)), m3_v(ld9(o + 9), av));
         aw = vadd(aw, qdd);
         float *s = S[b];
         s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
@@ -390,20 +454,22 @@ __global__ __launch_bounds__(kBlock) void k_physics_step(PhysView e, const float
     }
     // ---- semi-implicit Euler
     if (act && b > 0) {
+      const v3 kp = ld3(T + T_KP), kd = ld3(T + T_KD);
       applied = {tau.x - dt * (kd.x + dt * kp.x) * qdd.x, tau.y - dt * (kd.y + dt * kp.y) * qdd.y,
                  tau.z - dt * (kd.z + dt * kp.z) * qdd.z};
       om = vadd(om, vscale(qdd, dt));
-      r = qnormalize(qmul_std(r, quat_from_rotvec(vscale(om, dt))));
+      r = qnormalize(qmul_std(r, quat_exp_increment(vscale(om, dt))));
     } else if (act) {
       w0 = vadd(w0, vscale(aw, dt));
       v0 = vadd(v0, vscale(av, dt));
-      p0 = vadd(p0, vscale(m3_v(R, v0), dt));
-      q0 = qnormalize(qmul_std(q0, quat_from_rotvec(vscale(w0, dt))));
+      p0 = vadd(p0, vscale(m3_v(m3_quat(Q.x, Q.y, Q.z, Q.w), v0), dt));
+      q0 = qnormalize(qmul_std(q0, quat_exp_increment(vscale(w0, dt))));
     }
   }
   kinematics();
   if (!act) return;  // no barrier follows
   {
+    const M3 R = m3_quat(Q.x, Q.y, Q.z, Q.w);
     const v3 vw = m3_v(R, v), ww = m3_v(R, w);
     float *o = e.rb + (env * kBodies + b) * kRec;
     o[0] = P.x; o[1] = P.y; o[2] = P.z;
@@ -455,8 +521,8 @@ extern "C" int phc_physics_step(const phc_env_buffers *env, const float *pd_targ
   c.g = p->gravity;
   const PhysView v = {env->num_envs, env->rigid_body_state, env->root_state, env->dof_state,
                        const_cast<float *>(env->dof_force)};  // read-only for the env step, written here
-  const int64_t blocks = (env->num_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
-  hipLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kBlock), 0, as_stream(stream), v, body_model,
+  const int64_t blocks = (env->num_envs + kPhysEnvs - 1) / kPhysEnvs;
+  hipLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), v, body_model,
                      pd_target, c);
   return check_launch("physics_step");
 }
