@@ -28,13 +28,19 @@
 //   28 num_points  32..63 contact points (x y z radius) x 8
 #include "phc_common.h"
 
+// this file is not held to bit-exact torch rounding (its checker is a float64 restatement): let
+// multiply-adds contract into FMAs and divide through the hardware reciprocal
+#pragma clang fp contract(fast)
+
 namespace phc {
+
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 #ifndef PHC_PHYS_EPB
 #define PHC_PHYS_EPB 2  // envs per workgroup (half-waves): one wave per workgroup (measured: 8 -> 750 us, 4 -> 711 us, 2 -> 631 us per 4096-env step)
 #endif
 #ifndef PHC_PHYS_WAVES_PER_SIMD
-#define PHC_PHYS_WAVES_PER_SIMD 1  // occupancy hint to the register allocator
+#define PHC_PHYS_WAVES_PER_SIMD 2  // occupancy hint to the register allocator (<= 256 registers)
 #endif
 
 constexpr int kModel = PHC_BODY_MODEL_STRIDE;
@@ -103,12 +109,31 @@ __device__ __forceinline__ v3 m3_tv(const M3 &a, v3 v) {  // a^T v
 __device__ __forceinline__ M3 m3_inv(const M3 &a) {  // adjugate / determinant
   const float *m = a.m;
   const float c0 = m[4] * m[8] - m[5] * m[7], c1 = m[5] * m[6] - m[3] * m[8], c2 = m[3] * m[7] - m[4] * m[6];
-  const float id = 1.0f / (m[0] * c0 + m[1] * c1 + m[2] * c2);
+  const float id = rcp(m[0] * c0 + m[1] * c1 + m[2] * c2);
   return {{c0 * id, (m[2] * m[7] - m[1] * m[8]) * id, (m[1] * m[5] - m[2] * m[4]) * id, c1 * id,
            (m[0] * m[8] - m[2] * m[6]) * id, (m[2] * m[3] - m[0] * m[5]) * id, c2 * id,
            (m[1] * m[6] - m[0] * m[7]) * id, (m[0] * m[4] - m[1] * m[3]) * id}};
 }
 __device__ __forceinline__ v3 cross3(v3 a, v3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+// [r]x M (column j = r x M_col j) and M [r]x (row i = M_row i x r) without the skew matrix's zeros
+__device__ __forceinline__ M3 skew_mul(v3 r, const M3 &a) {
+  M3 o;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const v3 x = cross3(r, v3{a.m[j], a.m[3 + j], a.m[6 + j]});
+    o.m[j] = x.x; o.m[3 + j] = x.y; o.m[6 + j] = x.z;
+  }
+  return o;
+}
+__device__ __forceinline__ M3 mul_skew(const M3 &a, v3 r) {
+  M3 o;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const v3 x = cross3(v3{a.m[3 * i], a.m[3 * i + 1], a.m[3 * i + 2]}, r);
+    o.m[3 * i] = x.x; o.m[3 * i + 1] = x.y; o.m[3 * i + 2] = x.z;
+  }
+  return o;
+}
 __device__ __forceinline__ v3 vscale(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
 
 __device__ __forceinline__ q4 qmul_std(q4 a, q4 b) {
@@ -121,7 +146,7 @@ __device__ __forceinline__ q4 qnormalize(q4 q) {
 }
 __device__ __forceinline__ q4 quat_from_rotvec(v3 e) {
   const float th = sqrtf(e.x * e.x + e.y * e.y + e.z * e.z);
-  const float s = th > 1e-8f ? sinf(0.5f * th) / th : 0.5f - th * th / 48.0f;
+  const float s = th > 1e-8f ? sinf(0.5f * th) * rcp(th) : 0.5f - th * th * (1.0f / 48.0f);
   return {e.x * s, e.y * s, e.z * s, cosf(0.5f * th)};
 }
 // exp of a substep's rotation increment (|e| = |omega| dt, small): series to theta^4 below 0.25 rad
@@ -137,7 +162,7 @@ __device__ __forceinline__ v3 rotvec_of(q4 q) {
   if (q.w < 0.0f) q = {-q.x, -q.y, -q.z, -q.w};
   const float sn = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
   const float th = 2.0f * atan2f(sn, q.w);
-  const float k = sn > 1e-8f ? th / sn : 2.0f / fmaxf(q.w, 1e-30f);
+  const float k = sn > 1e-8f ? th * rcp(sn) : 2.0f * rcp(fmaxf(q.w, 1e-30f));
   return {q.x * k, q.y * k, q.z * k};
 }
 
@@ -295,7 +320,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
           const v3 vw = m3_v(R, vadd(v, cross3(w, a)));
           const float fn = fmaxf(0.0f, c.kn * d - c.cn * vw.z);
           const float vt = sqrtf(vw.x * vw.x + vw.y * vw.y);
-          const float kt = fminf(c.ct, c.mu * fn / fmaxf(vt, 1e-12f));
+          const float kt = fminf(c.ct, c.mu * fn * rcp(fmaxf(vt, 1e-12f)));
           const v3 Fb = m3_tv(R, v3{-kt * vw.x, -kt * vw.y, fn});
           fn_ = vadd(fn_, cross3(a, Fb));
           ff = vadd(ff, Fb);
@@ -366,11 +391,11 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
         // to parent coordinates: rotate by E, then shift by the joint offset
         const M3 E = m3_quat(r.x, r.y, r.z, r.w);
         const v3 off = ld3(T + T_OFF);
-        const M3 Rx = m3_skew(off);
         const M3 Br = m3_mul_t(m3_mul(E, Ba), E), Mr = m3_mul_t(m3_mul(E, Ma), E);
-        const M3 RM = m3_mul(Rx, Mr);
-        const M3 Ap = m3_sub(m3_add(m3_sub(m3_mul_t(m3_mul(E, Aa), E), m3_mul(Br, Rx)), m3_mul_t(Rx, Br)),
-                             m3_mul(RM, Rx));
+        const M3 RM = skew_mul(off, Mr);
+        // A_p = E Aa E^T - Br [r]x + [r]x Br^T - [r]x Mr [r]x, with [r]x Br^T = -(Br [r]x)^T
+        const M3 X = mul_skew(Br, off);
+        const M3 Ap = m3_sub(m3_sub(m3_mul_t(m3_mul(E, Aa), E), m3_add(X, m3_t(X))), mul_skew(RM, off));
         const M3 Bp = m3_add(Br, RM);
         const v3 Fp = m3_v(E, pab);
         const v3 Np = vadd(m3_v(E, pat), cross3(off, Fp));
@@ -405,8 +430,8 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
         float d = G[j][j];
 #pragma unroll
         for (int k = 0; k < j; ++k) d -= G[j][k] * G[j][k];
-        const float ljj = sqrtf(fmaxf(d, 1e-20f)), il = 1.0f / ljj;
-        G[j][j] = ljj;
+        const float ljj = sqrtf(fmaxf(d, 1e-20f)), il = rcp(ljj);
+        G[j][j] = il;  // the diagonal holds 1 / l_jj
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) {
           float s = G[i][j];
@@ -420,14 +445,14 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
         float s = rhs[i];
 #pragma unroll
         for (int k = 0; k < i; ++k) s -= G[i][k] * rhs[k];
-        rhs[i] = s / G[i][i];
+        rhs[i] = s * G[i][i];
       }
 #pragma unroll
       for (int i = 5; i >= 0; --i) {  // L^T x = y
         float s = rhs[i];
 #pragma unroll
         for (int k = i + 1; k < 6; ++k) s -= G[k][i] * rhs[k];
-        rhs[i] = s / G[i][i];
+        rhs[i] = s * G[i][i];
       }
       aw = {rhs[0], rhs[1], rhs[2]};
       av = {rhs[3], rhs[4], rhs[5]};
