@@ -69,6 +69,9 @@ def parse():
                     help="policy GEMM arithmetic (TrainConfig.precision)")
     ap.add_argument("--amp", action="store_true",
                     help="AMP discriminator obs + discriminator loss (BASELINE config C5, with --precision bf16)")
+    ap.add_argument("--physics", choices=["replay", "articulated"], default="replay",
+                    help="replay = BASELINE configs[1]'s physics stand-in (the headline); articulated = the N3 "
+                         "articulated-body step (phc_physics_step) in its place")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic-file", default=None)
@@ -100,7 +103,8 @@ def build_env(args, rank):
     q, t, counts, fps = synthetic_clips(args.envs, args.min_len, args.max_len, seed=1000 + rank, device=device)
     packed = PackedMotions.from_global_rotations(q, t, counts, fps)
     del q, t
-    cfg = EnvConfig(num_envs=args.envs, device_id=torch.cuda.current_device(), seed=rank, use_amp_obs=args.amp)
+    cfg = EnvConfig(num_envs=args.envs, device_id=torch.cuda.current_device(), seed=rank, use_amp_obs=args.amp,
+                    physics=args.physics)
     env = PHCPufferEnv(cfg, motion_data=packed)
     env.reset()
     return env, packed, cfg
@@ -372,16 +376,18 @@ def main():
             with open(tf) as f:
                 traffic = json.load(f).get("bytes_per_launch")
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.physics == "replay":
             cpu = cpu_baseline(env, packed, args.cpu_seconds)
         workloads = {
             "ppo": "clean_pufferl PPO iteration: evaluate %d rows (PHCPolicy %s inference + PHCPufferEnv.step) + "
                    "RMS update + train (GAE, 4 epochs x %d minibatches of %d, Adam)" % (
                        args.batch_size, args.precision, args.batch_size // args.minibatch_size, args.minibatch_size),
             "rollout": "PHCPolicy %s inference + PHCPufferEnv.step + on-device experience store" % args.precision,
-            "env": "PHCPufferEnv.step: actions->PD + replay physics + fused obs/reward/reset + reset re-init "
-                   "(fixed random actions, no policy)",
+            "env": "PHCPufferEnv.step: actions->PD + %s physics + fused obs/reward/reset + reset re-init "
+                   "(fixed random actions, no policy)" % args.physics,
         }
+        phys_note = ("replayed physics" if args.physics == "replay" else
+                     "articulated-body physics (phc_physics_step, %d substeps per sim step)" % env_cfg.physics_substeps)
         out = {
             "metric": "env-steps/sec (whole node), 24-joint SMPL humanoid, 4096 envs per GPU",
             "value": processed_all / elapsed,
@@ -395,12 +401,12 @@ def main():
             "vs_baseline": None,
             "dtype": {"xf32": "fp32", "fp16": "fp16", "bf16": "bf16"}[args.precision] if args.mode != "env"
             else "fp32",
-            "data": "synthetic (device-generated SMPL clips U{%d..%d} frames @30fps; replayed physics; "
-                    "random-init policy)" % (args.min_len, args.max_len),
+            "data": "synthetic (device-generated SMPL clips U{%d..%d} frames @30fps; %s; "
+                    "random-init policy)" % (args.min_len, args.max_len, phys_note),
             "config": {"workload": workloads[args.mode], "mode": args.mode, "envs_per_gpu": args.envs,
                        "global_envs": args.envs * world, "motions_per_gpu": args.envs,
                        "parallelism": f"dp{world} (env shards, RCCL grad all-reduce)",
-                       "amp_obs": bool(args.amp),
+                       "amp_obs": bool(args.amp), "physics": args.physics,
                        "policy_gemm": {"xf32": "fp32 storage, hipBLASLt xf32 (torch 'high', as the reference)",
                                        "fp16": "fp16 operands (TF32's 11-bit significand; the reference runs "
                                                "TF32) on hand-written MFMA GEMMs with fused bias/SiLU epilogues, "
