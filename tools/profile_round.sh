@@ -35,4 +35,7 @@ for E in 4096 32768; do
   python tools/pmc_summary.py "$O/pmc_env_${E}_FETCH_SIZE" "$O/pmc_env_${E}_WRITE_SIZE" k_env_step "$O/traffic_$E.json" \
     "$O/trace_env_$E" $((10886 * E))
 done
+# the AMP + bf16 configuration (BASELINE C5): kernel stats, to show which kernels the discriminator runs on
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/trace_ppo_amp_bf16" -o run --output-format csv -- \
+  python3 "$ROOT/bench.py" --amp --precision bf16 --steps 2 --warmup 1 --no-cpu-baseline > "$O/trace_ppo_amp_bf16.log" 2>&1
 echo "profile_round done"
