@@ -110,6 +110,50 @@ def build_env(args, rank):
     return env, packed, cfg
 
 
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9  # wave-instructions/s: 256 CUs x 4 SIMDs x 1 VALU issue/cycle at 2.4 GHz
+
+
+def physics_roofline(args, kern_s, launches):
+    """N3 physics kernel (phc_physics_step): VALU-issue bound.  achieved = the kernel's VALU
+    wave-instructions per launch (SQ_INSTS_VALU from the committed PMC pass,
+    profiles/physics_valu_4096.json, scaled by the wave count: one wave per 2 envs) / its mean launch
+    duration timed live by the launch's own events."""
+    f = os.path.join(ROOT, "profiles", "physics_valu_4096.json")
+    instr = None
+    if os.path.exists(f):
+        with open(f) as fh:
+            ref = json.load(fh)
+        instr = ref["valu_instr_per_launch"] * ((args.envs + 1) // 2) / ref["waves_per_launch"]
+    ach = instr / kern_s if instr and kern_s > 0 else None
+    return {"bound": "valu-issue", "kernel": "phc_physics_step", "achieved": ach, "peak": VALU_ISSUE_PEAK,
+            "unit": "wave-instr/s", "frac": ach / VALU_ISSUE_PEAK if ach else None, "kernel_us": kern_s * 1e6,
+            "launches_timed": launches, "env_steps_per_s_kernel": args.envs / kern_s if kern_s > 0 else None,
+            "valu_instr_per_launch": instr}
+
+
+def physics_cpu_baseline(seconds):
+    """The float64 numpy restatement of the physics step (oracle/physics_oracle.py, test
+    infrastructure) on this host, one thread, over a 64-env sample of standing humanoids."""
+    import numpy as np
+
+    from oracle import physics_oracle as PO
+
+    m = PO.load_model()
+    n = 64
+    rb, dof = PO.rest_state(m, n, 0.0)
+    tgt = np.random.default_rng(0).normal(0, 0.1, (n, PO.NUM_DOF))
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        rb, dof, _ = PO.step(m, rb, dof, tgt)
+        k += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n * k / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{k} physics steps x {n} envs (float64 numpy, vectorised over envs, 16 substeps each)"}
+
+
 def _host_cpu():
     model = "unknown"
     try:
@@ -341,6 +385,9 @@ def main():
     # epilogue GEMMs) timed by its own dispatch events, with its 2 m n k FLOPs
     gtimer = KernelTimer(capacity=max(4096, 256 * args.steps))
     gemm_set_timer(gtimer)
+    ptimer = None
+    if args.physics == "articulated":  # every phc_physics_step launch, timed by its dispatch events
+        ptimer = env.env.physics.timer = KernelTimer(capacity=max(4096, 64 * args.steps))
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -361,6 +408,11 @@ def main():
     gemm_set_timer(None)
     gemm_launches, gemm_flops = gtimer.count, gtimer.work
     gemm_s = gtimer.total_ms() * 1e-3 if gemm_launches else 0.0
+    phys_launches, phys_s = 0, 0.0
+    if ptimer is not None:
+        env.env.physics.timer = None
+        phys_launches = ptimer.count
+        phys_s = ptimer.total_ms() * 1e-3 / max(phys_launches, 1)
     t = torch.tensor([elapsed, kern_s], dtype=torch.float64, device=device)
     tot = torch.tensor([float(processed)], dtype=torch.float64, device=device)
     if world > 1:
@@ -423,6 +475,10 @@ def main():
                                      "phases (the per-epoch stat readback)" if args.mode == "ppo" else None},
             "cpu_baseline": cpu,
         }
+        if args.physics == "articulated":
+            out["roofline_physics"] = physics_roofline(args, phys_s, phys_launches)
+            if not args.no_cpu_baseline:
+                out["cpu_baseline_physics"] = physics_cpu_baseline(args.cpu_seconds)
         env_roof = {"bound": "hbm", "kernel": "phc_env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     "kernel_us": kern_s * 1e6, "launches_timed": env_steps,

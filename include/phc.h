@@ -207,6 +207,9 @@ typedef struct phc_physics_params {
 } phc_physics_params;
 int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const float *body_model,
                      const phc_physics_params *p, void *stream);
+/* the same launch with its start/stop events recorded into `timer` (bench.py); timer work += num_envs */
+int phc_physics_step_timed(const phc_env_buffers *env, const float *pd_target, const float *body_model,
+                           const phc_physics_params *p, phc_kernel_timer *timer, void *stream);
 
 /* R3-R5: load-time FK + velocities (poselib_skeleton.py:518-619, 1230-1251; motion_lib.py:119-140)
  * for `num_motions` clips packed back to back.  quat_global f64 [F,24,4], root_trans f64 [F,3],

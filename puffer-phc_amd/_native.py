@@ -219,6 +219,8 @@ _EXPORTS = {
                                            ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     "phc_physics_step": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), c_vp, c_vp, ctypes.POINTER(PhysicsParamsC),
                                          c_vp]),
+    "phc_physics_step_timed": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), c_vp, c_vp,
+                                               ctypes.POINTER(PhysicsParamsC), c_vp, c_vp]),
     "phc_fk_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_fk_motions": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
                                        ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -422,15 +424,15 @@ class KernelTimer:
         """Algorithmic work of the timed launches (phc_twin_gemm: FLOPs)."""
         return lib().phc_timer_work(self.handle)
 
-
-def gemm_set_timer(timer):
-    """Time every phc_twin_gemm launch outside graph capture into `timer` (None: off)."""
-    lib().phc_gemm_set_timer(timer.handle if timer is not None else None)
-
     def __del__(self):
         if getattr(self, "handle", None) and _lib is not None:
             _lib.phc_timer_destroy(self.handle)
             self.handle = None
+
+
+def gemm_set_timer(timer):
+    """Time every phc_twin_gemm launch outside graph capture into `timer` (None: off)."""
+    lib().phc_gemm_set_timer(timer.handle if timer is not None else None)
 
 
 def reset_envs(env_c, mlib, params, mask=None, phase=None, seed=0, counter=0, num_envs=None):
@@ -952,13 +954,16 @@ def physics_env_struct(rigid_body_state, dof_state, dof_force, root_state=None):
     return e
 
 
-def physics_step(env_c, pd_target, body_model, params):
-    """N3 articulated-body step (phc_physics_step) over the env buffers of env_c."""
+def physics_step(env_c, pd_target, body_model, params, timer=None):
+    """N3 articulated-body step (phc_physics_step) over the env buffers of env_c; with `timer`
+    (a KernelTimer) the launch's own start/stop events are recorded."""
     n = int(env_c.num_envs)
-    _check(lib().phc_physics_step(ctypes.byref(env_c), _ptr(pd_target, torch.float32, (n, NUM_DOF), "pd_target"),
-                                  _ptr(body_model, torch.float32, (NUM_BODIES, BODY_MODEL_STRIDE), "body_model"),
-                                  ctypes.byref(params), _stream()),
-           "phc_physics_step")
+    args = (ctypes.byref(env_c), _ptr(pd_target, torch.float32, (n, NUM_DOF), "pd_target"),
+            _ptr(body_model, torch.float32, (NUM_BODIES, BODY_MODEL_STRIDE), "body_model"), ctypes.byref(params))
+    if timer is not None:
+        _check(lib().phc_physics_step_timed(*args, timer.handle, _stream()), "phc_physics_step")
+    else:
+        _check(lib().phc_physics_step(*args, _stream()), "phc_physics_step")
 
 
 def actions_to_pd(actions, pd_out, offset, scale, frozen):

@@ -28,6 +28,8 @@
 //   28 num_points  32..63 contact points (x y z radius) x 8
 #include "phc_common.h"
 
+#include <hip/hip_ext.h>
+
 // this file is not held to bit-exact torch rounding (its checker is a float64 restatement): let
 // multiply-adds contract into FMAs and divide through the hardware reciprocal
 #pragma clang fp contract(fast)
@@ -520,8 +522,8 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
 
 using namespace phc;
 
-extern "C" int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const float *body_model,
-                                const phc_physics_params *p, void *stream) {
+extern "C" int phc_physics_step_timed(const phc_env_buffers *env, const float *pd_target, const float *body_model,
+                                      const phc_physics_params *p, phc_kernel_timer *timer, void *stream) {
   PHC_REQUIRE(env && env->num_envs > 0, "physics_step: num_envs must be > 0");
   PHC_REQUIRE(env->rigid_body_state && env->dof_state && env->dof_force, "physics_step: null env buffer");
   PHC_REQUIRE(pd_target && body_model && p, "physics_step: null target / model / params");
@@ -547,7 +549,19 @@ extern "C" int phc_physics_step(const phc_env_buffers *env, const float *pd_targ
   const PhysView v = {env->num_envs, env->rigid_body_state, env->root_state, env->dof_state,
                        const_cast<float *>(env->dof_force)};  // read-only for the env step, written here
   const int64_t blocks = (env->num_envs + kPhysEnvs - 1) / kPhysEnvs;
-  hipLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), v, body_model,
-                     pd_target, c);
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (timer && timer->used < (int32_t)timer->start.size()) {
+    ev0 = timer->start[timer->used];
+    ev1 = timer->stop[timer->used];
+    timer->used += 1;
+    timer->work += (double)env->num_envs;  // env-steps
+  }
+  hipExtLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), ev0, ev1, 0, v,
+                        body_model, pd_target, c);
   return check_launch("physics_step");
+}
+
+extern "C" int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const float *body_model,
+                                const phc_physics_params *p, void *stream) {
+  return phc_physics_step_timed(env, pd_target, body_model, p, nullptr, stream);
 }

@@ -115,6 +115,7 @@ class ArticulatedPhysics:
             self.config.kd_scale = kd_scale
         self.model = model or BodyModel(device=device)
         self.params = self._params()
+        self.timer = None  # bench: a _native.KernelTimer timing every launch
 
     def _params(self):
         c = self.config
@@ -124,4 +125,4 @@ class ArticulatedPhysics:
                                       float(c.gravity), 0.0)
 
     def step(self, env):
-        _native.physics_step(env._env_c, env.pd_target, self.model.table, self.params)
+        _native.physics_step(env._env_c, env.pd_target, self.model.table, self.params, timer=self.timer)

@@ -11,4 +11,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
   SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-include-regex "k_physics_step" -d "$O/pmc" -o run --output-format csv -- \
   python3 "$ROOT/tools/physics_probe.py" 4096 20 > "$O/pmc.log" 2>&1
+
+python "$ROOT/tools/physics_valu_summary.py" "$O/pmc" 4096 "$O/physics_valu_4096.json"
 echo done
