@@ -180,3 +180,31 @@ def test_env_steps_with_articulated_physics():
     assert torch.isfinite(env.env._rigid_body_state).all()
     assert not torch.equal(rb0, env.env._rigid_body_state)
     assert torch.isfinite(env.env.dof_force_tensor).all()
+
+
+def test_ppo_iteration_with_articulated_physics():
+    """One clean_pufferl iteration (graph rollout + PPO update) with the physics step in the env:
+    the rollout's physics launches run inside evaluate(), the update trains on their outcome."""
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig, TrainConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    q, t, c, fps = synthetic_clips(64, 20, 90, seed=6, device=DEV)
+    packed = PackedMotions.from_global_rotations(q, t, c, fps)
+    env = PHCPufferEnv(EnvConfig(num_envs=64, seed=4, physics="articulated"), motion_data=packed)
+    env.reset()
+    torch.manual_seed(0)
+    policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+    cfg = TrainConfig(batch_size=64 * 16, minibatch_size=256, bptt_horizon=8, checkpoint_interval=10 ** 9)
+    comps, info, util = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+    before = {k: v.detach().clone() for k, v in policy.named_parameters()}
+    clean_pufferl.evaluate(comps, info)
+    exp = comps.experience
+    assert info.global_step >= cfg.batch_size
+    assert torch.isfinite(exp.obs).all() and torch.isfinite(exp.rewards).all()
+    losses = clean_pufferl.train(comps, info, util)
+    assert np.isfinite([losses.policy_loss, losses.value_loss, losses.approx_kl]).all()
+    assert sum(not torch.equal(before[k], v) for k, v in policy.named_parameters() if v.requires_grad) > 0
