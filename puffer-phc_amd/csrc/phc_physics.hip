@@ -41,6 +41,9 @@ __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x);
 #ifndef PHC_PHYS_EPB
 #define PHC_PHYS_EPB 2  // envs per workgroup (half-waves): one wave per workgroup (measured: 8 -> 750 us, 4 -> 711 us, 2 -> 631 us per 4096-env step)
 #endif
+#ifndef PHC_PHYS_ABLATE
+#define PHC_PHYS_ABLATE 0  // measurement builds: bit 1 FK, 2 contacts, 4 inward, 8 outward, 16 root solve skipped
+#endif
 #ifndef PHC_PHYS_WAVES_PER_SIMD
 #define PHC_PHYS_WAVES_PER_SIMD 2  // occupancy hint to the register allocator (<= 256 registers)
 #endif
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
   // outward pass: world quaternion / origin and body twist of every body
   auto kinematics = [&]() {
     for (int L = 0; L <= c.depth; ++L) {
-      if (level == L) {
+      if (level == L && !(PHC_PHYS_ABLATE & 1)) {
         if (b == 0) {
           Q = q0; P = p0; w = w0; v = v0;
         } else {
@@ -312,7 +315,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
       v3 fn_ = cross3(com, F), ff = F;
       const v3 zb = {R.m[6], R.m[7], R.m[8]};  // R^T z
       const int npts = (int)T[T_NPTS];
-      for (int k = 0; k < npts; ++k) {
+      for (int k = 0; k < ((PHC_PHYS_ABLATE & 2) ? 0 : npts); ++k) {
         const float *pt = T + T_PTS + 4 * k;
         const v3 cp = ld3(pt);
         const float rho = pt[3];
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
     };
     // ---- inward pass
     for (int L = c.depth; L >= 1; --L) {
-      if (level == L) {
+      if (level == L && !(PHC_PHYS_ABLATE & 4)) {
         M3 A, B, M;
         gather(A, B, M);
         M3 Ka, Lm;
@@ -413,7 +416,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
     }
     // ---- floating root: a0 = -IA^-1 pA (6x6 Cholesky on lane 0)
     v3 aw = {0.0f, 0.0f, 0.0f}, av = {0.0f, 0.0f, 0.0f};
-    if (level == 0) {
+    if (level == 0 && !(PHC_PHYS_ABLATE & 16)) {
       M3 A, B, M;
       gather(A, B, M);
       float G[6][6], rhs[6];
@@ -465,7 +468,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
     // ---- outward pass: a' = X a_parent + c, qdd = y - K a'_w - L a'_v, a = a' + [qdd; 0]
     v3 qdd = {0.0f, 0.0f, 0.0f};
     for (int L = 1; L <= c.depth; ++L) {
-      if (level == L) {
+      if (level == L && !(PHC_PHYS_ABLATE & 8)) {  // ablation builds only (timing breakdown)
         const float *ps = S[parent];
         const v3 apw = ld3(ps);
         const M3 E = m3_quat(r.x, r.y, r.z, r.w);
