@@ -45,7 +45,7 @@ __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x);
 #define PHC_PHYS_ABLATE 0  // measurement builds: bit 1 FK, 2 contacts, 4 inward, 8 outward, 16 root solve skipped
 #endif
 #ifndef PHC_PHYS_WAVES_PER_SIMD
-#define PHC_PHYS_WAVES_PER_SIMD 2  // occupancy hint to the register allocator (<= 256 registers)
+#define PHC_PHYS_WAVES_PER_SIMD 2  // occupancy pinned (min = max): 3 waves per SIMD measured slower at 16384 envs
 #endif
 
 constexpr int kModel = PHC_BODY_MODEL_STRIDE;
@@ -205,7 +205,7 @@ __device__ __forceinline__ M3 ld9(const float *p) {
   return o;
 }
 
-__global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics_step(
+__global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_PHYS_WAVES_PER_SIMD, PHC_PHYS_WAVES_PER_SIMD))) void k_physics_step(
     PhysView e, const float *__restrict__ model, const float *__restrict__ target, PhysConsts c) {
   __shared__ float tab[kBodies * kTab];
   __shared__ float slots[kPhysEnvs][kBodies][kSlot];
@@ -253,6 +253,10 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
   const float *T = tab + b * kTab;
   const int parent = (int)T[T_PARENT];
   const int level = act ? (int)T[T_LEVEL] : -1;
+  // the tree passes run over the table's own depth (the host's tree_depth is only range-checked)
+  int depth = 0;
+  for (int i = 0; i < kBodies; ++i) depth = max(depth, (int)tab[i * kTab + T_LEVEL]);
+  depth = min(depth, 15);
 
   // ---- state: root (lane 0) in body coordinates, joints (lanes >= 1)
   q4 r = {0.0f, 0.0f, 0.0f, 1.0f};
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
   v3 P = {0.0f, 0.0f, 0.0f}, w = P, v = P;
   // outward pass: world quaternion / origin and body twist of every body
   auto kinematics = [&]() {
-    for (int L = 0; L <= c.depth; ++L) {
+    for (int L = 0; L <= depth; ++L) {
       if (level == L && !(PHC_PHYS_ABLATE & 1)) {
         if (b == 0) {
           Q = q0; P = p0; w = w0; v = v0;
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
       }
     };
     // ---- inward pass
-    for (int L = c.depth; L >= 1; --L) {
+    for (int L = depth; L >= 1; --L) {
       if (level == L && !(PHC_PHYS_ABLATE & 4)) {
         M3 A, B, M;
         gather(A, B, M);
@@ -467,7 +471,7 @@ __global__ __launch_bounds__(kPhysBlock, PHC_PHYS_WAVES_PER_SIMD) void k_physics
     __syncthreads();
     // ---- outward pass: a' = X a_parent + c, qdd = y - K a'_w - L a'_v, a = a' + [qdd; 0]
     v3 qdd = {0.0f, 0.0f, 0.0f};
-    for (int L = 1; L <= c.depth; ++L) {
+    for (int L = 1; L <= depth; ++L) {
       if (level == L && !(PHC_PHYS_ABLATE & 8)) {  // ablation builds only (timing breakdown)
         const float *ps = S[parent];
         const v3 apw = ld3(ps);
