@@ -196,7 +196,8 @@ typedef struct phc_physics_params {
   float sim_dt;             /* 1/60 (isaacgym_env.py:38) */
   int32_t control_freq_inv; /* 2 */
   int32_t substeps;         /* semi-implicit Euler substeps per sim step */
-  int32_t tree_depth;       /* deepest body level of the model (root = 0), 1..15 */
+  int32_t tree_depth;       /* deepest body level of the model (root = 0), 1..15; range-checked only:
+                               the kernel takes the depth from the body table itself */
   float kp_scale, kd_scale; /* EnvConfig kp_scale / kd_scale */
   float contact_stiffness;  /* N/m per contact point */
   float contact_damping;    /* N s/m per contact point */
