@@ -171,6 +171,41 @@ __device__ __forceinline__ v3 rotvec_of(q4 q) {
   return {q.x * k, q.y * k, q.z * k};
 }
 
+// symmetric 3x3 products: only the upper triangle of a product known to be symmetric
+struct S6 {
+  float xx, yy, zz, xy, xz, yz;
+};
+__device__ __forceinline__ float row_col(const M3 &a, int i, const M3 &b, int j) {  // (a b)_ij
+  return a.m[3 * i] * b.m[j] + a.m[3 * i + 1] * b.m[3 + j] + a.m[3 * i + 2] * b.m[6 + j];
+}
+__device__ __forceinline__ float col_col(const M3 &a, int i, const M3 &b, int j) {  // (a^T b)_ij
+  return a.m[i] * b.m[j] + a.m[3 + i] * b.m[3 + j] + a.m[6 + i] * b.m[6 + j];
+}
+__device__ __forceinline__ float row_row(const M3 &a, int i, const M3 &b, int j) {  // (a b^T)_ij
+  return a.m[3 * i] * b.m[3 * j] + a.m[3 * i + 1] * b.m[3 * j + 1] + a.m[3 * i + 2] * b.m[3 * j + 2];
+}
+__device__ __forceinline__ S6 sym_mul(const M3 &a, const M3 &b) {
+  return {row_col(a, 0, b, 0), row_col(a, 1, b, 1), row_col(a, 2, b, 2), row_col(a, 0, b, 1), row_col(a, 0, b, 2),
+          row_col(a, 1, b, 2)};
+}
+__device__ __forceinline__ S6 sym_tmul(const M3 &a, const M3 &b) {
+  return {col_col(a, 0, b, 0), col_col(a, 1, b, 1), col_col(a, 2, b, 2), col_col(a, 0, b, 1), col_col(a, 0, b, 2),
+          col_col(a, 1, b, 2)};
+}
+__device__ __forceinline__ M3 s6_full(const S6 &s) { return {{s.xx, s.xy, s.xz, s.xy, s.yy, s.yz, s.xz, s.yz, s.zz}}; }
+__device__ __forceinline__ S6 s6_of(const M3 &a) { return {a.m[0], a.m[4], a.m[8], a.m[1], a.m[2], a.m[5]}; }
+__device__ __forceinline__ S6 s6_sub(const S6 &a, const S6 &b) {
+  return {a.xx - b.xx, a.yy - b.yy, a.zz - b.zz, a.xy - b.xy, a.xz - b.xz, a.yz - b.yz};
+}
+__device__ __forceinline__ S6 sandwich(const M3 &e, const S6 &s) {  // e s e^T
+  const M3 t = m3_mul(e, s6_full(s));
+  return {row_row(t, 0, e, 0), row_row(t, 1, e, 1), row_row(t, 2, e, 2), row_row(t, 0, e, 1), row_row(t, 0, e, 2),
+          row_row(t, 1, e, 2)};
+}
+__device__ __forceinline__ void store_s6(const S6 &a, float *s) {
+  s[0] = a.xx; s[1] = a.yy; s[2] = a.zz; s[3] = a.xy; s[4] = a.xz; s[5] = a.yz;
+}
+
 // symmetric 3x3 (xx yy zz xy xz yz) <-> full
 __device__ __forceinline__ M3 sym_full(const float *s) { return {{s[0], s[3], s[4], s[3], s[1], s[5], s[4], s[5], s[2]}}; }
 __device__ __forceinline__ void full_sym(const M3 &a, float *s) {
@@ -391,28 +426,33 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
           o[9 + i] = Lm.m[i];
         }
         o[18] = y.x; o[19] = y.y; o[20] = y.z;
-        // Ia = I^A - U D^-1 U^T, pa = pA + Ia c + U D^-1 u  (U = [A; B^T])
-        const M3 Aa = m3_sub(A, m3_mul(A, Ka));
+        // Ia = I^A - U D^-1 U^T, pa = pA + Ia c + U D^-1 u  (U = [A; B^T]); the A and M blocks are
+        // symmetric, so only their upper triangles are formed
+        const S6 Aa = s6_sub(s6_of(A), sym_mul(A, Ka));
         const M3 Ba = m3_sub(B, m3_mul(A, Lm));
-        const M3 Ma = m3_sub(M, m3_mul(m3_t(B), Lm));
-        const v3 pat = vadd(vadd(pt_, vadd(m3_v(Aa, cw), m3_v(Ba, cv))), m3_v(A, y));
-        const v3 pab = vadd(vadd(pb_, vadd(m3_tv(Ba, cw), m3_v(Ma, cv))), m3_tv(B, y));
+        const S6 Ma = s6_sub(s6_of(M), sym_tmul(B, Lm));
+        const v3 pat = vadd(vadd(pt_, vadd(m3_v(s6_full(Aa), cw), m3_v(Ba, cv))), m3_v(A, y));
+        const v3 pab = vadd(vadd(pb_, vadd(m3_tv(Ba, cw), m3_v(s6_full(Ma), cv))), m3_tv(B, y));
         // to parent coordinates: rotate by E, then shift by the joint offset
         const M3 E = m3_quat(r.x, r.y, r.z, r.w);
         const v3 off = ld3(T + T_OFF);
-        const M3 Br = m3_mul_t(m3_mul(E, Ba), E), Mr = m3_mul_t(m3_mul(E, Ma), E);
-        const M3 RM = skew_mul(off, Mr);
+        const M3 Br = m3_mul_t(m3_mul(E, Ba), E);
+        const S6 Mr = sandwich(E, Ma);
+        const M3 RM = skew_mul(off, s6_full(Mr));
         // A_p = E Aa E^T - Br [r]x + [r]x Br^T - [r]x Mr [r]x, with [r]x Br^T = -(Br [r]x)^T
-        const M3 X = mul_skew(Br, off);
-        const M3 Ap = m3_sub(m3_sub(m3_mul_t(m3_mul(E, Aa), E), m3_add(X, m3_t(X))), mul_skew(RM, off));
+        const M3 X = mul_skew(Br, off), Z = mul_skew(RM, off);
+        const S6 Ar = sandwich(E, Aa);
+        const S6 Ap = {Ar.xx - 2.0f * X.m[0] - Z.m[0], Ar.yy - 2.0f * X.m[4] - Z.m[4], Ar.zz - 2.0f * X.m[8] - Z.m[8],
+                       Ar.xy - (X.m[1] + X.m[3]) - Z.m[1], Ar.xz - (X.m[2] + X.m[6]) - Z.m[2],
+                       Ar.yz - (X.m[5] + X.m[7]) - Z.m[5]};
         const M3 Bp = m3_add(Br, RM);
         const v3 Fp = m3_v(E, pab);
         const v3 Np = vadd(m3_v(E, pat), cross3(off, Fp));
         float *s = S[b];
-        full_sym(Ap, s);
+        store_s6(Ap, s);
 #pragma unroll
         for (int i = 0; i < 9; ++i) s[6 + i] = Bp.m[i];
-        full_sym(Mr, s + 15);
+        store_s6(Mr, s + 15);
         s[21] = Np.x; s[22] = Np.y; s[23] = Np.z;
         s[24] = Fp.x; s[25] = Fp.y; s[26] = Fp.z;
       }
