@@ -288,6 +288,8 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
   const float *T = tab + b * kTab;
   const int parent = (int)T[T_PARENT];
   const int level = act ? (int)T[T_LEVEL] : -1;
+  const int nch = (int)T[T_NCH];
+  const int ch0 = (int)T[T_CH], ch1 = (int)T[T_CH + 1], ch2 = (int)T[T_CH + 2];  // kept in registers
   // the tree passes run over the table's own depth (the host's tree_depth is only range-checked)
   int depth = 0;
   for (int i = 0; i < kBodies; ++i) depth = max(depth, (int)tab[i * kTab + T_LEVEL]);
@@ -389,9 +391,8 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       A = ld9(T + T_A0);
       B = m3_skew(vscale(ld3(T + T_COM), mass));
       M = {{mass, 0.0f, 0.0f, 0.0f, mass, 0.0f, 0.0f, 0.0f, mass}};
-      const int nch = (int)T[T_NCH];
       for (int k = 0; k < nch; ++k) {
-        const float *s = S[(int)T[T_CH + k]];
+        const float *s = S[k == 0 ? ch0 : (k == 1 ? ch1 : ch2)];
         const M3 As = sym_full(s), Ms = sym_full(s + 15);
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
