@@ -99,8 +99,27 @@ class BodyModel:
             t[i, 32:32 + 4 * len(pts)] = np.asarray(pts, dtype=np.float32).reshape(-1)
         self.names = [b["name"] for b in bodies]
         self.total_mass = float(sum(b["mass"] for b in bodies))
+        # zero pose (every joint rotation the identity): body origins are the summed offsets, and
+        # the root height that puts the lowest contact point on the ground
+        origin = np.zeros((n, 3))
+        for i in range(1, n):
+            origin[i] = origin[bodies[i]["parent"]] + np.asarray(bodies[i]["offset"])
+        low = min(origin[i][2] + p[2] - p[3] for i in range(n) for p in
+                  (t[i, 32:32 + 4 * int(t[i, 28])].reshape(-1, 4).astype(np.float64)))
+        self.rest_root_height = float(-low)
         self.host = t
         self.table = torch.from_numpy(t).to(device)
+
+
+def rest_state(model, num_envs, clearance=0.0, device="cuda"):
+    """Env buffers of `num_envs` humanoids standing in the zero pose at rest, the lowest contact
+    point `clearance` above the ground: (rigid_body_state [N,24,13] with the root record set — the
+    physics step reads only that record and dof_state — and dof_state [N,69,2])."""
+    rb = torch.zeros((num_envs, _native.NUM_BODIES, 13), device=device)
+    rb[:, :, 6] = 1.0
+    rb[:, 0, 2] = model.rest_root_height + clearance
+    dof = torch.zeros((num_envs, _native.NUM_DOF, 2), device=device)
+    return rb, dof
 
 
 class ArticulatedPhysics:

@@ -151,3 +151,16 @@ def test_device_table_layout(model):
         np.testing.assert_allclose(t[i, 32:32 + 4 * k].reshape(k, 4), model["points"][i], atol=1e-7)
         kids = [j for j in range(24) if model["parent"][j] == i and j > 0]
         assert int(t[i, 2]) == len(kids) and t[i, 3:3 + len(kids)].tolist() == kids
+
+
+def test_product_rest_state_matches_oracle(model):
+    """physics.rest_state (the product's standing start, used by tools/physics_probe.py) puts the
+    root at the oracle's rest height."""
+    pytest.importorskip("torch")
+    from puffer_phc_amd.physics import BodyModel, rest_state
+
+    bm = BodyModel(device="cpu")
+    rb, dof = rest_state(bm, 3, 0.05, device="cpu")
+    want, _ = P.rest_state(model, 1, 0.05)
+    np.testing.assert_allclose(rb[:, 0, 2].numpy(), want[0, 0, 2], atol=1e-6)
+    assert float(dof.abs().max()) == 0.0 and rb.shape == (3, 24, 13)

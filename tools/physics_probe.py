@@ -11,23 +11,17 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 import phc_amd_path  # noqa: E402
 
 phc_amd_path.register()
-from oracle import physics_oracle as P  # noqa: E402  (initial state only)
 from puffer_phc_amd import _native  # noqa: E402
-from puffer_phc_amd.physics import ArticulatedPhysics, BodyModel, PhysicsConfig  # noqa: E402
+from puffer_phc_amd.physics import ArticulatedPhysics, BodyModel, PhysicsConfig, rest_state  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 dev = "cuda:0"
-model = P.load_model()
-rb, dof = P.rest_state(model, 1, 0.0)
-rb = np.repeat(rb, n, 0)
-rb[:, :, 0] += np.arange(n)[:, None] * 2.0
-dof = np.repeat(dof, n, 0)
-rng = np.random.default_rng(0)
 bm = BodyModel(device=dev)
 phys = ArticulatedPhysics(PhysicsConfig(), model=bm)
-rb_t = torch.tensor(rb, dtype=torch.float32, device=dev)
-dof_t = torch.tensor(dof, dtype=torch.float32, device=dev)
+rb_t, dof_t = rest_state(bm, n, 0.0, device=dev)
+rb_t[:, 0, 0] += torch.arange(n, device=dev, dtype=torch.float32) * 2.0
+rng = np.random.default_rng(0)
 f_t = torch.zeros((n, 69), device=dev)
 tgt = torch.tensor(rng.normal(0, 0.1, (n, 69)), dtype=torch.float32, device=dev)
 env_c = _native.physics_env_struct(rb_t, dof_t, f_t)
