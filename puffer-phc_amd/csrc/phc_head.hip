@@ -14,9 +14,13 @@
 // MFMA step t of chunk q feeds lane group g the index 16 q + 4 g + t on both operands — so every
 // lane reads 4 consecutive K values with one 16-B load where the operand is K-contiguous.  A is at
 // most 80 (5 blocks of 16).
+// phc_mu_head_fwd / _dgrad launch the bf16-x3 forms below (k_head_fwd_x3 / k_head_dgrad_x3:
+// three-way bf16 operand splits on v_mfma_f32_16x16x32_bf16, fp32-class products) when H % 32 == 0;
+// the f32-MFMA kernels above serve the other widths (and PHC_MU_X3=0 for the input gradient).
 #include "phc_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace phc {
 
@@ -301,6 +305,253 @@ __global__ __launch_bounds__(kHeadFwdWaves * 64) void k_head_fwd_lds(const float
   }
 }
 
+// ---- forward / input gradient on the bf16 MFMA with three-way operand splits ------------------
+// Every fp32 operand x is split exactly as x = hi + mid + lo with hi = bf16(x), mid = bf16(x - hi),
+// lo = bf16(x - hi - mid) (8 + 8 + 8 significand bits: the fp32 significand), and each 16x16x32
+// step accumulates the six products whose magnitude reaches 2^-16 of hi·hi (smallest first):
+//   hi·lo + lo·hi + mid·mid + hi·mid + mid·hi + hi·hi
+// The dropped terms (mid·lo, lo·mid, lo·lo) are below 2^-23 of |x||w|, so each product carries
+// fp32-class error (the fp32 head's ulp, not the reference's TF32 2^-11) and the sums stay fp32.
+// bf16 keeps fp32's exponent range, so no scaling is needed for tiny gradients.  Six bf16 MFMAs
+// (16 cycles each) per 32-deep step against eight 32-cycle v_mfma_f32_16x16x4f32 per 32 K: the
+// launches become bound by their HBM traffic (h / dh: 64 MB per 32768-row minibatch) instead of
+// the fp32 matrix rate.
+using b8 = __attribute__((ext_vector_type(8))) __bf16;
+
+struct X3 {
+  b8 h, m, l;
+};
+
+__device__ __forceinline__ void split3(const float4 &x0, const float4 &x1, X3 &s) {
+  const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 a = (__bf16)v[j];
+    float r = v[j] - (float)a;
+    const __bf16 m = (__bf16)r;
+    r -= (float)m;
+    s.h[j] = a;
+    s.m[j] = m;
+    s.l[j] = (__bf16)r;
+  }
+}
+
+__device__ __forceinline__ hf4 mma_x3(const X3 &a, const X3 &b, hf4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.h, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+}
+
+// mu = h W^T + b.  W is split once per workgroup into three bf16 planes in LDS, 256 K at a time
+// ([80][256 + 8] per plane, rows past A zero); every wave owns one 16-row tile and keeps its
+// accumulators across the K chunks.  Lane (g, c): h row / W row c, K = k0 + 8 g .. + 7 of each
+// 32-deep step (the same K order on both operands); kX3FwdDepth steps of h are in flight per wave,
+// the first ones issued before the W staging.  Requires H % 32 == 0.
+constexpr int kX3FwdWaves = 8;
+constexpr int kX3FwdDepth = 4;  // 32-deep steps of h in flight per wave
+constexpr int kX3FwdKC = 256, kX3FwdKP = kX3FwdKC + 8;
+
+__global__ __launch_bounds__(kX3FwdWaves * 64) void k_head_fwd_x3(const float *__restrict__ h, const float *__restrict__ w,
+                                                                 const float *__restrict__ b, float *__restrict__ mu,
+                                                                 int64_t M, int H, int A) {
+  __shared__ __attribute__((aligned(16))) __bf16 pl[3][kHeadMaxA * kX3FwdKP];
+  constexpr int D = kX3FwdDepth;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int64_t r0 = ((int64_t)blockIdx.x * kX3FwdWaves + wave) * 16;
+  const bool live = r0 < M;  // uniform per wave; dead waves still stage W
+  int64_t hr = r0 + c;
+  hr = hr < M ? hr : M - 1;  // ragged last tile: clamp the read, mask the store
+  const float *hp = h + hr * H + 8 * g;
+  float4 ring[D][2];
+  auto fetch = [&](int d, int kk) {
+    ring[d][0] = *reinterpret_cast<const float4 *>(hp + kk);
+    ring[d][1] = *reinterpret_cast<const float4 *>(hp + kk + 4);
+  };
+  if (live) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (32 * d < H) fetch(d, 32 * d);
+  }
+  hf4 acc[5];
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) acc[nb] = hf4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int nblk = (A + 15) / 16;  // uniform
+  for (int kc = 0; kc < H; kc += kX3FwdKC) {
+    const int kn = H - kc < kX3FwdKC ? H - kc : kX3FwdKC;
+    if (kc) __syncthreads();  // the previous chunk's planes are no longer read
+    // stage W[:, kc : kc + kn] split into the planes: 4 consecutive K per thread item, 8 in flight
+    const int items = 16 * nblk * (kn / 4);
+    for (int base = threadIdx.x; base < items; base += 8 * kX3FwdWaves * 64) {
+      float4 tmp[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = base + u * kX3FwdWaves * 64, a = i / (kn / 4), k4 = i - a * (kn / 4);
+        tmp[u] = (i < items && a < A) ? *reinterpret_cast<const float4 *>(w + (int64_t)a * H + kc + 4 * k4)
+                                      : float4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = base + u * kX3FwdWaves * 64, a = i / (kn / 4), k4 = i - a * (kn / 4);
+        if (i >= items) break;
+        const float v[4] = {tmp[u].x, tmp[u].y, tmp[u].z, tmp[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const __bf16 hi = (__bf16)v[j];
+          float r = v[j] - (float)hi;
+          const __bf16 mi = (__bf16)r;
+          r -= (float)mi;
+          const int o = a * kX3FwdKP + 4 * k4 + j;
+          pl[0][o] = hi;
+          pl[1][o] = mi;
+          pl[2][o] = (__bf16)r;
+        }
+      }
+    }
+    __syncthreads();
+    if (!live) continue;
+    for (int k0 = kc; k0 < kc + kn; k0 += 32 * D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int kk = k0 + 32 * d;
+        if (kk >= kc + kn) break;
+        X3 xs;
+        split3(ring[d][0], ring[d][1], xs);
+        if (kk + 32 * D < H) fetch(d, kk + 32 * D);
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) {
+          if (nb >= nblk) break;
+          const int off = (16 * nb + c) * kX3FwdKP + (kk - kc) + 8 * g;
+          X3 ws;
+          ws.h = *reinterpret_cast<const b8 *>(&pl[0][off]);
+          ws.m = *reinterpret_cast<const b8 *>(&pl[1][off]);
+          ws.l = *reinterpret_cast<const b8 *>(&pl[2][off]);
+          acc[nb] = mma_x3(xs, ws, acc[nb]);
+        }
+      }
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) {
+    const int a = 16 * nb + c;
+    if (a >= A) continue;
+    const float bias = b[a];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t row = r0 + 4 * g + e;
+      if (row < M) mu[row * A + a] = acc[nb][e] + bias;
+    }
+  }
+}
+
+// dh = dmu W.  Workgroup = 4 waves = 256 rows x one 128-column panel (blockIdx.y); the panel's W
+// columns are split once into three bf16 planes in LDS, transposed to [column][K] (K = actions,
+// zero past A, padded to 96 + 8) so a lane's 8 consecutive K values are one 16-B read; wave tile =
+// 64 rows (4 row blocks) x 128 columns (8 column blocks), 32 accumulators.
+constexpr int kX3DgradKP = 104;
+
+__global__ __launch_bounds__(256, 2) void k_head_dgrad_x3(const float *__restrict__ dmu, const float *__restrict__ w,
+                                                       float *__restrict__ dh, int64_t M, int H, int A) {
+  __shared__ __attribute__((aligned(16))) __bf16 pl[3][128 * kX3DgradKP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int n0 = blockIdx.y * 128;
+  const int nq = (A + 31) / 32;  // 32-deep K steps (uniform)
+  for (int base = threadIdx.x; base < 32 * nq * 128; base += 16 * 256) {  // 16 loads in flight
+    float tmp[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = base + 256 * u, k = i >> 7, n = i & 127;
+      tmp[u] = (k < A && n0 + n < H) ? w[(int64_t)k * H + n0 + n] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = base + 256 * u, k = i >> 7, n = i & 127;
+      if (i >= 32 * nq * 128) break;
+      const __bf16 hi = (__bf16)tmp[u];
+      float r = tmp[u] - (float)hi;
+      const __bf16 mi = (__bf16)r;
+      r -= (float)mi;
+      pl[0][n * kX3DgradKP + k] = hi;
+      pl[1][n * kX3DgradKP + k] = mi;
+      pl[2][n * kX3DgradKP + k] = (__bf16)r;
+    }
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * 256 + wave * 64;
+  if (r0 >= M) return;  // after the barrier
+  const float *ap[4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    int64_t ar = r0 + 16 * rb + c;
+    ar = ar < M ? ar : M - 1;
+    ap[rb] = dmu + ar * A;
+  }
+  // computed transposed, dh^T = W^T dmu^T: lane (g, c) then holds 4 consecutive dh columns
+  // 16 nb + 4 g .. + 3 of row 16 rb + c, stored as one float4
+  hf4 acc[4][8];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) acc[rb][nb] = hf4{0.0f, 0.0f, 0.0f, 0.0f};
+  // dmu fragments of step q (clamped loads, masked after landing); step q + 1's loads are issued
+  // into the same registers once step q's split has consumed them, so they land during its MFMAs
+  float v[4][8];
+  auto load = [&](int q) {
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * q + 8 * g + j;
+        v[rb][j] = ap[rb][k < A ? k : A - 1];
+      }
+  };
+  load(0);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    if (q >= nq) break;
+    X3 as[4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = 32 * q + 8 * g + j < A ? v[rb][j] : 0.0f;
+      split3(float4{x[0], x[1], x[2], x[3]}, float4{x[4], x[5], x[6], x[7]}, as[rb]);
+    }
+    if (q + 1 < nq) load(q + 1);
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const int off = (16 * nb + c) * kX3DgradKP + 32 * q + 8 * g;
+      X3 ws;
+      ws.h = *reinterpret_cast<const b8 *>(&pl[0][off]);
+      ws.m = *reinterpret_cast<const b8 *>(&pl[1][off]);
+      ws.l = *reinterpret_cast<const b8 *>(&pl[2][off]);
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) acc[rb][nb] = mma_x3(ws, as[rb], acc[rb][nb]);
+    }
+  }
+  const bool vec = (H & 3) == 0;  // uniform
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    const int64_t row = r0 + 16 * rb + c;
+    if (row >= M) continue;
+    float *out = dh + row * H;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const int col = n0 + 16 * nb + 4 * g;
+      if (vec && col + 3 < H) {
+        *reinterpret_cast<float4 *>(out + col) = float4{acc[rb][nb][0], acc[rb][nb][1], acc[rb][nb][2], acc[rb][nb][3]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (col + e < H) out[col + e] = acc[rb][nb][e];
+      }
+    }
+  }
+}
+
 static int head_cus() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -326,7 +577,12 @@ extern "C" int phc_mu_head_fwd(const float *h, const float *w, const float *b, f
   PHC_REQUIRE((reinterpret_cast<uintptr_t>(h) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0,
               "mu_head_fwd: h and w must be 16-byte aligned");
   const size_t lds = (size_t)num_actions * (hidden + 4) * sizeof(float);
-  if (lds <= kHeadLdsMax) {  // W staged in LDS, persistent over 16-row tiles
+  if (hidden % 32 == 0) {  // bf16 x3 MFMA: W planes in LDS, one 16-row tile per wave
+    const int64_t blocks = (rows + 16 * kX3FwdWaves - 1) / (16 * kX3FwdWaves);
+    PHC_REQUIRE(blocks <= 0x7fffffff, "mu_head_fwd: too many rows");
+    hipLaunchKernelGGL(k_head_fwd_x3, dim3((unsigned)blocks), dim3(kX3FwdWaves * 64), 0, as_stream(stream), h, w, b, mu,
+                       rows, (int)hidden, (int)num_actions);
+  } else if (lds <= kHeadLdsMax) {  // W staged in LDS, persistent over 16-row tiles
     static bool attr = [] {
       (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_head_fwd_lds),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHeadLdsMax);
@@ -349,6 +605,16 @@ extern "C" int phc_mu_head_dgrad(const float *dmu, const float *w, float *dh, in
                                  int32_t num_actions, void *stream) {
   if (int rc = check_head(dmu, w, rows, hidden, num_actions)) return rc;
   PHC_REQUIRE(dh, "mu_head_dgrad: null output");
+  static const bool x3 = [] {
+    const char *e = getenv("PHC_MU_X3");
+    return !(e && atoi(e) == 0);
+  }();
+  if (x3) {  // bf16 x3 MFMA, 256 rows x 128 columns per workgroup
+    const dim3 grid((unsigned)((rows + 255) / 256), (unsigned)((hidden + 127) / 128));
+    hipLaunchKernelGGL(k_head_dgrad_x3, grid, dim3(256), 0, as_stream(stream), dmu, w, dh, rows, (int)hidden,
+                       (int)num_actions);
+    return check_launch("mu_head_dgrad");
+  }
   const dim3 grid((unsigned)((rows + 15) / 16), (unsigned)((hidden + 511) / 512));
   hipLaunchKernelGGL(k_head_dgrad, grid, dim3(256), 0, as_stream(stream), dmu, w, dh, rows, (int)hidden,
                      (int)num_actions);

@@ -31,9 +31,10 @@ def timeit(fn, reps=50):
     return s.elapsed_time(e) / reps * 1e3
 
 
-rows = [("fwd kernel", lambda: N.mu_head_fwd(h, w, b)), ("fwd addmm", lambda: torch.addmm(b, h, w.t())),
+rows = [("h.clone (67 MB read+write)", lambda: h.clone()), ("h.sum (67 MB read)", lambda: h.sum()),
+        ("fwd kernel", lambda: N.mu_head_fwd(h, w, b)), ("fwd addmm", lambda: torch.addmm(b, h, w.t())),
         ("dgrad kernel", lambda: N.mu_head_dgrad(dmu, w)), ("dgrad mm", lambda: torch.mm(dmu, w))]
-for s in (32, 64, 128, 256):
+for s in (128,):
     rows.append((f"wgrad kernel S={s}", lambda s=s: N.mu_head_wgrad_parts(dmu, h, s)))
     rows.append((f"wgrad kernel S={s} + sum", lambda s=s: N.mu_head_wgrad_parts(dmu, h, s).sum(0)))
 rows.append(("wgrad mm", lambda: torch.mm(dmu.t(), h)))
