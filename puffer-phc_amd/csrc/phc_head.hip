@@ -336,6 +336,22 @@ __device__ __forceinline__ void split3(const float4 &x0, const float4 &x1, X3 &s
   }
 }
 
+// the six terms for n independent accumulators, term-major: consecutive MFMAs write different
+// accumulators, so no MFMA waits for the previous one's result
+template <int n>
+__device__ __forceinline__ void mma_x3_n(const X3 *a, const X3 *b, hf4 *c, bool a_shared) {
+#define PHC_X3_TERM(P, Q)                                                                        \
+  _Pragma("unroll") for (int i = 0; i < n; ++i) c[i] =                                           \
+      __builtin_amdgcn_mfma_f32_16x16x32_bf16((a_shared ? a[0] : a[i]).P, (a_shared ? b[i] : b[0]).Q, c[i], 0, 0, 0);
+  PHC_X3_TERM(h, l)
+  PHC_X3_TERM(l, h)
+  PHC_X3_TERM(m, m)
+  PHC_X3_TERM(h, m)
+  PHC_X3_TERM(m, h)
+  PHC_X3_TERM(h, h)
+#undef PHC_X3_TERM
+}
+
 __device__ __forceinline__ hf4 mma_x3(const X3 &a, const X3 &b, hf4 c) {
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
@@ -378,12 +394,11 @@ __global__ __launch_bounds__(kX3FwdWaves * 64) void k_head_fwd_x3(const float *_
   hf4 acc[5];
 #pragma unroll
   for (int nb = 0; nb < 5; ++nb) acc[nb] = hf4{0.0f, 0.0f, 0.0f, 0.0f};
-  const int nblk = (A + 15) / 16;  // uniform
   for (int kc = 0; kc < H; kc += kX3FwdKC) {
     const int kn = H - kc < kX3FwdKC ? H - kc : kX3FwdKC;
     if (kc) __syncthreads();  // the previous chunk's planes are no longer read
     // stage W[:, kc : kc + kn] split into the planes: 4 consecutive K per thread item, 8 in flight
-    const int items = 16 * nblk * (kn / 4);
+    const int items = kHeadMaxA * (kn / 4);  // all 80 rows (zero past A)
     for (int base = threadIdx.x; base < items; base += 8 * kX3FwdWaves * 64) {
       float4 tmp[8];
 #pragma unroll
@@ -420,16 +435,15 @@ __global__ __launch_bounds__(kX3FwdWaves * 64) void k_head_fwd_x3(const float *_
         X3 xs;
         split3(ring[d][0], ring[d][1], xs);
         if (kk + 32 * D < H) fetch(d, kk + 32 * D);
+        X3 ws[5];
 #pragma unroll
         for (int nb = 0; nb < 5; ++nb) {
-          if (nb >= nblk) break;
           const int off = (16 * nb + c) * kX3FwdKP + (kk - kc) + 8 * g;
-          X3 ws;
-          ws.h = *reinterpret_cast<const b8 *>(&pl[0][off]);
-          ws.m = *reinterpret_cast<const b8 *>(&pl[1][off]);
-          ws.l = *reinterpret_cast<const b8 *>(&pl[2][off]);
-          acc[nb] = mma_x3(xs, ws, acc[nb]);
+          ws[nb].h = *reinterpret_cast<const b8 *>(&pl[0][off]);
+          ws[nb].m = *reinterpret_cast<const b8 *>(&pl[1][off]);
+          ws[nb].l = *reinterpret_cast<const b8 *>(&pl[2][off]);
         }
+        mma_x3_n<5>(&xs, ws, acc, true);  // blocks past A multiply zero planes
       }
     }
   }
@@ -528,8 +542,10 @@ __global__ __launch_bounds__(256, 2) void k_head_dgrad_x3(const float *__restric
       ws.h = *reinterpret_cast<const b8 *>(&pl[0][off]);
       ws.m = *reinterpret_cast<const b8 *>(&pl[1][off]);
       ws.l = *reinterpret_cast<const b8 *>(&pl[2][off]);
+      hf4 cc[4] = {acc[0][nb], acc[1][nb], acc[2][nb], acc[3][nb]};
+      mma_x3_n<4>(&ws, as, cc, true);
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) acc[rb][nb] = mma_x3(ws, as[rb], acc[rb][nb]);
+      for (int rb = 0; rb < 4; ++rb) acc[rb][nb] = cc[rb];
     }
   }
   const bool vec = (H & 3) == 0;  // uniform

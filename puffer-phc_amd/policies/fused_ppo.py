@@ -20,11 +20,12 @@ from .twin_mlp import _compute_dtype, _use_mfma, direct_grads_bound, mfma_trunk_
 
 
 MU_WGRAD_SPLITS = int(os.environ.get("PHC_MU_WGRAD_SPLITS", "128"))  # row chunks of the mu-head weight gradient
-# forward / input gradient of the mu head on phc_mu_head_fwd / _dgrad (1) or the library GEMMs (0):
-# the fp32-MFMA kernels measured 41.5 us (W staged in LDS) / 54 us against the library's 36 / 36 us
-# per 32768-row minibatch (tools/mu_head_probe.py); the weight gradient runs on phc_mu_head_wgrad
-# either way (39 us + its partial sum riding in phc_reduce_into, library 140 us)
-MU_HEAD_KERNELS = os.environ.get("PHC_MU_HEAD_KERNELS", "0") == "1"
+# forward / input gradient of the mu head on phc_mu_head_fwd / _dgrad (1, default) or the library
+# GEMMs (0): the bf16-x3 MFMA kernels (three-way bf16 operand splits, fp32-class products; see
+# phc_head.hip) against the library's fp32 GEMMs, per 32768-row minibatch (tools/mu_head_probe.py);
+# the weight gradient runs on phc_mu_head_wgrad either way (39 us + its partial sum riding in
+# phc_reduce_into, library 140 us)
+MU_HEAD_KERNELS = os.environ.get("PHC_MU_HEAD_KERNELS", "1") == "1"
 
 
 def _aligned(w):
