@@ -499,8 +499,10 @@ int phc_tail_ln_bwd(const phc_tail_ln_args *args, const float *dh_actor, const f
                     int32_t num_actions, void *dy, int32_t dtype, float *partial, void *stream);
 
 /* R19 + R21: the actor's mu head, nn.Linear(hidden, num_actions) in fp32
- * (policies/phc_policy.py:40-61; its autograd in clean_pufferl/core.py:298-354), on the fp32-input
- * MFMA (exact products, fp32 sums; the summation order differs from a library GEMM's):
+ * (policies/phc_policy.py:40-61; its autograd in clean_pufferl/core.py:298-354), fp32-class on the
+ * MFMA: fwd / dgrad split every fp32 operand into three bf16 parts (six bf16 MFMA products per
+ * step, fp32 sums; hidden % 32 == 0, else the fp32-input MFMA), wgrad on the fp32-input MFMA
+ * (exact products); the summation order differs from a library GEMM's:
  *   fwd  : mu [rows, A] = h [rows, hidden] . w [A, hidden]^T + b [A]   (h, w 16-byte aligned, hidden % 16 == 0)
  *   dgrad: dh [rows, hidden] = dmu [rows, A] . w
  *   wgrad: partial [splits, A, hidden], partial[s] = dmu[rows_s]^T . h[rows_s] over the s-th of
