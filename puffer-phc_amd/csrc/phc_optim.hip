@@ -33,7 +33,9 @@ __global__ __launch_bounds__(kOptBlock) void k_grad_partials(const float *__rest
   const int64_t s = blk_range[2 * blockIdx.x], e = blk_range[2 * blockIdx.x + 1];
   double acc = 0.0, l2 = 0.0;
   int bad = 0;
-  for (int64_t i = s + threadIdx.x; i < e; i += kOptBlock) {
+  // scalar head up to a 16-B boundary, float4 body (16-B loads: the pass is HBM-bound over the 3
+  // flat buffers), scalar tail; a fixed per-thread order, so the result stays deterministic
+  auto one = [&](int64_t i) {
     const float v = g[i];
     bad |= !__builtin_isfinite(v);
     acc += (double)v * (double)v;
@@ -41,7 +43,48 @@ __global__ __launch_bounds__(kOptBlock) void k_grad_partials(const float *__rest
       const double d = (double)p[i] - (double)p0[i];
       l2 += d * d;
     }
+  };
+  auto four = [&](const float4 v, const float4 a, const float4 b) {
+    bad |= !__builtin_isfinite(v.x) | !__builtin_isfinite(v.y) | !__builtin_isfinite(v.z) | !__builtin_isfinite(v.w);
+    acc += ((double)v.x * (double)v.x + (double)v.y * (double)v.y) + ((double)v.z * (double)v.z + (double)v.w * (double)v.w);
+    if (p0) {
+      const double d0 = (double)a.x - (double)b.x, d1 = (double)a.y - (double)b.y;
+      const double d2 = (double)a.z - (double)b.z, d3 = (double)a.w - (double)b.w;
+      l2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+  };
+  const bool aligned = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(p) |
+                         reinterpret_cast<uintptr_t>(p0)) & 15) == 0;  // uniform
+  int64_t vs = aligned ? (s + 3) & ~(int64_t)3 : e;
+  vs = vs < e ? vs : e;
+  const int64_t ve = aligned ? vs + ((e - vs) & ~(int64_t)3) : vs;
+  for (int64_t t = s + threadIdx.x; t < vs; t += kOptBlock) one(t);  // < 4 elements when aligned
+  int64_t i = vs + 4 * (int64_t)threadIdx.x;
+  if (p0) {  // uniform: no select around the loads (it would serialise them)
+    for (; i + 4 * kOptBlock < ve; i += 8 * kOptBlock) {  // two 16-B loads per buffer in flight
+      const float4 v0 = *reinterpret_cast<const float4 *>(g + i);
+      const float4 v1 = *reinterpret_cast<const float4 *>(g + i + 4 * kOptBlock);
+      const float4 a0 = *reinterpret_cast<const float4 *>(p + i);
+      const float4 a1 = *reinterpret_cast<const float4 *>(p + i + 4 * kOptBlock);
+      const float4 b0 = *reinterpret_cast<const float4 *>(p0 + i);
+      const float4 b1 = *reinterpret_cast<const float4 *>(p0 + i + 4 * kOptBlock);
+      four(v0, a0, b0);
+      four(v1, a1, b1);
+    }
+    if (i < ve)
+      four(*reinterpret_cast<const float4 *>(g + i), *reinterpret_cast<const float4 *>(p + i),
+           *reinterpret_cast<const float4 *>(p0 + i));
+  } else {
+    const float4 z4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (; i + 4 * kOptBlock < ve; i += 8 * kOptBlock) {
+      const float4 v0 = *reinterpret_cast<const float4 *>(g + i);
+      const float4 v1 = *reinterpret_cast<const float4 *>(g + i + 4 * kOptBlock);
+      four(v0, z4, z4);
+      four(v1, z4, z4);
+    }
+    if (i < ve) four(*reinterpret_cast<const float4 *>(g + i), z4, z4);
   }
+  for (int64_t t = ve + threadIdx.x; t < e; t += kOptBlock) one(t);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     acc += __shfl_xor(acc, o, 64);
