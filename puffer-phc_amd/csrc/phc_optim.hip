@@ -240,11 +240,45 @@ struct ReduceJobs {
 };
 constexpr int kRedThreads = 256, kRedPerThread = 4;
 
+constexpr int kRedManyParts = 8;  // jobs with more parts split them over the block's 4 waves
+
+__host__ __device__ inline int64_t red_elems_per_block(const phc_reduce_job &j) {
+  return j.parts > kRedManyParts ? 64 : kRedThreads * kRedPerThread;
+}
+
 __global__ __launch_bounds__(kRedThreads) void k_reduce_into(ReduceJobs js) {
   int q = 0;
   while (q + 1 < js.n && (int64_t)blockIdx.x >= js.first_block[q + 1]) ++q;
   const phc_reduce_job &job = js.j[q];
   const int64_t total = job.rows * job.cols;
+  if (job.parts > kRedManyParts) {  // uniform per block
+    // many parts (fine split-K): one element per lane, the parts split into 4 contiguous ranges,
+    // one per wave, each summed with 8 independent running sums (8 loads in flight per lane), the
+    // 4 wave sums combined through LDS in a fixed order: deterministic, 4x shorter load chains
+    __shared__ float red[kRedThreads / 64][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = ((int64_t)blockIdx.x - js.first_block[q]) * 64 + lane;
+    const int per = (job.parts + 3) / 4, s0 = w * per, s1 = s0 + per < job.parts ? s0 + per : job.parts;
+    float a8[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (i < total) {
+      const int64_t r = i / job.cols, c = i - r * job.cols;
+      const float *src = job.src + r * job.src_ld + c;
+      int s = s0;
+      for (; s + 8 <= s1; s += 8) {
+#pragma unroll
+        for (int l = 0; l < 8; ++l) a8[l] += src[(int64_t)(s + l) * job.part_stride];
+      }
+      for (int l = 0; s + l < s1; ++l) a8[l] += src[(int64_t)(s + l) * job.part_stride];
+    }
+    red[w][lane] = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
+    __syncthreads();
+    if (w == 0 && i < total) {
+      const float acc = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      if (job.accumulate) job.dst[i] += acc;
+      else job.dst[i] = acc;
+    }
+    return;
+  }
   const int64_t base = ((int64_t)blockIdx.x - js.first_block[q]) * kRedThreads * kRedPerThread + threadIdx.x;
 #pragma unroll
   for (int u = 0; u < kRedPerThread; ++u) {
@@ -252,24 +286,8 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_into(ReduceJobs js) {
     if (i >= total) break;
     const int64_t r = i / job.cols, c = i - r * job.cols;
     const float *src = job.src + r * job.src_ld + c;
-    float acc;
-    if (job.parts <= 8) {
-      acc = src[0];
-      for (int s = 1; s < job.parts; ++s) acc += src[s * job.part_stride];
-    } else {
-      // many parts (a persistent kernel's per-block rows, fine split-K): 8 independent running
-      // sums (parts s = 8q + l) keep 8 loads in flight, combined in a fixed order: deterministic
-      float a8[8];
-#pragma unroll
-      for (int l = 0; l < 8; ++l) a8[l] = src[l * job.part_stride];
-      int s = 8;
-      for (; s + 8 <= job.parts; s += 8) {
-#pragma unroll
-        for (int l = 0; l < 8; ++l) a8[l] += src[(int64_t)(s + l) * job.part_stride];
-      }
-      for (int l = 0; s + l < job.parts; ++l) a8[l] += src[(int64_t)(s + l) * job.part_stride];
-      acc = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
-    }
+    float acc = src[0];
+    for (int s = 1; s < job.parts; ++s) acc += src[s * job.part_stride];
     if (job.accumulate) job.dst[i] += acc;
     else job.dst[i] = acc;
   }
@@ -292,7 +310,7 @@ extern "C" int phc_reduce_into(const phc_reduce_job *jobs, int32_t num_jobs, voi
     PHC_REQUIRE(j.src && j.dst, "reduce_into: job %d null pointer", q);
     js.j[n] = j;
     js.first_block[n] = blocks;
-    blocks += (j.rows * j.cols + kRedThreads * kRedPerThread - 1) / (kRedThreads * kRedPerThread);
+    blocks += (j.rows * j.cols + red_elems_per_block(j) - 1) / red_elems_per_block(j);
     ++n;
   }
   if (n == 0) return PHC_OK;

@@ -127,7 +127,7 @@ def test_state_dict_round_trip():
         assert torch.equal(x.detach(), y.detach())
 
 
-@pytest.mark.parametrize("parts", [1, 2, 8, 9, 16, 17, 32])
+@pytest.mark.parametrize("parts", [1, 2, 8, 9, 16, 17, 32, 128, 131])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_reduce_into_many_parts(parts, accumulate):
     """phc_reduce_into (phc_optim.hip k_reduce_into) over many parts: the 8-running-sum branch
