@@ -214,18 +214,36 @@ __global__ __launch_bounds__(kBwdThreads) void k_tail_ln_bwd(phc_tail_ln_args a,
       p6[0][k][e] = p6[1][k][e] = pwv[k][e] = 0.0f;
     }
   float pbmu0 = 0.0f, pbmu1 = 0.0f, pbv = 0.0f;
-  // one row (both trunks) per wave at a time, its loads issued together
-  for (int64_t row = (int64_t)blockIdx.x * kWaves + wave; row < M; row += (int64_t)gridDim.x * kWaves) {
+  // one row (both trunks) per wave at a time; the wave's next row is loaded while this one is
+  // processed (its loads land during the reductions), dmu through clamped loads masked after
+  struct RowIn {
     float xa[kTC][4], xc[kTC][4], da[kTC][4];
-    t_load_row(a.trunk_out + row * kTH, lane, xa);
-    t_load_row(a.trunk_out + (M + row) * kTH, lane, xc);
-    t_load_row(dh_actor + row * kTH, lane, da);
-    const float dv = dvalue[row];
-    pbmu0 += lane < A ? dmu[row * A + lane] : 0.0f;
-    pbmu1 += lane + 64 < A ? dmu[row * A + lane + 64] : 0.0f;
-    pbv += dv;
-    t_ln_bwd_row<T, false>(xa, da, gm[0], bt[0], a.ln_eps, 0.0f, lane, dy + row * kTH, pg[0], pb[0], p6[0], pwv);
-    t_ln_bwd_row<T, true>(xc, wv, gm[1], bt[1], a.ln_eps, dv, lane, dy + (M + row) * kTH, pg[1], pb[1], p6[1], pwv);
+    float dv, m0, m1;
+  };
+  const int l0 = lane < A ? lane : A - 1, l1 = lane + 64 < A ? lane + 64 : A - 1;
+  auto fetch = [&](int64_t r, RowIn &in) {
+    t_load_row(a.trunk_out + r * kTH, lane, in.xa);
+    t_load_row(a.trunk_out + (M + r) * kTH, lane, in.xc);
+    t_load_row(dh_actor + r * kTH, lane, in.da);
+    in.dv = dvalue[r];
+    in.m0 = dmu[r * A + l0];
+    in.m1 = dmu[r * A + l1];
+  };
+  const int64_t step = (int64_t)gridDim.x * kWaves;
+  int64_t row = (int64_t)blockIdx.x * kWaves + wave;
+  RowIn cur;
+  if (row < M) fetch(row, cur);
+  for (; row < M; row += step) {
+    RowIn nxt;
+    if (row + step < M) fetch(row + step, nxt);
+    pbmu0 += lane < A ? cur.m0 : 0.0f;
+    pbmu1 += lane + 64 < A ? cur.m1 : 0.0f;
+    pbv += cur.dv;
+    t_ln_bwd_row<T, false>(cur.xa, cur.da, gm[0], bt[0], a.ln_eps, 0.0f, lane, dy + row * kTH, pg[0], pb[0], p6[0],
+                           pwv);
+    t_ln_bwd_row<T, true>(cur.xc, wv, gm[1], bt[1], a.ln_eps, cur.dv, lane, dy + (M + row) * kTH, pg[1], pb[1], p6[1],
+                          pwv);
+    cur = nxt;
   }
   // the block's partial row (tail_layout): the 8 waves' column sums added through LDS in order
   const TailLayout L = tail_layout(A, kTH);
