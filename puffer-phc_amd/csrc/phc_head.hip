@@ -361,14 +361,14 @@ __device__ __forceinline__ hf4 mma_x3(const X3 &a, const X3 &b, hf4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
 }
 
-// mu = h W^T + b.  W is split once per workgroup into three bf16 planes in LDS, 256 K at a time
-// ([80][256 + 8] per plane, rows past A zero); every wave owns one 16-row tile and keeps its
+// mu = h W^T + b.  W is split once per workgroup into three bf16 planes in LDS, 128 K at a time
+// ([80][128 + 8] per plane, rows past A zero); every wave owns one 16-row tile and keeps its
 // accumulators across the K chunks.  Lane (g, c): h row / W row c, K = k0 + 8 g .. + 7 of each
 // 32-deep step (the same K order on both operands); kX3FwdDepth steps of h are in flight per wave,
 // the first ones issued before the W staging.  Requires H % 32 == 0.
 constexpr int kX3FwdWaves = 8;
 constexpr int kX3FwdDepth = 4;  // 32-deep steps of h in flight per wave
-constexpr int kX3FwdKC = 256, kX3FwdKP = kX3FwdKC + 8;
+constexpr int kX3FwdKC = 128, kX3FwdKP = kX3FwdKC + 8;
 
 __global__ __launch_bounds__(kX3FwdWaves * 64) void k_head_fwd_x3(const float *__restrict__ h, const float *__restrict__ w,
                                                                  const float *__restrict__ b, float *__restrict__ mu,
