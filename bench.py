@@ -1,7 +1,8 @@
 """Benchmark: whole-job env-steps/s of the PHC imitation rollout + PPO step on MI355X.
 
-Contract: `python bench.py --gpus N --steps K --warmup W` (N>1 under torch.distributed.run,
-one rank per GPU over RCCL).  Rank 0 prints ONE JSON line.  Default workload (BASELINE.json
+Contract: `python bench.py --gpus N --steps K --warmup W`: N>1 runs one rank per GPU over RCCL,
+either under the caller's torch.distributed.run or, without one, under a torch.distributed.run
+this script starts as a child process (launch_ranks).  Rank 0 prints ONE JSON line.  Default workload (BASELINE.json
 configs[2] at 4096 envs per GPU; the metric's config):
 
   --mode ppo (default): one step = one full PPO iteration of clean_pufferl exactly as
@@ -267,8 +268,24 @@ def cpu_baseline(env, packed, seconds):
                       f"GAE: oracle/gae.c over 131072 rows x {reps}"}
 
 
+def whole_job_steps(counts, is_global, world):
+    """Whole-job env-steps of the timed region from each rank's count.  ppo mode counts the
+    reference's SPS numerator, `global_step` (clean_pufferl/core.py:135-138), which data-parallel
+    evaluate() already sums over ranks (core._global_count): every rank holds the whole-job count
+    and it is taken once.  env / rollout modes count each rank's own env steps: they are summed."""
+    counts = [float(c) for c in counts]
+    if len(counts) != world:
+        raise ValueError(f"{len(counts)} rank counts for world size {world}")
+    if is_global:
+        if max(counts) != min(counts):
+            raise ValueError(f"ranks disagree on the whole-job step count: {counts}")
+        return counts[0]
+    return sum(counts)
+
+
 class Runner:
-    """One benchmark 'step' per mode; returns the env-steps it processed on this rank."""
+    """One benchmark 'step' per mode; returns the env-steps it processed (ppo mode: the
+    whole-job count, see whole_job_steps)."""
 
     def __init__(self, args, env, env_cfg):
         self.args, self.env = args, env
@@ -365,8 +382,29 @@ class Runner:
         return {k: v / n for k, v in tot.items()}
 
 
+def launch_ranks(n):
+    """`--gpus N` without a torch.distributed launcher around this process: start N ranks (one per
+    GPU) under torch.distributed.run as CHILD processes and return their exit code.  This parent
+    never touches the GPU (nothing before this point initialises HIP); rank 0 prints the JSON line
+    on the inherited stdout."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:  # a free rendezvous port on the loopback interface
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: the launcher's world "
+              "size is used", file=sys.stderr)
     if os.environ.get("PHC_WATCHDOG_S"):  # debugging aid: dump every thread's stack periodically
         import faulthandler
 
@@ -416,11 +454,15 @@ def main():
         phys_launches = ptimer.count
         phys_s = ptimer.total_ms() * 1e-3 / max(phys_launches, 1)
     t = torch.tensor([elapsed, kern_s], dtype=torch.float64, device=device)
-    tot = torch.tensor([float(processed)], dtype=torch.float64, device=device)
+    counts = [float(processed)]
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        torch.distributed.all_reduce(tot)
-    elapsed, kern_s, processed_all = float(t[0]), float(t[1]), float(tot[0])
+        mine = torch.tensor([float(processed)], dtype=torch.float64, device=device)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(every, mine)
+        counts = [float(c) for c in every]
+    elapsed, kern_s = float(t[0]), float(t[1])
+    processed_all = whole_job_steps(counts, args.mode == "ppo", world)
 
     if rank == 0:
         achieved = BYTES_PER_ENV_STEP * args.envs / kern_s / 1e9
@@ -477,6 +519,7 @@ def main():
                                      "phases (the per-epoch stat readback)" if args.mode == "ppo" else None},
             "cpu_baseline": cpu,
         }
+        out["config"]["env_steps_timed"] = processed_all  # value = env_steps_timed / wall seconds
         if args.physics == "articulated":
             out["roofline_physics"] = physics_roofline(args, phys_s, phys_launches)
             if not args.no_cpu_baseline:

@@ -452,6 +452,23 @@ typedef struct phc_reduce_job {
 } phc_reduce_job;
 int phc_reduce_into(const phc_reduce_job *jobs, int32_t num_jobs, void *stream);
 
+/* R19 / R21 / R22: the GEMM-operand copies of the fp32 parameters, rewritten after every optimizer
+ * step in ONE launch (the reference's modules read their fp32 parameters directly; here the MFMA
+ * GEMMs read f16 / bf16 copies: weights [rows, cols] at a leading dimension, and for the
+ * input-gradient GEMMs their transposes [cols, rows]; fp32 bias copies use dtype PHC_DT_F32).
+ * Rounding is round-to-nearest-even, as torch's copy_.  Job j: dst[r * dst_ld + c] and
+ * dst_t[c * dst_t_ld + r] = src[r * src_ld + c] for r < rows, c < cols (dst or dst_t may be NULL);
+ * columns of dst beyond cols are not touched (the K padding stays zero). */
+#define PHC_MAX_PACK_JOBS 32
+typedef struct phc_pack_job {
+  const float *src;
+  void *dst;
+  void *dst_t;
+  int64_t rows, cols, src_ld, dst_ld, dst_t_ld;
+  int32_t dtype, reserved;
+} phc_pack_job;
+int phc_pack_weights(const phc_pack_job *jobs, int32_t num_jobs, void *stream);
+
 /* R21: the PPO minibatch objective (clean_pufferl/core.py:298-352 with the fixed-sigma Normal
  * log-prob / entropy of pufferlib.sample_logits and PHCPolicy.bound_loss).  Forward: stats[0] =
  * loss = pg - ent_coef*ent + vf_coef*v + bound_coef*bound, stats[1..7] = pg, v, ent,

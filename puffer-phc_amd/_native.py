@@ -131,6 +131,14 @@ class ReduceJobC(ctypes.Structure):
 MAX_REDUCE_JOBS = 32
 
 
+class PackJobC(ctypes.Structure):
+    _fields_ = [("src", c_vp), ("dst", c_vp), ("dst_t", c_vp), ("rows", c_i64), ("cols", c_i64), ("src_ld", c_i64),
+                ("dst_ld", c_i64), ("dst_t_ld", c_i64), ("dtype", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+MAX_PACK_JOBS = 32
+
+
 class PolicyActArgsC(ctypes.Structure):
     _fields_ = [("trunk_out", c_vp), ("ln_gamma", c_vp * 2), ("ln_beta", c_vp * 2), ("w_mu", c_vp), ("b_mu", c_vp),
                 ("w_value", c_vp), ("b_value", c_vp), ("log_sigma", c_vp), ("noise", c_vp), ("actions", c_vp),
@@ -187,6 +195,7 @@ _EXPORTS = {
     "phc_weight_grad_group": (ctypes.c_int, [ctypes.POINTER(WgradProblemC), ctypes.c_int32, c_i64, ctypes.c_int32,
                                               ctypes.c_int32, c_vp]),
     "phc_reduce_into": (ctypes.c_int, [ctypes.POINTER(ReduceJobC), ctypes.c_int32, c_vp]),
+    "phc_pack_weights": (ctypes.c_int, [ctypes.POINTER(PackJobC), ctypes.c_int32, c_vp]),
     "phc_obs_half": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int32, c_vp, c_vp, ctypes.c_float, ctypes.c_float,
                                      c_vp, ctypes.c_int32, ctypes.c_int32, c_vp]),
     "phc_policy_act": (ctypes.c_int, [ctypes.POINTER(PolicyActArgsC), c_vp]),
@@ -638,6 +647,53 @@ def reduce_into(jobs, accumulate=True):
             arr[q] = ReduceJobC(src.data_ptr(), dst.data_ptr(), R, C, src.stride(1) if R > 1 else C,
                                 src.stride(0) if P > 1 else 0, P, int(accumulate))
         _check(lib().phc_reduce_into(arr, len(chunk), _stream()), "phc_reduce_into")
+
+
+def _rows2d(t, name):
+    if t.dim() == 1:
+        t = t[None]
+    if t.dim() != 2 or not t.is_cuda or (t.shape[1] > 1 and t.stride(1) != 1):
+        raise ValueError(f"pack_weights: {name} must be a 1-D or 2-D device tensor with contiguous columns")
+    return t, (t.stride(0) if t.shape[0] > 1 else t.shape[1])
+
+
+class PackPlan:
+    """A fixed list of operand-refresh jobs (phc_pack_weights): (src fp32 [rows, cols], dst
+    [rows, cols] or None, dst_t [cols, rows] or None), f16 / bf16 / fp32 destinations.  The C
+    argument arrays are built once; run() is one launch per 32 jobs."""
+
+    def __init__(self, jobs):
+        self._keep, self._arrs = [], []
+        for i in range(0, len(jobs), MAX_PACK_JOBS):
+            chunk = jobs[i:i + MAX_PACK_JOBS]
+            arr = (PackJobC * len(chunk))()
+            for q, (src, dst, dst_t) in enumerate(chunk):
+                if src.dtype != torch.float32:
+                    raise ValueError("pack_weights: fp32 sources only")
+                s2, sld = _rows2d(src, "src")
+                rows, cols = s2.shape
+                dt = (dst if dst is not None else dst_t).dtype
+                if dt not in DTYPE_CODE:
+                    raise ValueError(f"pack_weights: unsupported destination dtype {dt}")
+                d_ptr = dt_ptr = None
+                dld = dtld = 0
+                if dst is not None:
+                    d2, dld = _rows2d(dst, "dst")
+                    if tuple(d2.shape) != (rows, cols) or dst.dtype != dt:
+                        raise ValueError(f"pack_weights: job {q}: dst {tuple(dst.shape)} vs src {tuple(src.shape)}")
+                    d_ptr = d2.data_ptr()
+                if dst_t is not None:
+                    t2, dtld = _rows2d(dst_t, "dst_t")
+                    if tuple(t2.shape) != (cols, rows) or dst_t.dtype != dt:
+                        raise ValueError(f"pack_weights: job {q}: dst_t {tuple(dst_t.shape)} vs src {tuple(src.shape)}")
+                    dt_ptr = t2.data_ptr()
+                arr[q] = PackJobC(s2.data_ptr(), d_ptr, dt_ptr, rows, cols, sld, dld, dtld, DTYPE_CODE[dt], 0)
+                self._keep += [src, dst, dst_t]
+            self._arrs.append(arr)
+
+    def run(self):
+        for arr in self._arrs:
+            _check(lib().phc_pack_weights(arr, len(arr), _stream()), "phc_pack_weights")
 
 
 def obs_half(obs, mean, var, eps, clip, out, rows=None):

@@ -406,9 +406,12 @@ def train(components, info, utilization=None):
                         if tail_coefs is None:
                             tail_coefs = ppo_coefs(cfg, pol.soft_bound)
                         # every gradient of this backward has one writer that stores it: the flat
-                        # buffer need not be zeroed first (AMP adds the discriminator's on top)
-                        store_grads = STORE_GRADS and not info.use_amp_obs and isinstance(components.optimizer,
-                                                                                          FlatAdam)
+                        # buffer need not be zeroed first.  Not with a second gradient source: AMP
+                        # adds the discriminator's on top, and the L2-init term's AccumulateGrad
+                        # nodes run BEFORE this node's backward (created later, higher sequence
+                        # number), so a store would overwrite their gradient
+                        store_grads = (STORE_GRADS and not info.use_amp_obs and cfg.l2_reg_coef == 0
+                                       and isinstance(components.optimizer, FlatAdam))
                         loss, st = fused_ppo_loss(pol, obs, atn, log_probs, adv, ms, val, ret, tail_coefs,
                                                   store_grads=store_grads)
                     elif fused_obj:
@@ -457,12 +460,16 @@ def train(components, info, utilization=None):
                     if info.use_amp_obs:
                         # agent rows, replay rows and demo rows through the discriminator in one
                         # pass (core.py:336-344 calls it twice; rows are independent)
+                        idx_agent = experience.b_amp_idx[mb][:amp_mb]
+                        idx_replay = experience.b_amp_rep_idx[mb][:amp_mb]
                         with autocast(cfg):
                             d_all = pol.discriminate_rows(
-                                [(experience.amp_obs, experience.b_amp_idx[mb][:amp_mb]),
-                                 (experience.amp_obs_replay, experience.b_amp_rep_idx[mb][:amp_mb]),
+                                [(experience.amp_obs, idx_agent), (experience.amp_obs_replay, idx_replay),
                                  (amp_obs_demo, None)]).float()
-                        d_agent, d_demo = d_all[:2 * amp_mb], d_all[2 * amp_mb:]
+                        # a minibatch may hold fewer than amp_mb rows (minibatch_size < num_envs):
+                        # split at the agent + replay rows actually gathered, not at 2 * amp_mb
+                        n_agent = idx_agent.numel() + idx_replay.numel()
+                        d_agent, d_demo = d_all[:n_agent], d_all[n_agent:]
                         bce = torch.nn.BCEWithLogitsLoss()
                         disc_loss = 0.5 * (bce(d_agent, torch.zeros_like(d_agent)) + bce(d_demo, torch.ones_like(d_demo)))
                         # core.py:394-395

@@ -68,7 +68,8 @@ __global__ __launch_bounds__(256) void k_disc_head_fwd(const T *__restrict__ h, 
       if (reward) {
         const float prob = 1.0f / (1.0f + expf(-l));
         const float q = 1.0f - prob;
-        reward[r] = -logf(q > 1.0e-4f ? q : 1.0e-4f);
+        // torch.maximum(1 - prob, 1e-4) propagates a NaN (a diverged discriminator stays visible)
+        reward[r] = -logf(q != q ? q : (q > 1.0e-4f ? q : 1.0e-4f));
       }
     }
   }

@@ -293,9 +293,78 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_into(ReduceJobs js) {
   }
 }
 
+// --------------------------------------------------------------- pack_weights --
+// GEMM-operand refresh after an optimizer step: 64 x 64 tiles of every fp32 parameter staged
+// through LDS (coalesced row reads), written converted row-wise (dst) and column-wise (dst_t: the
+// transpose, coalesced along the source's rows).  One launch for all of a policy's operands.
+struct PackJobs {
+  phc_pack_job j[PHC_MAX_PACK_JOBS];
+  int64_t first_block[PHC_MAX_PACK_JOBS + 1];
+  int64_t tiles_c[PHC_MAX_PACK_JOBS];
+  int n;
+};
+constexpr int kPackTile = 64, kPackThreads = 256;
+
+__device__ __forceinline__ void pack_store(void *base, int64_t idx, int32_t dt, float v) {
+  if (dt == PHC_DT_F16) static_cast<_Float16 *>(base)[idx] = (_Float16)v;  // RNE conversions
+  else if (dt == PHC_DT_BF16) static_cast<__bf16 *>(base)[idx] = (__bf16)v;
+  else static_cast<float *>(base)[idx] = v;
+}
+
+__global__ __launch_bounds__(kPackThreads) void k_pack_weights(PackJobs js) {
+  __shared__ float tile[kPackTile][kPackTile + 1];
+  int q = 0;
+  while (q + 1 < js.n && (int64_t)blockIdx.x >= js.first_block[q + 1]) ++q;
+  const phc_pack_job &job = js.j[q];
+  const int64_t t = (int64_t)blockIdx.x - js.first_block[q];
+  const int64_t r0 = (t / js.tiles_c[q]) * kPackTile, c0 = (t % js.tiles_c[q]) * kPackTile;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int rr = wv; rr < kPackTile; rr += kPackThreads / 64) {
+    const int64_t r = r0 + rr, c = c0 + lane;
+    const bool in = r < job.rows && c < job.cols;
+    const float v = in ? job.src[r * job.src_ld + c] : 0.0f;
+    tile[rr][lane] = v;
+    if (in && job.dst) pack_store(job.dst, r * job.dst_ld + c, job.dtype, v);
+  }
+  if (!job.dst_t) return;
+  __syncthreads();
+  for (int cc = wv; cc < kPackTile; cc += kPackThreads / 64) {  // dst_t row c0 + cc, columns r0 + lane
+    const int64_t c = c0 + cc, r = r0 + lane;
+    if (c < job.cols && r < job.rows) pack_store(job.dst_t, c * job.dst_t_ld + r, job.dtype, tile[lane][cc]);
+  }
+}
+
 }  // namespace phc
 
 using namespace phc;
+
+extern "C" int phc_pack_weights(const phc_pack_job *jobs, int32_t num_jobs, void *stream) {
+  PHC_REQUIRE(jobs && num_jobs >= 0 && num_jobs <= PHC_MAX_PACK_JOBS, "pack_weights: 0..%d jobs", PHC_MAX_PACK_JOBS);
+  PackJobs js{};
+  int64_t blocks = 0;
+  int n = 0;
+  for (int q = 0; q < num_jobs; ++q) {
+    const phc_pack_job &j = jobs[q];
+    PHC_REQUIRE(j.rows >= 0 && j.cols >= 0 && j.src_ld >= j.cols, "pack_weights: job %d bad shape", q);
+    PHC_REQUIRE(j.dtype == PHC_DT_F32 || j.dtype == PHC_DT_F16 || j.dtype == PHC_DT_BF16,
+                "pack_weights: job %d bad dtype", q);
+    if (j.rows * j.cols == 0 || (!j.dst && !j.dst_t)) continue;
+    PHC_REQUIRE(j.src, "pack_weights: job %d null source", q);
+    PHC_REQUIRE(!j.dst || j.dst_ld >= j.cols, "pack_weights: job %d dst_ld < cols", q);
+    PHC_REQUIRE(!j.dst_t || j.dst_t_ld >= j.rows, "pack_weights: job %d dst_t_ld < rows", q);
+    js.j[n] = j;
+    js.first_block[n] = blocks;
+    js.tiles_c[n] = (j.cols + kPackTile - 1) / kPackTile;
+    blocks += ((j.rows + kPackTile - 1) / kPackTile) * js.tiles_c[n];
+    ++n;
+  }
+  if (n == 0) return PHC_OK;
+  js.first_block[n] = blocks;
+  js.n = n;
+  PHC_REQUIRE(blocks < (1ll << 31), "pack_weights: too large");
+  hipLaunchKernelGGL(k_pack_weights, dim3((unsigned)blocks), dim3(kPackThreads), 0, as_stream(stream), js);
+  return check_launch("pack_weights");
+}
 
 extern "C" int phc_reduce_into(const phc_reduce_job *jobs, int32_t num_jobs, void *stream) {
   PHC_REQUIRE(jobs && num_jobs >= 0 && num_jobs <= PHC_MAX_REDUCE_JOBS, "reduce_into: 0..%d jobs",

@@ -145,8 +145,11 @@ class FlatGrads:
 def broadcast_params(module, src=0):
     if not is_dist():
         return
+    from .policies import weight_cache
+
     for t in list(module.parameters()) + list(module.buffers()):
         dist.broadcast(t.data, src)
+    weight_cache.bump()  # written through .data: invisible to the version counters
 
 
 def global_mean_std(x):

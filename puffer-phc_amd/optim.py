@@ -17,6 +17,7 @@ import math
 import torch
 
 from . import _native as N
+from .policies import weight_cache
 
 _STATE_BYTES = ctypes.sizeof(N.OptStateC)
 
@@ -103,6 +104,7 @@ class FlatAdam(torch.optim.Adam):
                 self._i[1] = extra["growth_tracker"]
                 self._i[3] = extra["skipped"]
         self._bind_state()
+        weight_cache.bump()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -148,4 +150,7 @@ class FlatAdam(torch.optim.Adam):
                                       self.param_init.data_ptr() if self.param_init is not None else None,
                                       self._ws.data_ptr(), N._stream()),
                  "phc_opt_step")
+        # the parameters changed behind torch's version counters: every GEMM-operand cache of
+        # them is stale now (policies/weight_cache.py)
+        weight_cache.bump()
         return self.norms

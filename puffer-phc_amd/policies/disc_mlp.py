@@ -17,18 +17,20 @@ loss of agent / replay rows against demo rows, with gradients).  Here, in the f1
           reward in the same launch), its backward producing the second layer's input gradient
 
 Parameters stay the reference's nn.Linear modules (state-dict keys _disc_mlp.0 / .2,
-_disc_logits); the half-precision weight copies are a cache keyed on parameter versions.
+_disc_logits); the half-precision weight copies are a cache keyed on parameter versions and the
+optimizer generation (weight_cache.py), refreshed by one phc_pack_weights launch.
 """
 
 import torch
 
 from .. import _native as N
 from .twin_mlp import _compute_dtype, _pad64, _wgrad_splits, _wgrad_tiles
+from .weight_cache import cache_key, layout_key
 
 
 class DiscOperands:
     def __init__(self):
-        self.key = None
+        self.key = self.plan_key = self.plan = None
         self.w1 = self.w2 = self.w2t = None
         self.b1 = self.b2 = None
 
@@ -54,20 +56,24 @@ def mfma_disc_supported(pol, dtype):
 def disc_operands(pol, dtype):
     l1, l2, _ = _linears(pol)
     ps = disc_params(pol)
-    key = (dtype,) + tuple((p._version, p.data_ptr()) for p in ps)
+    key = cache_key(dtype, ps)
     ops = pol.__dict__.setdefault("_disc_ops", DiscOperands())
     if ops.key == key:
         return ops
     with torch.no_grad():
         n1, k1 = l1.weight.shape
-        if ops.w1 is None or ops.w1.dtype != dtype:
+        fresh = ops.w1 is None or ops.w1.dtype != dtype
+        if fresh:
             dev = l1.weight.device
             ops.w1 = torch.zeros((n1, _pad64(k1)), dtype=dtype, device=dev)
             ops.w2 = torch.empty(l2.weight.shape, dtype=dtype, device=dev)
             ops.w2t = torch.empty((l2.weight.shape[1], l2.weight.shape[0]), dtype=dtype, device=dev)
-        ops.w1[:, :k1].copy_(l1.weight)
-        ops.w2.copy_(l2.weight)
-        ops.w2t.copy_(l2.weight.t())
+        lk = layout_key(dtype, ps)
+        if fresh or ops.plan_key != lk:
+            ops.plan = N.PackPlan([(l1.weight.detach(), ops.w1[:, :k1], None),
+                                   (l2.weight.detach(), ops.w2, ops.w2t)])
+            ops.plan_key = lk
+        ops.plan.run()
         ops.b1 = l1.bias.detach().float().contiguous()
         ops.b2 = l2.bias.detach().float().contiguous()
     ops.key = key
@@ -105,10 +111,17 @@ def _forward(ops, l3, x):
 def _weight_grad_sum(g, z, n_valid=None):
     """dW = g^T z [m, n_valid] fp32 over all rows (split-K MFMA partials + one reduce)."""
     R = g.shape[0]
-    S = _wgrad_splits(_wgrad_tiles(g[None], z[None]), R, g.device) if R % 64 == 0 else 1
-    while R % (S * 64):
-        S //= 2
-    part = N.weight_grad(g, z, max(S, 1))  # [S, 1, m, n]
+    if R % 64:
+        # phc_weight_grad reduces whole 64-row chunks: zero rows (which add nothing to g^T z) pad
+        # a ragged row count, e.g. AMP training with num_envs not a multiple of 64
+        Rp = -(-R // 64) * 64
+        gp = torch.zeros((Rp, g.shape[1]), dtype=g.dtype, device=g.device)
+        zp = torch.zeros((Rp, z.shape[1]), dtype=z.dtype, device=z.device)
+        gp[:R].copy_(g)
+        zp[:R].copy_(z)
+        g, z, R = gp, zp, Rp
+    S = _wgrad_splits(_wgrad_tiles(g[None], z[None]), R, g.device)
+    part = N.weight_grad(g, z, S)  # [S, 1, m, n]
     nv = n_valid or part.shape[3]
     out = torch.empty((part.shape[2], nv), dtype=torch.float32, device=g.device)
     N.reduce_into([(part[:, 0, :, :nv], out)], accumulate=False)

@@ -6,8 +6,8 @@ goes through ONE GEMM against the stacked first-layer weights ([2*2048, 934]), l
 batched GEMMs over the two trunks ([2, M, K] x [2, K, N]), and every bias-add / SiLU /
 SiLU-backward / bias-gradient between the GEMMs is one fused HIP kernel (phc_bias_act_fwd,
 phc_act_bwd).  Parameters stay the reference's nn.Linear modules (same state-dict keys); the
-stacked weights are a cache in the GEMM dtype, rebuilt when a parameter's version changes
-(i.e. after each optimizer step).
+stacked weights are a cache in the GEMM dtype, rebuilt when a parameter's version or the
+optimizer generation changes (weight_cache.py: after each optimizer step).
 
 GEMM arithmetic follows the autocast context: fp32 storage with torch's "high" matmul
 precision (hipBLASLt xf32) outside autocast, fp16 / bf16 operands inside.  In the half-precision
@@ -28,6 +28,7 @@ import os
 import torch
 
 from .. import _native as N
+from .weight_cache import cache_key, layout_key
 
 
 def _compute_dtype():
@@ -110,8 +111,7 @@ class TwinWeights:
     def get(self, dtype):
         """Stacked weights for `dtype`; refreshed IN PLACE when a parameter changed, so a captured
         rollout graph that reads these buffers sees every optimizer update."""
-        ps = self.params()
-        key = (dtype,) + tuple((p._version, p.data_ptr()) for p in ps)
+        key = cache_key(dtype, self.params())
         if key == self._key:
             return self.w, self.b
         with torch.no_grad():
@@ -149,10 +149,13 @@ class MfmaOperands:
     """Operands of the hand-written MFMA GEMM path (phc_twin_gemm) in a half-precision dtype:
     the first layer's stacked weight zero-padded to K % 64 == 0, the stacked [2, N, K] weights
     of layers 2..L (forward B operands) and their transposes [2, K, N] (input-gradient B
-    operands).  Refreshed in place, like TwinWeights.get."""
+    operands), the stacked fp32 biases.  Refreshed in place (a captured rollout graph reads
+    these buffers) by one phc_pack_weights launch."""
 
     def __init__(self):
         self.key = None
+        self.plan_key = None
+        self.plan = None
         self.w0 = None
         self.w, self.wt, self.b = [], [], []
 
@@ -166,9 +169,21 @@ def mfma_supported(weights):
     return True
 
 
+def _pack_jobs(weights, ops):
+    a0, c0 = weights.pairs[0]
+    n0, k0 = a0.weight.shape
+    jobs = [(a0.weight.detach(), ops.w0[:n0, :k0], None), (c0.weight.detach(), ops.w0[n0:, :k0], None)]
+    for i, (a, c) in enumerate(weights.pairs):
+        na = a.bias.shape[0]
+        jobs += [(a.bias.detach(), ops.b[i][:na], None), (c.bias.detach(), ops.b[i][na:], None)]
+    for i, (a, c) in enumerate(weights.pairs[1:]):
+        jobs += [(a.weight.detach(), ops.w[i][0], ops.wt[i][0]), (c.weight.detach(), ops.w[i][1], ops.wt[i][1])]
+    return jobs
+
+
 def mfma_operands(weights, dtype):
     ps = weights.params()
-    key = (dtype,) + tuple((p._version, p.data_ptr()) for p in ps)
+    key = cache_key(dtype, ps)
     ops = weights.__dict__.setdefault("_mfma", MfmaOperands())
     if ops.key == key:
         return ops
@@ -184,16 +199,10 @@ def mfma_operands(weights, dtype):
                       for a, _ in weights.pairs[1:]]
             ops.b = [torch.empty(2 * a.bias.shape[0], dtype=torch.float32, device=a.bias.device)
                      for a, _ in weights.pairs]
-        ops.w0[:n0, :k0].copy_(a0.weight)
-        ops.w0[n0:, :k0].copy_(c0.weight)
-        for i, (a, c) in enumerate(weights.pairs):
-            ops.b[i][:a.bias.shape[0]].copy_(a.bias)
-            ops.b[i][a.bias.shape[0]:].copy_(c.bias)
-        for i, (a, c) in enumerate(weights.pairs[1:]):
-            ops.w[i][0].copy_(a.weight)
-            ops.w[i][1].copy_(c.weight)
-            ops.wt[i][0].copy_(a.weight.t())
-            ops.wt[i][1].copy_(c.weight.t())
+        lk = layout_key(dtype, ps)
+        if fresh or ops.plan_key != lk:
+            ops.plan, ops.plan_key = N.PackPlan(_pack_jobs(weights, ops)), lk
+        ops.plan.run()
     ops.key = key
     return ops
 
