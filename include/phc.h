@@ -236,6 +236,14 @@ int phc_rms_update(const float *x, int64_t rows, int64_t cols, float *mean, floa
                    void *workspace, void *stream);
 int phc_rms_normalize(const float *x, float *y, int64_t rows, int64_t cols, const float *mean,
                       const float *var, float eps, float clip, void *stream);
+/* R17 under data parallelism: phc_rms_moments writes this rank's batch moments
+ * moments[cols][2] = (mean, M2) in float64 (same chunked Chan merge as phc_rms_update);
+ * the caller gathers every rank's moments [parts][cols][2] and row counts part_rows [parts] and
+ * phc_rms_apply merges them in part order (identical on every rank) and applies the running
+ * update + count increment.  With one part the result equals phc_rms_update's bit for bit. */
+int phc_rms_moments(const float *x, int64_t rows, int64_t cols, double *moments, void *workspace, void *stream);
+int phc_rms_apply(const double *moments, const double *part_rows, int32_t parts, int64_t cols, float *mean,
+                  float *var, float *count, void *stream);
 
 /* R19/R21: fused epilogues of the twin actor/critic SiLU trunks (policies/phc_policy.py:10-61:
  * nn.Linear bias + nn.SiLU forward, their backward and the bias gradient).  A twin tensor holds

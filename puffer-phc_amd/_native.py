@@ -237,6 +237,8 @@ _EXPORTS = {
     "phc_gae": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.c_float, ctypes.c_float, c_vp, c_vp, c_vp]),
     "phc_rms_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
     "phc_rms_update": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "phc_rms_moments": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "phc_rms_apply": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "phc_rms_normalize": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, ctypes.c_float,
                                           c_vp]),
     "phc_disc_head_bwd_blocks": (c_i64, [c_i64]),
@@ -1094,6 +1096,29 @@ def rms_update(x, mean, var, count, workspace=None):
                               _ptr(count, torch.float32, (1,), "count"), workspace.data_ptr(), _stream())
     _check(rc, "phc_rms_update")
     return workspace
+
+
+def rms_moments(x, workspace=None):
+    """This rank's batch moments [cols, 2] float64 = (mean, M2) of x [rows, cols] (phc_rms_moments)."""
+    rows, cols = x.shape
+    need = int(lib().phc_rms_workspace_bytes(rows, cols))
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
+    mom = torch.empty((cols, 2), dtype=torch.float64, device=x.device)
+    _check(lib().phc_rms_moments(_ptr(x, torch.float32, (rows, cols), "x"), rows, cols, mom.data_ptr(),
+                                 workspace.data_ptr(), _stream()), "phc_rms_moments")
+    return mom, workspace
+
+
+def rms_apply(moments, part_rows, mean, var, count):
+    """Merge every rank's moments [parts, cols, 2] (rows per part: part_rows [parts] float64) in
+    part order and apply the running update (phc_rms_apply)."""
+    parts, cols, _ = moments.shape
+    _check(lib().phc_rms_apply(_ptr(moments, torch.float64, (parts, cols, 2), "moments"),
+                               _ptr(part_rows, torch.float64, (parts,), "part_rows"), parts, cols,
+                               _ptr(mean, torch.float32, None, "running_mean"),
+                               _ptr(var, torch.float32, None, "running_var"),
+                               _ptr(count, torch.float32, (1,), "count"), _stream()), "phc_rms_apply")
 
 
 def rms_normalize(x, mean, var, eps=1e-5, clip=10.0, out=None):

@@ -124,12 +124,12 @@ __global__ __launch_bounds__(kRmsCols) void k_rms_partial(const float *__restric
   p[1] = m2;
 }
 
-__global__ __launch_bounds__(kRmsCols) void k_rms_merge(const double *__restrict__ part, int64_t rows, int64_t cols,
-                                                        int64_t nchunks, float *__restrict__ rmean,
-                                                        float *__restrict__ rvar, const float *__restrict__ count) {
-  const int64_t col = (int64_t)blockIdx.x * kRmsCols + threadIdx.x;
-  if (col >= cols) return;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
+// Chan merge of a column's row-chunk partials (mean, M2) in chunk order
+__device__ __forceinline__ void rms_chunk_merge(const double *__restrict__ part, int64_t rows, int64_t cols,
+                                                int64_t nchunks, int64_t col, double &n, double &mean, double &m2) {
+  n = 0.0;
+  mean = 0.0;
+  m2 = 0.0;
   for (int64_t k = 0; k < nchunks; ++k) {
     const double nb = (double)((k + 1) * kRmsRows < rows ? kRmsRows : rows - k * kRmsRows);
     const double mb = part[(k * cols + col) * 2];
@@ -140,11 +140,59 @@ __global__ __launch_bounds__(kRmsCols) void k_rms_merge(const double *__restrict
     m2 += m2b + delta * delta * (n * nb / tot);
     n = tot;
   }
+}
+
+__device__ __forceinline__ void rms_running_update(float *__restrict__ rmean, float *__restrict__ rvar,
+                                                   const float *__restrict__ count, int64_t col, double mean,
+                                                   double m2, double n) {
   const float bm = (float)mean;
   const float bv = (float)(m2 / n);
   const float w = 1.0f / count[0];
   rmean[col] = rmean[col] * (1.0f - w) + bm * w;
   rvar[col] = rvar[col] * (1.0f - w) + bv * w;
+}
+
+__global__ __launch_bounds__(kRmsCols) void k_rms_merge(const double *__restrict__ part, int64_t rows, int64_t cols,
+                                                        int64_t nchunks, float *__restrict__ rmean,
+                                                        float *__restrict__ rvar, const float *__restrict__ count) {
+  const int64_t col = (int64_t)blockIdx.x * kRmsCols + threadIdx.x;
+  if (col >= cols) return;
+  double n, mean, m2;
+  rms_chunk_merge(part, rows, cols, nchunks, col, n, mean, m2);
+  rms_running_update(rmean, rvar, count, col, mean, m2, n);
+}
+
+// data parallel: this rank's batch moments (mean, M2) per column, exchanged by the caller
+__global__ __launch_bounds__(kRmsCols) void k_rms_moments(const double *__restrict__ part, int64_t rows, int64_t cols,
+                                                          int64_t nchunks, double *__restrict__ mom) {
+  const int64_t col = (int64_t)blockIdx.x * kRmsCols + threadIdx.x;
+  if (col >= cols) return;
+  double n, mean, m2;
+  rms_chunk_merge(part, rows, cols, nchunks, col, n, mean, m2);
+  mom[col * 2] = mean;
+  mom[col * 2 + 1] = m2;
+}
+
+// every rank's moments merged in rank order (the same result on every rank), then the running
+// update; with one part this is exactly k_rms_merge's result
+__global__ __launch_bounds__(kRmsCols) void k_rms_apply(const double *__restrict__ mom, const double *__restrict__ prows,
+                                                        int32_t parts, int64_t cols, float *__restrict__ rmean,
+                                                        float *__restrict__ rvar, const float *__restrict__ count) {
+  const int64_t col = (int64_t)blockIdx.x * kRmsCols + threadIdx.x;
+  if (col >= cols) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int32_t k = 0; k < parts; ++k) {
+    const double nb = prows[k];
+    if (nb <= 0.0) continue;
+    const double mb = mom[((int64_t)k * cols + col) * 2];
+    const double m2b = mom[((int64_t)k * cols + col) * 2 + 1];
+    const double tot = n + nb;
+    const double delta = mb - mean;
+    mean += delta * (nb / tot);
+    m2 += m2b + delta * delta * (n * nb / tot);
+    n = tot;
+  }
+  rms_running_update(rmean, rvar, count, col, mean, m2, n);
 }
 
 __global__ void k_count_inc(float *count) { count[0] = count[0] + 1.0f; }
@@ -207,6 +255,32 @@ extern "C" int phc_rms_update(const float *x, int64_t rows, int64_t cols, float 
   if (int rc = check_launch("rms_partial")) return rc;
   hipLaunchKernelGGL(k_rms_merge, dim3(gx), dim3(kRmsCols), 0, s, part, rows, cols, nchunks, mean, var, count);
   if (int rc = check_launch("rms_merge")) return rc;
+  hipLaunchKernelGGL(k_count_inc, dim3(1), dim3(1), 0, s, count);
+  return check_launch("rms_count");
+}
+
+extern "C" int phc_rms_moments(const float *x, int64_t rows, int64_t cols, double *moments, void *workspace,
+                               void *stream) {
+  PHC_REQUIRE(x && moments && workspace, "rms_moments: null argument");
+  PHC_REQUIRE(rows > 0 && cols > 0, "rms_moments: empty batch");
+  hipStream_t s = as_stream(stream);
+  const int64_t nchunks = (rows + kRmsRows - 1) / kRmsRows;
+  double *part = reinterpret_cast<double *>(workspace);
+  const unsigned gx = (unsigned)((cols + kRmsCols - 1) / kRmsCols);
+  hipLaunchKernelGGL(k_rms_partial, dim3(gx, (unsigned)nchunks), dim3(kRmsCols), 0, s, x, rows, cols, part);
+  if (int rc = check_launch("rms_partial")) return rc;
+  hipLaunchKernelGGL(k_rms_moments, dim3(gx), dim3(kRmsCols), 0, s, part, rows, cols, nchunks, moments);
+  return check_launch("rms_moments");
+}
+
+extern "C" int phc_rms_apply(const double *moments, const double *part_rows, int32_t parts, int64_t cols, float *mean,
+                             float *var, float *count, void *stream) {
+  PHC_REQUIRE(moments && part_rows && mean && var && count, "rms_apply: null argument");
+  PHC_REQUIRE(parts > 0 && cols > 0, "rms_apply: empty");
+  hipStream_t s = as_stream(stream);
+  const unsigned gx = (unsigned)((cols + kRmsCols - 1) / kRmsCols);
+  hipLaunchKernelGGL(k_rms_apply, dim3(gx), dim3(kRmsCols), 0, s, moments, part_rows, parts, cols, mean, var, count);
+  if (int rc = check_launch("rms_apply")) return rc;
   hipLaunchKernelGGL(k_count_inc, dim3(1), dim3(1), 0, s, count);
   return check_launch("rms_count");
 }

@@ -19,7 +19,9 @@ import torch.distributed as dist
 
 
 def is_dist():
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    """A process group is up: every collective below runs (a 1-rank group included, so the
+    data-parallel path can be exercised on one GPU; without a group they are all no-ops)."""
+    return dist.is_available() and dist.is_initialized()
 
 
 def world_size():
@@ -30,9 +32,10 @@ def rank():
     return dist.get_rank() if is_dist() else 0
 
 
-def init_from_env(backend=None):
-    """Initialise from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*)."""
-    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+def init_from_env(backend=None, force=False):
+    """Initialise from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*); a single
+    process only with force=True (a 1-rank group: the data-parallel path on one GPU)."""
+    if (int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not force) or dist.is_initialized():
         return rank(), world_size()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend is None:

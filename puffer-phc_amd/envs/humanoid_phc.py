@@ -329,15 +329,16 @@ class HumanoidPHC:
         self._global_offset[:, :2] = self._humanoid_root_states[:, :2] - root[:, :2]
         self.reset()
 
-    def begin_seq_motion_samples(self):
-        self._motion_sample_start_idx = 0
+    def begin_seq_motion_samples(self, start_idx=0):
+        self._motion_sample_start_idx = start_idx
         self._motion_lib.load_motions(skeleton_trees=self.skeleton_trees, gender_betas=self.humanoid_shapes.cpu(),
                                       limb_weights=self.humanoid_limb_and_weights.cpu(), random_sample=False,
                                       start_idx=self._motion_sample_start_idx)
         self.reset()
 
     def forward_motion_samples(self):
-        self._motion_sample_start_idx += self.cfg.num_envs
+        # eval sharded over data-parallel ranks: this rank's next batch is `world` batches on
+        self._motion_sample_start_idx += self.cfg.num_envs * getattr(self, "_eval_world", 1)
         self._motion_lib.load_motions(skeleton_trees=self.skeleton_trees, gender_betas=self.humanoid_shapes.cpu(),
                                       limb_weights=self.humanoid_limb_and_weights.cpu(), random_sample=False,
                                       start_idx=self._motion_sample_start_idx)
@@ -362,8 +363,12 @@ class HumanoidPHC:
     def get_motion_steps(self):
         return self._motion_lib.get_motion_num_steps()
 
-    def toggle_eval_mode(self):
-        """humanoid_phc.py:1424-1436."""
+    def toggle_eval_mode(self, shard=(0, 1)):
+        """humanoid_phc.py:1424-1436.  shard = (rank, world): the sequential motion batches are
+        dealt round-robin over the data-parallel ranks (batch b on rank b % world; eval_stats.py
+        merges the ranks' results)."""
+        rank, world = shard
+        self._eval_world = int(world)
         self.flag_test = True
         self.flag_im_eval = True
         self._termination_distances[:] = 0.5
@@ -371,13 +376,14 @@ class HumanoidPHC:
         if len(self._reset_bodies_id) > 15:
             self._reset_bodies_id = list(self._eval_track_bodies_id)
         self._build_step_params()
-        self.begin_seq_motion_samples()
+        self.begin_seq_motion_samples(int(rank) * self.cfg.num_envs)
         return self._motion_lib._num_unique_motions
 
     def untoggle_eval_mode(self, failed_keys):
         """humanoid_phc.py:1438-1454."""
         self.flag_test = False
         self.flag_im_eval = False
+        self._eval_world = 1
         self._termination_distances[:] = self._termination_distances_backup
         self._motion_lib = self._motion_train_lib
         self._reset_bodies_id = list(self._reset_bodies_id_backup)

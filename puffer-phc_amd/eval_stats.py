@@ -9,24 +9,94 @@ current batch of motions has been played out (or terminated); then the next batc
 last frame; per-motion MPJPE & co come from `metrics.compute_metrics_lite` over the recorded
 body positions.  The per-step positions are copied to the host as the reference does (the eval
 path is outside the training hot loop).
+
+Data parallel: the motion set is sharded over the ranks (batch b of num_envs
+motions is played by rank b % world), each rank keeps per-motion rows (terminated, lengths, metric
+sums), one all-reduce merges them, so every rank derives the same failed keys and PMCP sampling
+weights, which rank 0 then broadcasts (motion_lib.py:454-500).
 """
 
 import numpy as np
 import torch
 
+from . import distributed as D
 from .metrics import compute_metrics_lite
+
+METRICS = ("mpjpe_g", "mpjpe_l", "mpjpe_pa", "accel_dist", "vel_dist")
+# per-motion columns of the shard merge: evaluated, terminated, motion length, played steps, then
+# (sum over frames, frame count) of every metric
+COLS = 4 + 2 * len(METRICS)
+
+
+def merge_eval_shards(rows, reduce_sum=None):
+    """Merge the per-motion rows [n, COLS] of every rank's eval shard (disjoint motion sets, zero
+    rows elsewhere) by one all-reduce (eval is sharded over data-parallel
+    ranks; every rank then holds the whole-set result)."""
+    reduce_sum = D.allreduce_sum_ if reduce_sum is None else reduce_sum
+    out = reduce_sum(rows.clone())
+    if bool((out[:, 0] > 1.5).any()):
+        raise RuntimeError("eval shards overlap: a motion was evaluated on more than one rank")
+    return out
+
+
+def summarize_eval(rows):
+    """Reference results (scripts/train.py:187-236) from merged per-motion rows."""
+    r = rows.double().cpu().numpy()
+    if not np.all(r[:, 0] == 1):
+        raise RuntimeError(f"{int((r[:, 0] != 1).sum())} motions were not evaluated")
+    terminated = r[:, 1] > 0.5
+    succ = ~terminated
+
+    def mean(sel, k):
+        s, c = r[sel, 4 + 2 * k].sum(), r[sel, 5 + 2 * k].sum()
+        return float(s / c) if c > 0 else float("nan")
+
+    all_p = {m: mean(slice(None), k) for k, m in enumerate(METRICS)}
+    succ_p = {m: mean(succ, k) for k, m in enumerate(METRICS)} if succ.any() else dict(all_p)
+    results = {
+        "eval/success_rate": float(1 - terminated.mean()),
+        "eval/mpjpe_all": all_p["mpjpe_g"],
+        "eval/mpjpe_succ": succ_p["mpjpe_g"],
+        "eval/accel_dist": succ_p["accel_dist"],
+        "eval/vel_dist": succ_p["vel_dist"],
+        "eval/mpjpel_all": all_p["mpjpe_l"],
+        "eval/mpjpel_succ": succ_p["mpjpe_l"],
+        "eval/mpjpe_pa": succ_p["mpjpe_pa"],
+    }
+    return results, terminated, r[:, 2].astype(np.int64), r[:, 3].astype(np.int64)
+
+
+def sync_sampling_state(motion_lib, src=0):
+    """After untoggle_eval_mode every rank updated its sampling weights from the same merged
+    failed keys; broadcast rank src's _sampling_prob / _termination_history anyway so the replicas
+    cannot drift (reference motion_lib.py:454-500 has one process)."""
+    if not D.is_dist():
+        return
+    import torch.distributed as dist
+
+    for name in ("_sampling_prob", "_termination_history"):
+        t = getattr(motion_lib, name).contiguous()
+        dist.broadcast(t, src)
+        setattr(motion_lib, name, t)
 
 
 class EvalStats:
-    def __init__(self, vec_env, failed_save_path=None, progress=True):
+    def __init__(self, vec_env, failed_save_path=None, progress=True, shard=None):
+        """shard = (rank, world): this rank evaluates motion batches rank, rank + world, ... of
+        num_envs motions each (default: the data-parallel rank / world size; (0, 1) is the
+        reference's sequential pass over every motion)."""
         self.task_env = vec_env.env
         self.num_envs = self.task_env.cfg.num_envs
         dev = self.task_env.device
         self.failed_save_path = failed_save_path
-        self.num_unique_motions = self.task_env.toggle_eval_mode()
+        self.rank, self.world = shard if shard is not None else (D.rank(), D.world_size())
+        self.num_unique_motions = self.task_env.toggle_eval_mode(shard=(self.rank, self.world))
+        # more ranks than motion batches: this rank has nothing to play, it only joins the merge
+        self.idle = self.task_env.motion_sample_start_idx >= self.num_unique_motions
         self.terminate_state = torch.zeros(self.num_envs, dtype=torch.bool, device=dev)
         self.played_steps_buf = torch.zeros(self.num_envs, dtype=torch.int16, device=dev)
         self.terminate_memory, self.motion_length, self.played_steps = [], [], []
+        self.batch_ids = []  # motion ids of every finished batch (this rank's shard, in order)
         self.mpjpe, self.mpjpe_all = [], []
         self.gt_pos, self.gt_pos_all = [], []
         self.pred_pos, self.pred_pos_all = [], []
@@ -39,19 +109,20 @@ class EvalStats:
         if progress:
             from tqdm import tqdm
 
-            self.pbar = tqdm(range(max(self.num_unique_motions // self.num_envs, 1)))
+            self.pbar = tqdm(range(max(self.num_unique_motions // (self.num_envs * self.world), 1)))
+
+    def _valid(self):
+        """Envs of the current batch that play a motion of the set (the batch may wrap around
+        past the last motion; those envs are not counted, scripts/train.py:119-130)."""
+        return min(self.num_envs, self.num_unique_motions - self.task_env.motion_sample_start_idx)
 
     def _batch_horizon(self, motion_num_steps):
         """Step count at which the current batch is complete (scripts/train.py:118-137)."""
         alive = ~self.terminate_state
         if not bool(alive.any()):
             return int(motion_num_steps.max())
-        last_id = self.num_unique_motions - 1
-        curr_ids = self.task_env.current_motion_ids
-        at_last = curr_ids == last_id
-        if bool(at_last.any()):
-            # more envs than remaining motions: envs past the last motion id are not counted
-            bound = int(at_last.nonzero()[0]) + 1
+        bound = self._valid()
+        if bound < self.num_envs:
             if bool(alive[:bound].any()):
                 horizon = int(motion_num_steps[:bound][alive[:bound]].max())
             else:
@@ -65,6 +136,8 @@ class EvalStats:
 
     def post_step_eval(self):
         """Book-keeping after one env step.  Returns (all motions evaluated, moved to next batch)."""
+        if self.idle:
+            return self.get_final_stats(), False
         env = self.task_env
         motion_num_steps = env.get_motion_steps()
         info = env.extras
@@ -83,11 +156,13 @@ class EvalStats:
         next_batch = False
         if self.curr_steps >= horizon or int(self.terminate_state.sum()) == self.num_envs:
             self.curr_steps = 0
-            self.terminate_memory.append(self.terminate_state.cpu().numpy())
-            steps = env.get_motion_steps().cpu().numpy()
+            start, bound = env.motion_sample_start_idx, self._valid()
+            self.batch_ids.append(np.arange(start, start + bound))
+            self.terminate_memory.append(self.terminate_state.cpu().numpy()[:bound])
+            steps = env.get_motion_steps().cpu().numpy()[:bound]
             self.motion_length.append(steps)
-            self.played_steps.append(self.played_steps_buf.cpu().numpy())
-            self.success_rate = 1 - np.concatenate(self.terminate_memory)[: self.num_unique_motions].mean()
+            self.played_steps.append(self.played_steps_buf.cpu().numpy()[:bound])
+            self.success_rate = 1 - np.concatenate(self.terminate_memory).mean()
 
             mpjpe = torch.stack(self.mpjpe)
             self.mpjpe_all.append([mpjpe[: (n - 1), i].mean() for i, n in enumerate(steps)])
@@ -96,7 +171,7 @@ class EvalStats:
             self.pred_pos_all += [pred[: (n - 1), i] for i, n in enumerate(steps)]
             self.gt_pos_all += [gt[: (n - 1), i] for i, n in enumerate(steps)]
 
-            if env.motion_sample_start_idx + self.num_envs >= self.num_unique_motions:
+            if start + self.world * self.num_envs >= self.num_unique_motions:
                 return self.get_final_stats(), next_batch
             next_batch = True
             env.forward_motion_samples()
@@ -111,40 +186,50 @@ class EvalStats:
                                       f"Succ rate: {self.success_rate:.3f} | Mpjpe: {mp:.3f}")
         return False, next_batch
 
-    def get_final_stats(self):
+    def local_rows(self):
+        """[n, COLS] float64 per-motion rows of this rank's shard (zero rows for other motions)."""
+        rows = torch.zeros((self.num_unique_motions, COLS), dtype=torch.float64)
+        if not self.batch_ids:
+            return rows
+        ids = np.concatenate(self.batch_ids)
+        m = compute_metrics_lite(self.pred_pos_all, self.gt_pos_all, concatenate=False)
+        loc = np.zeros((len(ids), COLS))
+        loc[:, 0] = 1.0
+        loc[:, 1] = np.concatenate(self.terminate_memory)
+        loc[:, 2] = np.concatenate(self.motion_length)
+        loc[:, 3] = np.concatenate(self.played_steps)
+        for k, name in enumerate(METRICS):
+            loc[:, 4 + 2 * k] = [float(np.sum(v)) for v in m[name]]
+            loc[:, 5 + 2 * k] = [float(len(v)) for v in m[name]]
+        rows[torch.from_numpy(ids)] = torch.from_numpy(loc)
+        return rows
+
+    def get_final_stats(self, reduce_sum=None):
         if self.pbar is not None:
             self.pbar.clear()
-        n = self.num_unique_motions
-        terminated = np.concatenate(self.terminate_memory)[:n]
-        succ = np.flatnonzero(~terminated).tolist()
-        pred_all, gt_all = self.pred_pos_all[:n], self.gt_pos_all[:n]
+        rows = self.local_rows()
+        if self.world > 1 or reduce_sum is not None:
+            dev = self.task_env.device if D.is_dist() else "cpu"
+            rows = merge_eval_shards(rows.to(dev), reduce_sum).cpu()
+        self.results, terminated, lengths, played = summarize_eval(rows)
+        self.success_rate = self.results["eval/success_rate"]
         self.failed_keys = self.task_env.motion_data_keys[terminated]
-        m_all = compute_metrics_lite(pred_all, gt_all)
-        m_succ = compute_metrics_lite([pred_all[i] for i in succ], [gt_all[i] for i in succ])
-        all_p = {k: float(np.mean(v)) for k, v in m_all.items()}
-        succ_p = {k: float(np.mean(v)) for k, v in m_succ.items()} if succ else dict(all_p)
-        self.results = {
-            "eval/success_rate": float(self.success_rate),
-            "eval/mpjpe_all": all_p["mpjpe_g"],
-            "eval/mpjpe_succ": succ_p["mpjpe_g"],
-            "eval/accel_dist": succ_p["accel_dist"],
-            "eval/vel_dist": succ_p["vel_dist"],
-            "eval/mpjpel_all": all_p["mpjpe_l"],
-            "eval/mpjpel_succ": succ_p["mpjpe_l"],
-            "eval/mpjpe_pa": succ_p["mpjpe_pa"],
-        }
         self.results_by_motion = {
             "motion_keys": self.task_env.motion_data_keys.tolist(),
-            "motion_length": np.concatenate(self.motion_length)[:n],
-            "played_steps": np.concatenate(self.played_steps)[:n],
+            "motion_length": lengths,
+            "played_steps": played,
             "success": ~terminated,
         }
         return True
 
     def update_env_and_close(self):
-        """Back to training mode; the termination history feeds the PMCP sampling weights."""
+        """Back to training mode; the termination history feeds the PMCP sampling weights, the
+        same merged failure set on every rank (then rank 0's weights broadcast)."""
         history = self.task_env.untoggle_eval_mode(self.failed_keys)
-        if self.failed_save_path:
+        if self.world > 1:
+            sync_sampling_state(self.task_env._motion_lib)
+            history = self.task_env._motion_lib._termination_history.clone()
+        if self.failed_save_path and D.rank() == 0:
             import joblib
 
             joblib.dump({"failed_keys": self.failed_keys, "termination_history": history}, self.failed_save_path)
@@ -153,8 +238,12 @@ class EvalStats:
 
 def eval_rollout(vec_env, policy, eval_stats, max_steps=None):
     """scripts/train.py:392-429 rollout with EvalStats: deterministic actions until every motion
-    of the eval set has been played.  Returns the number of env steps taken."""
+    of this rank's eval shard has been played (an idle rank only joins the final merge).
+    Returns the number of env steps taken."""
     pol = policy.policy if hasattr(policy, "policy") else policy
+    if eval_stats.idle:
+        eval_stats.get_final_stats()
+        return 0
     pol.set_deterministic_action(True)
     obs, _ = vec_env.reset()
     steps = 0

@@ -3,14 +3,15 @@
 forward: clamp((x - mean) / sqrt(var + eps), -clip, clip) (phc_rms_normalize on device,
 differentiable w.r.t. nothing, like the reference's buffers-only module);
 update: whole-batch mean / biased var folded in with weight 1/count (phc_rms_update).
-Under torch.distributed the batch statistics are merged across ranks first so every replica
-keeps identical stats.
+Under torch.distributed the batch moments are merged across ranks first so every replica keeps
+identical stats.
 """
 
 import torch
 from torch import nn
 
 from .. import _native
+from .. import distributed as D
 
 
 class RunningNorm(nn.Module):
@@ -32,24 +33,25 @@ class RunningNorm(nn.Module):
     def update(self, x):
         x = x.float()
         assert x.dim() == 2, "x must be 2D"
-        if torch.distributed.is_available() and torch.distributed.is_initialized() and \
-                torch.distributed.get_world_size() > 1:
-            return self._update_distributed(x)
+        if not x.is_cuda:
+            raise RuntimeError("RunningNorm runs on the HIP path only (float32 [rows, features] device tensor)")
+        if D.is_dist():
+            return self._update_distributed(x.contiguous())
         self._ws = _native.rms_update(x.contiguous(), self.running_mean, self.running_var, self.count, self._ws)
 
     def _update_distributed(self, x):
-        """Global batch mean / biased var over all ranks' rows via one all-reduce of
-        (n, sum, sum of squares) in float64, then the reference's running update."""
-        n = torch.tensor([x.shape[0]], dtype=torch.float64, device=x.device)
-        s = x.double().sum(0)
-        s2 = (x.double() ** 2).sum(0)
-        buf = torch.cat([n, s, s2])
-        torch.distributed.all_reduce(buf)
-        F = x.shape[1]
-        n_tot = buf[0]
-        mean = buf[1:1 + F] / n_tot
-        var = (buf[1 + F:] / n_tot - mean * mean).clamp_min(0.0)
-        w = 1.0 / self.count
-        self.running_mean.copy_(self.running_mean * (1 - w) + mean.float()[None] * w)
-        self.running_var.copy_(self.running_var * (1 - w) + var.float()[None] * w)
-        self.count += 1
+        """The global batch's mean / biased var over all ranks' rows: each rank's (mean, M2) per
+        feature (phc_rms_moments, float64), one all-gather, the ranks' moments merged in rank
+        order on every rank (phc_rms_apply: identical stats on every replica), then the
+        reference's running update."""
+        import torch.distributed as dist
+
+        mom, self._ws = _native.rms_moments(x, self._ws)
+        ws = D.world_size()
+        moms = [torch.empty_like(mom) for _ in range(ws)]
+        dist.all_gather(moms, mom)
+        rows = torch.tensor([float(x.shape[0])], dtype=torch.float64, device=x.device)
+        all_rows = [torch.empty_like(rows) for _ in range(ws)]
+        dist.all_gather(all_rows, rows)
+        _native.rms_apply(torch.stack(moms).contiguous(), torch.cat(all_rows).contiguous(), self.running_mean,
+                          self.running_var, self.count)

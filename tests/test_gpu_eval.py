@@ -76,3 +76,81 @@ def test_eval_high_noise_reports_failures(golden):
     succ = stats.results_by_motion["success"]
     assert res["eval/success_rate"] == pytest.approx(succ.mean())
     assert (~succ).sum() == len(stats.failed_keys) > 0
+
+
+def _eval_shard_worker(rank, world, port, out_dir):
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import phc_amd_path
+
+    phc_amd_path.register()
+    import torch.distributed as dist
+
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig
+    from puffer_phc_amd.eval_stats import EvalStats, eval_rollout
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = dict(np.load(os.path.join(root, "tests", "golden", "motion_lib.npz")))
+        clips = {}
+        for i in range(int(g["num_input_motions"])):
+            q, t = g[f"in_quat_{i}"], g[f"in_trans_{i}"]
+            clips[f"synth_{i:02d}"] = {"pose_quat_global": q, "root_trans_offset": torch.from_numpy(t),
+                                       "pose_aa": np.zeros((q.shape[0], 72)), "fps": 30}
+
+        def run(shard, seed):
+            env = PHCPufferEnv(EnvConfig(num_envs=2, seed=seed, replay_pos_sigma=0.02, min_motion_len=-1),
+                               motion_data=clips)
+            torch.manual_seed(0)
+            policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+            stats = EvalStats(env, progress=False, shard=shard)
+            eval_rollout(env, policy, stats, max_steps=5000)
+            assert stats.results is not None
+            res = stats.update_env_and_close()
+            lib = env.env._motion_lib
+            return stats, res, lib
+
+        stats, res, lib = run(None, 10 + rank)  # the DP shard of this rank
+        out = {"ids": np.concatenate(stats.batch_ids).tolist(), "res": res,
+               "len": stats.results_by_motion["motion_length"].tolist(),
+               "played": stats.results_by_motion["played_steps"].tolist(),
+               "succ": stats.results_by_motion["success"].tolist(),
+               "prob": lib._sampling_prob.cpu().tolist(), "hist": lib._termination_history.cpu().tolist()}
+        if rank == 0:  # the reference's single sequential pass over every motion, same process
+            s1, r1, _ = run((0, 1), 10)
+            out["single_len"] = s1.results_by_motion["motion_length"].tolist()
+            out["single_succ"] = s1.results_by_motion["success"].tolist()
+            out["single_ids"] = np.concatenate(s1.batch_ids).tolist()
+        torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_eval_sharded_over_two_ranks(tmp_path):
+    """§8e(5): two data-parallel ranks (gloo, one GPU) play disjoint motion batches (rank 0:
+    batches 0 and 2, rank 1: batch 1 of 2 motions each), merge the per-motion results, and end
+    with the same results, failed keys and PMCP sampling weights; the merged per-motion lengths
+    and successes equal one rank's sequential pass over all 6 motions (low replay noise)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_eval_shard_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    assert r0["ids"] == [0, 1, 4, 5] and r1["ids"] == [2, 3]
+    assert r0["single_ids"] == list(range(6))
+    assert r0["res"] == r1["res"] and r0["len"] == r1["len"] and r0["succ"] == r1["succ"]
+    assert r0["prob"] == r1["prob"] and r0["hist"] == r1["hist"]
+    assert r0["len"] == r0["single_len"] and r0["succ"] == r0["single_succ"]
+    assert r0["res"]["eval/success_rate"] == 1.0
