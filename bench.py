@@ -21,12 +21,14 @@ available offline).  Policy weights are random-init (orthogonal, as the referenc
 shard across ranks (weak scaling); the PPO update all-reduces gradients and advantage
 statistics over RCCL.
 
-Roofline: the dominant kernel of the env step is phc_env_step (HBM-bound); algorithmic bytes
-per env-step = 10,886 (7,122 read + 3,764 written); achieved = bytes x envs /
-average kernel time from HIP start/stop events recorded by each launch's own dispatch
-(hipExtLaunchKernel, phc_env_step_timed) for every launch in the timed region.
-`traffic` = HBM bytes per launch from rocprofv3 PMC counters (2 x FETCH_SIZE + WRITE_SIZE,
-gfx950 correction) read from profiles/traffic_<envs>.json when present, else null.
+Roofline: with the replay physics the whole env phase is ONE launch, phc_env_step_replay
+(HBM-bound; R13 + the stand-in + the fused obs / reward / reset step): 11,714 algorithmic bytes per
+env-step (BYTES_PER_ENV_STEP_FUSED); with articulated physics the env step is phc_env_step,
+10,886 B (7,122 read + 3,764 written).  achieved = bytes x envs / average kernel
+time from HIP start/stop events recorded by each launch's own dispatch (hipExtLaunchKernel) for
+every launch in the timed region.  `traffic` = HBM bytes per launch from rocprofv3 PMC counters
+(2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) read from profiles/traffic[_fused]_<envs>.json
+when present, else null.
 
 cpu_baseline: the numpy oracle (oracle/phc_oracle.py) env step on the same 4096-env batch at
 1 thread and over all available cores (forked env shards), plus the C restatement of the
@@ -49,7 +51,12 @@ import phc_amd_path  # noqa: E402
 
 phc_amd_path.register()
 
-BYTES_PER_ENV_STEP = 10886
+BYTES_PER_ENV_STEP = 10886  # phc_env_step (K1+K2) after a separate physics launch
+# phc_env_step_replay (the default with replay physics): R13 + the stand-in + the env step in one
+# launch.  Reads 5,874 B: 4 frame rows 4,992 + the 2 dof-vel frame rows at t 552 + actions 276 +
+# scalars 54; writes 5,840 B: rigid bodies 1,248 + dof vel 276 + forces 276 + PD targets 276 + obs /
+# reward / flags / progress 3,764
+BYTES_PER_ENV_STEP_FUSED = 11714
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16 / bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
 DEFAULTS = {"env": (200, 20), "rollout": (64, 8), "ppo": (3, 1)}
@@ -465,9 +472,11 @@ def main():
     processed_all = whole_job_steps(counts, args.mode == "ppo", world)
 
     if rank == 0:
-        achieved = BYTES_PER_ENV_STEP * args.envs / kern_s / 1e9
+        fused = bool(getattr(env.env, "fused_env_step", False)) and args.physics == "replay"
+        env_bytes = BYTES_PER_ENV_STEP_FUSED if fused else BYTES_PER_ENV_STEP
+        achieved = env_bytes * args.envs / kern_s / 1e9
         traffic = None
-        tf = args.traffic_file or os.path.join(ROOT, "profiles", f"traffic_{args.envs}.json")
+        tf = args.traffic_file or os.path.join(ROOT, "profiles", f"traffic_{'fused_' if fused else ''}{args.envs}.json")
         if os.path.exists(tf):
             with open(tf) as f:
                 traffic = json.load(f).get("bytes_per_launch")
@@ -524,10 +533,13 @@ def main():
             out["roofline_physics"] = physics_roofline(args, phys_s, phys_launches)
             if not args.no_cpu_baseline:
                 out["cpu_baseline_physics"] = physics_cpu_baseline(args.cpu_seconds)
-        env_roof = {"bound": "hbm", "kernel": "phc_env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        env_roof = {"bound": "hbm",
+                    "kernel": "phc_env_step_replay (action->PD + replay physics + env step, one launch: the whole "
+                              "env phase)" if fused else "phc_env_step",
+                    "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     "kernel_us": kern_s * 1e6, "launches_timed": env_steps,
-                    "algorithmic_bytes_per_env_step": BYTES_PER_ENV_STEP}
+                    "algorithmic_bytes_per_env_step": env_bytes}
         if gemm_launches:
             # the dominant kernel of the PPO / rollout modes: the trunk GEMMs (MFMA-bound)
             tfs = gemm_flops / gemm_s / 1e12

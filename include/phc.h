@@ -181,6 +181,30 @@ int phc_actions_to_pd(const float *actions, float *pd_target, int64_t n, const f
 int phc_physics_replay(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
                        float pos_sigma, float force_scale, uint64_t seed, uint64_t counter, void *stream);
 
+/* R13 folded into the kernel that consumes the PD targets: the action -> PD-target map of
+ * phc_actions_to_pd as an argument block (pd_target is still written, as the env buffer). */
+typedef struct phc_pd_map {
+  const float *actions; /* [N, 69] policy actions */
+  float *pd_target;     /* [N, 69] written */
+  const float *offset;  /* [69] */
+  const float *scale;   /* [69] */
+  const uint8_t *frozen; /* [69] nullable */
+} phc_pd_map;
+
+typedef struct phc_replay_params {
+  float pos_sigma, force_scale;
+  uint64_t seed, counter;
+} phc_replay_params;
+
+/* HumanoidPHC.step with the physics stand-in in ONE launch (R13 + stand-in + R6,R7,R9-R12,R14):
+ * the same buffers and values as phc_actions_to_pd (pd nullable: skipped) -> phc_physics_replay ->
+ * phc_env_step, bit for bit; the replayed state IS the blended reference at the step's time, so its
+ * frame rows are gathered once and the sim record / dof velocities / forces never make an HBM round
+ * trip.  timer nullable (start/stop events of the launch, as phc_env_step_timed). */
+int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                        const phc_replay_params *replay, const phc_pd_map *pd, phc_kernel_timer *timer,
+                        void *stream);
+
 /* N3: articulated-body physics step, replacing `gym.simulate(sim)` x control_freq_inv
  * (puffer_phc/envs/humanoid_phc.py:129-134; sim params envs/isaacgym_env.py:6-42; PD drives
  * humanoid_phc.py:274-281; ground plane :255-262).  Featherstone ABA over the 24-body tree (6-DoF
@@ -211,6 +235,10 @@ int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const f
 /* the same launch with its start/stop events recorded into `timer` (bench.py); timer work += num_envs */
 int phc_physics_step_timed(const phc_env_buffers *env, const float *pd_target, const float *body_model,
                            const phc_physics_params *p, phc_kernel_timer *timer, void *stream);
+/* the same step with R13 folded in: PD targets computed in-kernel from pd->actions (and written to
+ * pd->pd_target), replacing phc_actions_to_pd + phc_physics_step (timer nullable) */
+int phc_physics_step_actions(const phc_env_buffers *env, const phc_pd_map *pd, const float *body_model,
+                             const phc_physics_params *p, phc_kernel_timer *timer, void *stream);
 
 /* R3-R5: load-time FK + velocities (poselib_skeleton.py:518-619, 1230-1251; motion_lib.py:119-140)
  * for `num_motions` clips packed back to back.  quat_global f64 [F,24,4], root_trans f64 [F,3],

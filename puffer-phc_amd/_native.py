@@ -66,6 +66,15 @@ class PhysicsParamsC(ctypes.Structure):
                 ("reserved", ctypes.c_float)]
 
 
+class PdMapC(ctypes.Structure):
+    _fields_ = [("actions", c_vp), ("pd_target", c_vp), ("offset", c_vp), ("scale", c_vp), ("frozen", c_vp)]
+
+
+class ReplayParamsC(ctypes.Structure):
+    _fields_ = [("pos_sigma", ctypes.c_float), ("force_scale", ctypes.c_float), ("seed", ctypes.c_uint64),
+                ("counter", ctypes.c_uint64)]
+
+
 class RowFieldC(ctypes.Structure):
     _fields_ = [("src", c_vp), ("dst", c_vp), ("row_elems", c_i64), ("kind", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
@@ -230,6 +239,11 @@ _EXPORTS = {
                                          c_vp]),
     "phc_physics_step_timed": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), c_vp, c_vp,
                                                ctypes.POINTER(PhysicsParamsC), c_vp, c_vp]),
+    "phc_physics_step_actions": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(PdMapC), c_vp,
+                                                 ctypes.POINTER(PhysicsParamsC), c_vp, c_vp]),
+    "phc_env_step_replay": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
+                                            ctypes.POINTER(StepParamsC), ctypes.POINTER(ReplayParamsC),
+                                            ctypes.POINTER(PdMapC), c_vp, c_vp]),
     "phc_fk_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_fk_motions": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
                                        ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -1022,6 +1036,35 @@ def physics_step(env_c, pd_target, body_model, params, timer=None):
         _check(lib().phc_physics_step_timed(*args, timer.handle, _stream()), "phc_physics_step")
     else:
         _check(lib().phc_physics_step(*args, _stream()), "phc_physics_step")
+
+
+def pd_map(actions, pd_out, offset, scale, frozen):
+    """phc_pd_map of R13 (the action -> PD-target map folded into its consumer kernel)."""
+    n = actions.shape[0]
+    return PdMapC(_ptr(actions, torch.float32, (n, NUM_DOF), "actions"),
+                  _ptr(pd_out, torch.float32, (n, NUM_DOF), "pd_target"),
+                  _ptr(offset, torch.float32, (NUM_DOF,), "offset"), _ptr(scale, torch.float32, (NUM_DOF,), "scale"),
+                  _ptr(_as_u8(frozen), torch.uint8, (NUM_DOF,), "frozen", nullable=True))
+
+
+def env_step_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter, pd=None, timer=None):
+    """phc_env_step_replay: R13 + the physics stand-in + the fused env step in one launch."""
+    rp = ReplayParamsC(float(pos_sigma), float(force_scale), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                       int(counter) & 0xFFFFFFFFFFFFFFFF)
+    if pd is not None and pd.actions and int(env_c.num_envs) <= 0:
+        raise ValueError("env_step_replay: empty env")
+    _check(lib().phc_env_step_replay(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(params), ctypes.byref(rp),
+                                     ctypes.byref(pd) if pd is not None else None,
+                                     timer.handle if timer is not None else None, _stream()),
+           "phc_env_step_replay")
+
+
+def physics_step_actions(env_c, pd, body_model, params, timer=None):
+    """N3 step with the PD targets computed in-kernel from the actions (phc_physics_step_actions)."""
+    _ptr(body_model, torch.float32, (NUM_BODIES, BODY_MODEL_STRIDE), "body_model")
+    _check(lib().phc_physics_step_actions(ctypes.byref(env_c), ctypes.byref(pd), body_model.data_ptr(),
+                                          ctypes.byref(params), timer.handle if timer is not None else None, _stream()),
+           "phc_physics_step_actions")
 
 
 def actions_to_pd(actions, pd_out, offset, scale, frozen):

@@ -113,6 +113,9 @@ class EnvConfig(DeviceConfig):
     physics_substeps: int = 8
     replay_pos_sigma: float = 0.02
     replay_force_scale: float = 50.0
+    # replay physics: the action -> PD map, the stand-in and the env step in one launch
+    # (phc_env_step_replay); False = three launches (same values)
+    fused_env_step: bool = True
     seed: int = 0
 
     robot: RobotConfig = field(default_factory=RobotConfig)

@@ -221,6 +221,15 @@ struct PhysView {
   float *dof_force;
 };
 
+// R13 folded in (phc_pd_map): with actions set, the PD targets are computed here from the actions
+// (clip, offset + scale a, frozen dofs 0) and written to pd_target; else pd_target is read
+struct PdArgs {
+  const float *actions;
+  float *pd;
+  const float *off, *scale;
+  const uint8_t *frozen;
+};
+
 // Per-block LDS: the body table with the derived constants (row stride 65 floats: lanes b = 0..23
 // reading the same field hit 24 distinct banks), per env the tree-pass slots (FK record 13 / inward
 // contribution 27 / acceleration 6 floats) and each body's outward-pass operands K = D^-1 A,
@@ -241,7 +250,7 @@ __device__ __forceinline__ M3 ld9(const float *p) {
 }
 
 __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_PHYS_WAVES_PER_SIMD, PHC_PHYS_WAVES_PER_SIMD))) void k_physics_step(
-    PhysView e, const float *__restrict__ model, const float *__restrict__ target, PhysConsts c) {
+    PhysView e, const float *__restrict__ model, const float *__restrict__ target, PdArgs pa, PhysConsts c) {
   __shared__ float tab[kBodies * kTab];
   __shared__ float slots[kPhysEnvs][kBodies][kSlot];
   __shared__ float outw[kPhysEnvs][kBodies][kOut];
@@ -311,8 +320,22 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     const float *d = e.dof_state + (ev * PHC_NUM_DOF + 3 * (b - 1)) * 2;
     r = quat_from_rotvec(v3{d[0], d[2], d[4]});
     om = {d[1], d[3], d[5]};
-    const float *t = target + ev * PHC_NUM_DOF + 3 * (b - 1);
-    tgt = {t[0], t[1], t[2]};
+    const int64_t i0 = ev * PHC_NUM_DOF + 3 * (b - 1);
+    if (pa.actions) {
+      float tv[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float x = pa.actions[i0 + k];
+        x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+        const int d = 3 * (b - 1) + k;
+        tv[k] = (pa.frozen && pa.frozen[d]) ? 0.0f : pa.off[d] + pa.scale[d] * x;
+        if (env < e.n) pa.pd[i0 + k] = tv[k];
+      }
+      tgt = {tv[0], tv[1], tv[2]};
+    } else {
+      const float *t = target + i0;
+      tgt = {t[0], t[1], t[2]};
+    }
   }
 
   q4 Q = {0.0f, 0.0f, 0.0f, 1.0f};
@@ -570,11 +593,13 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
 
 using namespace phc;
 
-extern "C" int phc_physics_step_timed(const phc_env_buffers *env, const float *pd_target, const float *body_model,
-                                      const phc_physics_params *p, phc_kernel_timer *timer, void *stream) {
+static int physics_launch(const phc_env_buffers *env, const float *pd_target, const phc_pd_map *pd,
+                          const float *body_model, const phc_physics_params *p, phc_kernel_timer *timer,
+                          void *stream) {
   PHC_REQUIRE(env && env->num_envs > 0, "physics_step: num_envs must be > 0");
   PHC_REQUIRE(env->rigid_body_state && env->dof_state && env->dof_force, "physics_step: null env buffer");
-  PHC_REQUIRE(pd_target && body_model && p, "physics_step: null target / model / params");
+  PHC_REQUIRE((pd_target || pd) && body_model && p, "physics_step: null target / model / params");
+  PHC_REQUIRE(!pd || (pd->actions && pd->pd_target && pd->offset && pd->scale), "physics_step: bad pd map");
   PHC_REQUIRE(p->sim_dt > 0.0f && p->control_freq_inv >= 1 && p->substeps >= 1 && p->substeps <= 1024 &&
                   p->control_freq_inv <= 64,
               "physics_step: bad time stepping (sim_dt %g, control_freq_inv %d, substeps %d)", (double)p->sim_dt,
@@ -604,9 +629,22 @@ extern "C" int phc_physics_step_timed(const phc_env_buffers *env, const float *p
     timer->used += 1;
     timer->work += (double)env->num_envs;  // env-steps
   }
+  const PdArgs pa{pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
+                  pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr};
   hipExtLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), ev0, ev1, 0, v,
-                        body_model, pd_target, c);
+                        body_model, pd_target, pa, c);
   return check_launch("physics_step");
+}
+
+extern "C" int phc_physics_step_timed(const phc_env_buffers *env, const float *pd_target, const float *body_model,
+                                      const phc_physics_params *p, phc_kernel_timer *timer, void *stream) {
+  return physics_launch(env, pd_target, nullptr, body_model, p, timer, stream);
+}
+
+extern "C" int phc_physics_step_actions(const phc_env_buffers *env, const phc_pd_map *pd, const float *body_model,
+                                        const phc_physics_params *p, phc_kernel_timer *timer, void *stream) {
+  PHC_REQUIRE(pd, "physics_step_actions: null pd map");
+  return physics_launch(env, nullptr, pd, body_model, p, timer, stream);
 }
 
 extern "C" int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const float *body_model,

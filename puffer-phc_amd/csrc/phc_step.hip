@@ -206,6 +206,96 @@ __global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, Ste
   }
 }
 
+// --------------------------------------------------------- physics stand-in --
+// Triangular noise with standard deviation `sd` from 16 random bits pairs (cheap integer RNG).
+__device__ __forceinline__ float tri_noise(unsigned long long h, int k, float sd) {
+  const unsigned a = (unsigned)(h >> (32 * (k & 1))) & 0xFFFFu;
+  const unsigned b = (unsigned)(h >> (32 * (k & 1) + 16)) & 0xFFFFu;
+  return ((float)a - (float)b) * (sd * 2.4494897f / 65536.0f);
+}
+
+struct ReplayArgs {
+  float sigma, force_scale;
+  unsigned long long seed, counter;
+  // R13 folded in: the action -> PD-target map (actions nullable: no PD targets written)
+  const float *actions;
+  float *pd;
+  const float *off, *scale;
+  const uint8_t *frozen;
+};
+
+// The replayed sim state of one (env, body): the reference record at the env's next control time
+// (`s` = that blend, offset applied) plus noise keyed by (seed, counter, env, body) and, when the env
+// has RNG counters, by the env's episode (rng_counter) and step (progress): no per-step host value,
+// so a captured graph replays fresh noise every step.  Body b >= 1 also gets its dof velocities
+// (reference + noise) and forces (noise), returned in dv / f.
+__device__ __forceinline__ void replay_perturb(const EnvView &e, const ReplayArgs &r, int64_t env, int b, int prog,
+                                               BodyRec &s, const LibView &l, const Blend &bl, v3 &dv, v3 &f) {
+  const float sigma = r.sigma;
+  unsigned long long key = r.seed ^ mix64(r.counter);
+  if (e.rng) key ^= mix64(((unsigned long long)e.rng[env] << 20) ^ (unsigned long long)(unsigned)prog ^ 0x5bd1e995ull);
+  const unsigned long long base = mix64(key ^ ((unsigned long long)(env * kBodies + b) << 8));
+  unsigned long long h = mix64(base + 1);
+  s.p.x += tri_noise(h, 0, sigma);
+  s.p.y += tri_noise(h, 1, sigma);
+  h = mix64(base + 2);
+  s.p.z += tri_noise(h, 0, sigma);
+  q4 q = {s.r.x + tri_noise(h, 1, sigma), s.r.y, s.r.z, s.r.w};
+  h = mix64(base + 3);
+  q.y += tri_noise(h, 0, sigma);
+  q.z += tri_noise(h, 1, sigma);
+  s.r = quat_unit(q);
+  h = mix64(base + 4);
+  s.v.x += tri_noise(h, 0, 10.0f * sigma);
+  s.v.y += tri_noise(h, 1, 10.0f * sigma);
+  h = mix64(base + 5);
+  s.v.z += tri_noise(h, 0, 10.0f * sigma);
+  s.av.x += tri_noise(h, 1, 20.0f * sigma);
+  h = mix64(base + 6);
+  s.av.y += tri_noise(h, 0, 20.0f * sigma);
+  s.av.z += tri_noise(h, 1, 20.0f * sigma);
+  dv = {0.0f, 0.0f, 0.0f};
+  f = {0.0f, 0.0f, 0.0f};
+  if (b >= 1) {
+    dv = ref_dof_vel(l.dof_vel, bl, b);
+    h = mix64(base + 7);
+    dv.x = dv.x + tri_noise(h, 0, 10.0f * sigma);
+    dv.y = dv.y + tri_noise(h, 1, 10.0f * sigma);
+    h = mix64(base + 8);
+    dv.z = dv.z + tri_noise(h, 0, 10.0f * sigma);
+    f.x = tri_noise(h, 1, r.force_scale);
+    h = mix64(base + 9);
+    f.y = tri_noise(h, 0, r.force_scale);
+    f.z = tri_noise(h, 1, r.force_scale);
+  }
+}
+
+__device__ __forceinline__ void store_replay(const EnvView &e, int64_t env, int b, const BodyRec &s, v3 dv, v3 f) {
+  store_body(e.rb + (env * kBodies + b) * kRec, s);
+  if (b >= 1) {
+    float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+    d[1] = dv.x; d[3] = dv.y; d[5] = dv.z;
+    float *fo = const_cast<float *>(e.dof_force) + env * PHC_NUM_DOF + 3 * (b - 1);
+    fo[0] = f.x; fo[1] = f.y; fo[2] = f.z;
+  }
+}
+
+// R13 (clean_pufferl/env.py:91-93, humanoid_phc.py:1216-1226): clip(a, -1, 1), pd = offset +
+// scale a, frozen dofs 0
+__device__ __forceinline__ float action_to_pd(float x, int d, const float *__restrict__ off,
+                                              const float *__restrict__ scale, const uint8_t *__restrict__ frozen) {
+  x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+  return (frozen && frozen[d]) ? 0.0f : off[d] + scale[d] * x;
+}
+
+// the 3 PD targets of body b >= 1 (dofs 3(b-1) .. 3(b-1)+2)
+__device__ __forceinline__ void map_actions(const ReplayArgs &r, int64_t env, int b) {
+  if (!r.actions || b < 1) return;
+  const int64_t i0 = env * PHC_NUM_DOF + 3 * (b - 1);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) r.pd[i0 + k] = action_to_pd(r.actions[i0 + k], 3 * (b - 1) + k, r.off, r.scale, r.frozen);
+}
+
 // --------------------------------------------------------------- env step --
 // Post-physics part of HumanoidPHC.step (humanoid_phc.py:136-146):
 //   progress += 1; reward with the reference at t (:1228-1303); reset at t (:1311-1333);
@@ -220,9 +310,10 @@ struct Outcome {
 
 // reward (common.py:271-322 + power :1295-1303) and reset (common.py:326-364) of one env from
 // its half-wave; every lane returns the env's totals
+// pw_reg >= 0: this lane's power term already in registers (the fused replay step), else read
 __device__ __forceinline__ Outcome env_reward(const EnvView &e, const StepConsts &c, int64_t ei, int lane, int prog,
                                               float t, const MotionScalars &m, const BodyRec &s,
-                                              const BodyRec &ref0) {
+                                              const BodyRec &ref0, float pw_reg = -1.0f) {
   const bool active = lane < kBodies;
   const int b = active ? lane : 0;
   const v3 dp = vsub(ref0.p, s.p);
@@ -247,7 +338,9 @@ __device__ __forceinline__ Outcome env_reward(const EnvView &e, const StepConsts
   float dsum = counted ? dist : 0.0f;
   // power: lane j < 23 owns dofs 3j..3j+2
   float pw = 0.0f;
-  if (lane < kBodies - 1) {
+  if (pw_reg >= 0.0f) {
+    pw = pw_reg;
+  } else if (lane < kBodies - 1) {
     const float *f = e.dof_force + ei * PHC_NUM_DOF + 3 * lane;
     const float *ds = e.dof_state + (ei * PHC_NUM_DOF + 3 * lane) * 2;
     pw = fabsf(f[0] * ds[1]);
@@ -325,8 +418,12 @@ __device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10]) 
 }
 
 // Half-wave per env, 8 envs per workgroup: the throughput form (large env counts).
-template <bool AUTO>
-__global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, StepConsts c) {
+// REPLAY: HumanoidPHC.step with the physics stand-in in ONE launch — the action -> PD map (R13),
+// the replayed sim state (k_physics_replay: the reference at t plus noise, which is exactly ref0
+// below plus noise, so its frame rows are gathered once) and the post-physics step; the same
+// values as k_actions_to_pd -> k_physics_replay -> k_env_step bit for bit.
+template <bool AUTO, bool REPLAY>
+__global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
   const int g = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + g;
@@ -351,12 +448,31 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   Blend bl1 = frame_blend(t1n, m);
 
   // one memory round for the sim record and all four reference rows (t and t+dt)
-  BodyRec s = load_body(e.rb + (ei * kBodies + b) * kRec);
+  BodyRec s;
+  if (!REPLAY) s = load_body(e.rb + (ei * kBodies + b) * kRec);
   const RowPair rows0 = load_rows(l.frames, bl0, b);
   RowPair rows1 = load_rows(l.frames, bl1, b);
   const BodyRec ref0 = blend_body(rows0.a, rows0.c, bl0.b, &go);
 
-  const Outcome o = env_reward(e, c, ei, lane, prog, t, m, s, ref0);
+  float pw_reg = -1.0f;
+  if (REPLAY) {
+    v3 dv, f;
+    s = ref0;
+    replay_perturb(e, r, ei, b, prog, s, l, bl0, dv, f);
+    if (valid && lane < kBodies) {
+      store_replay(e, ei, b, s, dv, f);
+      map_actions(r, ei, b);
+    }
+    // power: k_env_step's lane j sums the |force x dof vel| of dofs 3j..3j+2, i.e. body j+1's
+    float mine = fabsf(f.x * dv.x);
+    mine = mine + fabsf(f.y * dv.y);
+    mine = mine + fabsf(f.z * dv.z);
+    if (lane >= kBodies) mine = 0.0f;
+    pw_reg = __shfl_down(mine, 1, kGroup);
+    if (lane >= kBodies - 1) pw_reg = 0.0f;
+  }
+
+  const Outcome o = env_reward(e, c, ei, lane, prog, t, m, s, ref0, pw_reg);
   double st_row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (valid && lane == 0) env_bookkeeping(e, ei, o, st_row);
 
@@ -396,17 +512,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   }
 }
 
-// --------------------------------------------------------- physics stand-in --
-// Triangular noise with standard deviation `sd` from 16 random bits pairs (cheap integer RNG).
-__device__ __forceinline__ float tri_noise(unsigned long long h, int k, float sd) {
-  const unsigned a = (unsigned)(h >> (32 * (k & 1))) & 0xFFFFu;
-  const unsigned b = (unsigned)(h >> (32 * (k & 1) + 16)) & 0xFFFFu;
-  return ((float)a - (float)b) * (sd * 2.4494897f / 65536.0f);
-}
-
-__global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l, StepConsts c, float sigma,
-                                                           float force_scale, unsigned long long seed,
-                                                           unsigned long long counter) {
+__global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
   const int64_t env = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / kGroup;
   const int lane = threadIdx.x % kGroup;
   if (env >= e.n || lane >= kBodies) return;
@@ -417,46 +523,9 @@ __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l,
   const Blend bl = frame_blend(t, m);
   const v3 go = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
   BodyRec s = ref_body(l.frames, bl, b, &go);
-  // noise keyed by (seed, counter, env, body) and, when the env has RNG counters, by the env's
-  // episode (rng_counter) and step (progress): no per-step host value, so a captured graph replays
-  // fresh noise every step
-  unsigned long long key = seed ^ mix64(counter);
-  if (e.rng) key ^= mix64(((unsigned long long)e.rng[env] << 20) ^ (unsigned long long)(unsigned)prog ^ 0x5bd1e995ull);
-  const unsigned long long base = mix64(key ^ ((unsigned long long)(env * kBodies + b) << 8));
-  unsigned long long h = mix64(base + 1);
-  s.p.x += tri_noise(h, 0, sigma);
-  s.p.y += tri_noise(h, 1, sigma);
-  h = mix64(base + 2);
-  s.p.z += tri_noise(h, 0, sigma);
-  q4 r = {s.r.x + tri_noise(h, 1, sigma), s.r.y, s.r.z, s.r.w};
-  h = mix64(base + 3);
-  r.y += tri_noise(h, 0, sigma);
-  r.z += tri_noise(h, 1, sigma);
-  s.r = quat_unit(r);
-  h = mix64(base + 4);
-  s.v.x += tri_noise(h, 0, 10.0f * sigma);
-  s.v.y += tri_noise(h, 1, 10.0f * sigma);
-  h = mix64(base + 5);
-  s.v.z += tri_noise(h, 0, 10.0f * sigma);
-  s.av.x += tri_noise(h, 1, 20.0f * sigma);
-  h = mix64(base + 6);
-  s.av.y += tri_noise(h, 0, 20.0f * sigma);
-  s.av.z += tri_noise(h, 1, 20.0f * sigma);
-  store_body(e.rb + (env * kBodies + b) * kRec, s);
-  if (b >= 1) {
-    const v3 dv = ref_dof_vel(l.dof_vel, bl, b);
-    float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
-    h = mix64(base + 7);
-    d[1] = dv.x + tri_noise(h, 0, 10.0f * sigma);
-    d[3] = dv.y + tri_noise(h, 1, 10.0f * sigma);
-    h = mix64(base + 8);
-    d[5] = dv.z + tri_noise(h, 0, 10.0f * sigma);
-    float *f = const_cast<float *>(e.dof_force) + env * PHC_NUM_DOF + 3 * (b - 1);
-    f[0] = tri_noise(h, 1, force_scale);
-    h = mix64(base + 9);
-    f[1] = tri_noise(h, 0, force_scale);
-    f[2] = tri_noise(h, 1, force_scale);
-  }
+  v3 dv, f;
+  replay_perturb(e, r, env, b, prog, s, l, bl, dv, f);
+  store_replay(e, env, b, s, dv, f);
 }
 
 // --------------------------------------------------------------- actions --
@@ -466,10 +535,7 @@ __global__ __launch_bounds__(kBlock) void k_actions_to_pd(const float *__restric
                                                           const uint8_t *__restrict__ frozen) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= total) return;
-  const int d = (int)(i % PHC_NUM_DOF);
-  float x = a[i];
-  x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
-  pd[i] = (frozen && frozen[d]) ? 0.0f : off[d] + scale[d] * x;
+  pd[i] = action_to_pd(a[i], (int)(i % PHC_NUM_DOF), off, scale, frozen);
 }
 
 static int grid_envs(int64_t n) { return (int)((n + kEnvsPerBlock - 1) / kEnvsPerBlock); }
@@ -575,14 +641,47 @@ extern "C" int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_l
   const EnvView ev = env_view(env);
   const LibView lv = lib_view(lib);
   const StepConsts cs = make_consts(p);
+  const ReplayArgs none{};
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot && lib->dof_vel, "env_step: auto_reset needs local_rot and dof_vel");
     PHC_REQUIRE(env->rng_counter, "env_step: auto_reset needs rng_counter");
-    hipExtLaunchKernelGGL(k_env_step<true>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs);
+    hipExtLaunchKernelGGL(k_env_step<true, false>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs, none);
   } else {
-    hipExtLaunchKernelGGL(k_env_step<false>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs);
+    hipExtLaunchKernelGGL(k_env_step<false, false>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs, none);
   }
   return check_launch("env_step");
+}
+
+extern "C" int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
+                                   const phc_replay_params *rp, const phc_pd_map *pd, phc_kernel_timer *timer,
+                                   void *stream) {
+  if (int rc = check_env(env)) return rc;
+  if (int rc = check_lib(lib)) return rc;
+  PHC_REQUIRE(p && p->dt > 0.0f && rp, "env_step_replay: bad params");
+  PHC_REQUIRE(lib->dof_vel, "env_step_replay: motion lib needs dof_vel");
+  PHC_REQUIRE(!pd || (pd->actions && pd->pd_target && pd->offset && pd->scale), "env_step_replay: bad pd map");
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (timer && timer->used < (int32_t)timer->start.size()) {
+    ev0 = timer->start[timer->used];
+    ev1 = timer->stop[timer->used];
+    timer->used += 1;
+  }
+  ReplayArgs ra{rp->pos_sigma, rp->force_scale, (unsigned long long)rp->seed, (unsigned long long)rp->counter,
+                pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
+                pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr};
+  const dim3 block(kBlock), grid(grid_envs(env->num_envs));
+  hipStream_t st = as_stream(stream);
+  const EnvView ev = env_view(env);
+  const LibView lv = lib_view(lib);
+  const StepConsts cs = make_consts(p);
+  if (p->auto_reset) {
+    PHC_REQUIRE(lib->local_rot, "env_step_replay: auto_reset needs local_rot");
+    PHC_REQUIRE(env->rng_counter, "env_step_replay: auto_reset needs rng_counter");
+    hipExtLaunchKernelGGL(k_env_step<true, true>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs, ra);
+  } else {
+    hipExtLaunchKernelGGL(k_env_step<false, true>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs, ra);
+  }
+  return check_launch("env_step_replay");
 }
 
 extern "C" int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
@@ -610,9 +709,10 @@ extern "C" int phc_physics_replay(const phc_env_buffers *env, const phc_motion_l
   if (int rc = check_lib(lib)) return rc;
   PHC_REQUIRE(lib->dof_vel, "physics_replay: motion lib needs dof_vel");
   PHC_REQUIRE(p, "physics_replay: bad params");
+  ReplayArgs ra{pos_sigma, force_scale, (unsigned long long)seed, (unsigned long long)counter,
+                nullptr, nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(k_physics_replay, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
-                     env_view(env), lib_view(lib), make_consts(p), pos_sigma, force_scale,
-                     (unsigned long long)seed, (unsigned long long)counter);
+                     env_view(env), lib_view(lib), make_consts(p), ra);
   return check_launch("physics_replay");
 }
 

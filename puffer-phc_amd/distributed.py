@@ -61,7 +61,10 @@ class FlatGrads:
     being computed."""
 
     def __init__(self, params, bucket_bytes=32 << 20, order=None):
-        params = [p for p in params if p.requires_grad]
+        # the module's own parameter order (requires_grad or not): the index space of a
+        # torch.optim.Adam(module.parameters()) state dict (optim.FlatAdam.state_dict)
+        self.module_params = list(params)
+        params = [p for p in self.module_params if p.requires_grad]
         if order is not None:
             first = [p for p in order if p.requires_grad]
             ids = {id(p) for p in first}

@@ -1,11 +1,11 @@
 """HumanoidPHC drop-in (puffer_phc/envs/humanoid_phc.py:46-1454) on the HIP hot path.
 
 Per step (HumanoidPHC.step, :105-172) the env launches, on the current HIP stream:
-  phc_actions_to_pd  (R13)  action -> PD target
-  physics            `ReplayPhysics` (BASELINE configs[1], "physics stubbed with replayed rigid-body
-                     states"; the default) or `physics.ArticulatedPhysics` (N3, cfg.physics =
-                     "articulated": phc_physics_step, the articulated-body PD step); both write the
-                     same buffers
+  with `ReplayPhysics` (BASELINE configs[1], "physics stubbed with replayed rigid-body states"; the
+  default): ONE launch, phc_env_step_replay = the action -> PD map (R13) + the stand-in + the
+  post-physics step below (cfg.fused_env_step = False: the three separate launches);
+  with `physics.ArticulatedPhysics` (N3, cfg.physics = "articulated"):
+  phc_physics_step_actions  the articulated-body PD step with R13 folded in, then
   phc_env_step       (R6,R7,R9-R12,R14) progress, reward(t), reset(t), obs(t+dt) and the
                      PufferEnv bookkeeping, fused in one kernel
 and `reset_done()` / `reset(env_ids)` (R15) re-initialises terminated envs from the motion
@@ -58,6 +58,14 @@ class ReplayPhysics:
         _native.physics_replay(env._env_c, env._motion_lib.packed.c, env._step_params, self.pos_sigma,
                                self.force_scale, self.seed, self.counter)
 
+    def step_fused(self, env, params, pd, timer=None):
+        """The stand-in, the action -> PD map and the post-physics env step in one launch
+        (phc_env_step_replay): the replayed state is the reference blend the env step reads
+        anyway, so it never makes an HBM round trip."""
+        self.counter += 1
+        _native.env_step_replay(env._env_c, env._motion_lib.packed.c, params, self.pos_sigma, self.force_scale,
+                                self.seed, self.counter, pd=pd, timer=timer)
+
 
 class HumanoidPHC:
     def __init__(self, cfg: EnvConfig, motion_data=None, physics=None):
@@ -84,6 +92,8 @@ class HumanoidPHC:
         self._rng_seed = int(cfg.seed) * 7919 + 17
         self._rng_counter = 0
         self.kernel_timer = None  # bench: _native.KernelTimer timing every phc_env_step launch
+        # the replay stand-in + R13 fused into the env step launch (False: the three launches)
+        self.fused_env_step = bool(getattr(cfg, "fused_env_step", True))
         self._load_motion(cfg.motion_file if motion_data is None else motion_data)
 
     # ------------------------------------------------------------ setup --
@@ -277,13 +287,22 @@ class HumanoidPHC:
         fused kernel, as PHCPufferEnv.step's env.reset(reset_indices) does next."""
         if actions.dtype != torch.float32 or not actions.is_contiguous():
             actions = actions.float().contiguous()
-        _native.actions_to_pd(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale, self._pd_frozen)
-        self.physics.step(self)
         # eval mode records MPJPE / positions of the step's own outcome before the envs reset
         # (the reference resets after HumanoidPHC.step returns): no in-launch reset there
         fused_reset = auto_reset and not self.flag_im_eval
         params = self._step_params_auto if fused_reset else self._step_params
-        _native.env_step(self._env_c, self._motion_lib.packed.c, params, timer=self.kernel_timer)
+        pd = _native.pd_map(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale, self._pd_frozen)
+        if self.fused_env_step and hasattr(self.physics, "step_fused"):
+            # R13 + the physics stand-in + the env step: one launch
+            self.physics.step_fused(self, params, pd, timer=self.kernel_timer)
+        else:
+            if hasattr(self.physics, "step_actions"):  # R13 folded into the physics launch
+                self.physics.step_actions(self, pd)
+            else:
+                _native.actions_to_pd(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale,
+                                      self._pd_frozen)
+                self.physics.step(self)
+            _native.env_step(self._env_c, self._motion_lib.packed.c, params, timer=self.kernel_timer)
         if fused_reset and "terminals" in self._puffer:
             self.extras["terminate"] = self._puffer["terminals"]  # this step's outcome, written by the kernel
         else:

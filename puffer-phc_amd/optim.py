@@ -76,33 +76,55 @@ class FlatAdam(torch.optim.Adam):
             st["step"] = self._i[2:3].view(())  # int32 device step counter shared by all slices
 
     def state_dict(self):
+        """torch.optim.Adam's state dict as the REFERENCE's optimizer would write it
+        (clean_pufferl/utils.py:18-42 saves torch.optim.Adam(policy.parameters()).state_dict()):
+        parameter indices in the module's parameter order (frozen ones, e.g. sigma, included and
+        without state), per-parameter exp_avg / exp_avg_sq / step.  The loss-scaler state rides
+        in an extra "flat_adam" entry that torch's load_state_dict ignores."""
         sd = super().state_dict()
-        step = float(self._i[2])
-        for st in sd["state"].values():
-            st["step"] = torch.tensor(step)
-            st["exp_avg"] = st["exp_avg"].clone()
-            st["exp_avg_sq"] = st["exp_avg_sq"].clone()
-        sd["flat_adam"] = {"loss_scale": float(self._f[0]), "growth_tracker": int(self._i[1]),
-                           "skipped": int(self._i[3])}
-        return sd
+        order = self.flat_grads.module_params
+        views = {id(p): v for p, v in zip(self.flat_grads.params, self._views)}
+        step = torch.tensor(float(self._i[2]))
+        state = {}
+        for i, p in enumerate(order):
+            if id(p) in views:
+                off, k = views[id(p)]
+                state[i] = {"step": step.clone(), "exp_avg": self.exp_avg[off:off + k].view_as(p).clone(),
+                            "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p).clone()}
+        group = {k: v for k, v in sd["param_groups"][0].items() if k != "params"}
+        group["params"] = list(range(len(order)))
+        return {"state": state, "param_groups": [group],
+                "flat_adam": {"loss_scale": float(self._f[0]), "growth_tracker": int(self._i[1]),
+                              "skipped": int(self._i[3])}}
 
     def load_state_dict(self, state_dict):
+        """Loads a state dict in the module-parameter index space (what state_dict writes and what
+        a torch.optim.Adam(policy.parameters()) checkpoint holds)."""
         extra = state_dict.get("flat_adam")
-        sd = {k: v for k, v in state_dict.items() if k != "flat_adam"}
-        super().load_state_dict(sd)
+        order = self.flat_grads.module_params
+        groups = state_dict["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(order):
+            raise ValueError(f"optimizer state dict has {sum(len(g['params']) for g in groups)} parameters in "
+                             f"{len(groups)} groups; this policy has {len(order)} in one")
+        views = {id(p): v for p, v in zip(self.flat_grads.params, self._views)}
         step = 0
         with torch.no_grad():
-            for p, (off, k) in zip(self.flat_grads.params, self._views):
-                st = self.state[p]
-                if "exp_avg" in st:
-                    self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
-                    self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
-                    step = int(float(st["step"]))
+            for i, p in zip(groups[0]["params"], order):
+                st = state_dict["state"].get(i)
+                if st is None or id(p) not in views:
+                    continue
+                off, k = views[id(p)]
+                self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                step = int(float(st["step"]))
             self._i[2] = step
             if extra:
                 self._f[0] = extra["loss_scale"]
                 self._i[1] = extra["growth_tracker"]
                 self._i[3] = extra["skipped"]
+        for k, v in groups[0].items():
+            if k != "params":
+                self.param_groups[0][k] = v
         self._bind_state()
         weight_cache.bump()
 

@@ -144,4 +144,9 @@ class ArticulatedPhysics:
                                       float(c.gravity), 0.0)
 
     def step(self, env):
+        """One step from env.pd_target (written by the caller)."""
         _native.physics_step(env._env_c, env.pd_target, self.model.table, self.params, timer=self.timer)
+
+    def step_actions(self, env, pd):
+        """One step with the action -> PD-target map (R13) folded into the physics launch."""
+        _native.physics_step_actions(env._env_c, pd, self.model.table, self.params, timer=self.timer)

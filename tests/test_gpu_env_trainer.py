@@ -210,3 +210,42 @@ def test_graph_rollout_matches_eager_loop(use_amp):
     if use_amp:
         assert torch.equal(a["amp"], b["amp"])
     assert torch.isfinite(b["logp"]).all()
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_fused_replay_step_equals_three_launches(amp):
+    """phc_env_step_replay (R13 + the physics stand-in + the env step in one launch) against
+    phc_actions_to_pd -> phc_physics_replay -> phc_env_step on identical envs: every buffer bit for
+    bit over 30 PufferEnv steps with auto-resets (short clips) and random actions beyond [-1, 1]."""
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    envs = []
+    for fused in (False, True):
+        q, t, c, fps = synthetic_clips(37, 12, 50, seed=4, device=DEV)
+        env = PHCPufferEnv(EnvConfig(num_envs=301, seed=6, use_amp_obs=amp, fused_env_step=fused),
+                           motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
+        env.reset()
+        envs.append(env)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    resets = 0
+    for step in range(30):
+        act = torch.randn((301, 69), device=DEV, generator=g) * 1.5
+        outs = [env.step(act) for env in envs]
+        a, b = envs
+        ea, eb = a.env, b.env
+        for name in ("_rigid_body_state", "_dof_state", "dof_force_tensor", "pd_target", "obs_buf", "rew_buf",
+                     "reward_raw", "progress_buf", "reset_buf", "_terminate_buf", "_motion_start_times"):
+            assert torch.equal(getattr(ea, name), getattr(eb, name)), (step, name)
+        for name in ("terminals", "truncations", "masks"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), (step, name)
+        if amp:
+            assert torch.equal(ea._amp_obs_buf, eb._amp_obs_buf), step
+        resets += int(a.terminals.sum() + a.truncations.sum())
+        assert torch.equal(outs[0][1], outs[1][1])
+    assert resets > 0
+    # the PD targets follow the reference's map (clip, scale, frozen hands / toes)
+    ref = O.actions_to_pd(act.cpu().numpy())
+    np.testing.assert_array_equal(envs[1].env.pd_target.cpu().numpy(), ref)

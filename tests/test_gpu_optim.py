@@ -149,3 +149,63 @@ def test_reduce_into_many_parts(parts, accumulate):
     torch.cuda.synchronize()
     for (_, dst), ref in zip(jobs, refs):
         torch.testing.assert_close(dst.double(), ref, rtol=1e-6, atol=1e-5)
+
+
+def test_checkpoint_optimizer_state_loads_into_torch_adam(tmp_path):
+    """trainer_state.pt's optimizer_state_dict is in the reference's layout
+    (clean_pufferl/utils.py:18-42: torch.optim.Adam(policy.parameters()).state_dict()): a plain
+    torch.optim.Adam over a copy of the policy loads it and takes the same next step as FlatAdam
+    (state indices follow policy.parameters(), frozen sigma included; FlatAdam's flat buffer is
+    laid out in backward-ready order instead)."""
+    import copy
+
+    import numpy as np
+
+    from puffer_phc_amd.clean_pufferl.utils import save_checkpoint
+    from puffer_phc_amd.config import TrainConfig
+    from puffer_phc_amd.distributed import FlatGrads
+    from puffer_phc_amd.envs.humanoid_phc import Box
+    from puffer_phc_amd.optim import FlatAdam
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+
+    class E:
+        single_observation_space = Box(np.full(934, -np.inf), np.full(934, np.inf))
+        single_action_space = Box(-np.ones(69), np.ones(69))
+        amp_observation_space = None
+
+    torch.manual_seed(0)
+    policy = Policy(PHCPolicy(E(), hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+    fg = FlatGrads(policy.parameters(), order=policy.policy.grad_ready_order())
+    opt = FlatAdam(fg, lr=3e-4, eps=1e-5)
+    assert fg.params[0] is not list(policy.parameters())[0]  # the flat layout is NOT module order
+    g = torch.Generator(device=DEV).manual_seed(1)
+    for _ in range(3):
+        fg.flat.copy_(torch.randn(fg.flat.shape, device=DEV, generator=g))
+        opt.step()
+    cfg = TrainConfig(data_dir=str(tmp_path))
+    save_checkpoint(policy, opt, cfg, "ck", 3, 123)
+    st = torch.load(tmp_path / "ck" / "trainer_state.pt", weights_only=True)
+    sd = st["optimizer_state_dict"]
+    names = [n for n, _ in policy.named_parameters()]
+    assert sd["param_groups"][0]["params"] == list(range(len(names)))
+    frozen = [i for i, p in enumerate(policy.parameters()) if not p.requires_grad]
+    assert frozen and all(i not in sd["state"] for i in frozen)  # sigma: no state, as torch's Adam
+    twin = copy.deepcopy(policy)
+    ref = torch.optim.Adam(twin.parameters(), lr=3e-4, eps=1e-5)
+    ref.load_state_dict(sd)
+    grads = torch.randn(fg.flat.shape, device=DEV, generator=g)
+    fg.flat.copy_(grads)
+    for p, q in zip(policy.parameters(), twin.parameters()):
+        if p.requires_grad:
+            q.grad = p.grad.detach().clone()
+    opt.step()
+    ref.step()
+    for (n, p), q in zip(policy.named_parameters(), twin.parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=2e-6, atol=1e-8, msg=n)
+    # and back: FlatAdam loads torch's own state dict
+    fg2 = FlatGrads(twin.parameters(), order=twin.policy.grad_ready_order())
+    opt2 = FlatAdam(fg2, lr=3e-4, eps=1e-5)
+    opt2.load_state_dict(ref.state_dict())
+    assert int(opt2._i[2]) == 4
+    torch.testing.assert_close(opt2.exp_avg_sq[fg2._range[id(fg2.params[0])][0]:][:5],
+                               ref.state[fg2.params[0]]["exp_avg_sq"].reshape(-1)[:5])

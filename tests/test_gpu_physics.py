@@ -208,3 +208,37 @@ def test_ppo_iteration_with_articulated_physics():
     losses = clean_pufferl.train(comps, info, util)
     assert np.isfinite([losses.policy_loss, losses.value_loss, losses.approx_kl]).all()
     assert sum(not torch.equal(before[k], v) for k, v in policy.named_parameters() if v.requires_grad) > 0
+
+
+def test_physics_step_actions_equals_separate_pd_launch(device_model):
+    """phc_physics_step_actions (R13 folded into the physics launch) == phc_actions_to_pd +
+    phc_physics_step, bit for bit, including the PD-target buffer it writes."""
+    import torch
+
+    from puffer_phc_amd import _native
+    from puffer_phc_amd.physics import ArticulatedPhysics, rest_state
+
+    phys = ArticulatedPhysics(model=device_model)
+    n = 67
+    g = torch.Generator(device="cuda").manual_seed(2)
+    act = torch.randn((n, 69), device="cuda", generator=g) * 1.3
+    off = torch.zeros(69, device="cuda")
+    scale = torch.full((69,), 3.1415927, device="cuda")
+    frozen = torch.zeros(69, dtype=torch.uint8, device="cuda")
+    frozen[30:33] = 1
+    outs = []
+    for fused in (False, True):
+        rb, dof = rest_state(device_model, n, 0.02)
+        force = torch.zeros((n, 69), device="cuda")
+        pd = torch.full((n, 69), float("nan"), device="cuda")
+        env_c = _native.physics_env_struct(rb, dof, force)
+        if fused:
+            phys_pd = _native.pd_map(act, pd, off, scale, frozen)
+            _native.physics_step_actions(env_c, phys_pd, device_model.table, phys.params)
+        else:
+            _native.actions_to_pd(act, pd, off, scale, frozen)
+            _native.physics_step(env_c, pd, device_model.table, phys.params)
+        torch.cuda.synchronize()
+        outs.append((rb, dof, force, pd))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
