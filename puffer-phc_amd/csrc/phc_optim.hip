@@ -311,6 +311,28 @@ __device__ __forceinline__ void pack_store(void *base, int64_t idx, int32_t dt, 
   else static_cast<float *>(base)[idx] = v;
 }
 
+// 4 consecutive values at element idx (8-B aligned for half types, 16-B for fp32), or one by one
+__device__ __forceinline__ void pack_store4(void *base, int64_t idx, int32_t dt, const float v[4], bool vec) {
+  if (vec && dt == PHC_DT_F16) {
+    _Float16 h[4] = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+    uint2 raw;
+    __builtin_memcpy(&raw, h, sizeof(raw));
+    *reinterpret_cast<uint2 *>(static_cast<_Float16 *>(base) + idx) = raw;
+  } else if (vec && dt == PHC_DT_BF16) {
+    __bf16 h[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    uint2 raw;
+    __builtin_memcpy(&raw, h, sizeof(raw));
+    *reinterpret_cast<uint2 *>(static_cast<__bf16 *>(base) + idx) = raw;
+  } else if (vec) {
+    *reinterpret_cast<float4 *>(static_cast<float *>(base) + idx) = float4{v[0], v[1], v[2], v[3]};
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pack_store(base, idx + q, dt, v[q]);
+  }
+}
+
+// 64 x 64 tile per block: thread t owns columns 4 (t % 16) .. +3 of rows t / 16 + 16 i (16-B source
+// loads, 8-B half stores), and for the transpose 4 consecutive tile rows of one column
 __global__ __launch_bounds__(kPackThreads) void k_pack_weights(PackJobs js) {
   __shared__ float tile[kPackTile][kPackTile + 1];
   int q = 0;
@@ -318,19 +340,53 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_weights(PackJobs js) {
   const phc_pack_job &job = js.j[q];
   const int64_t t = (int64_t)blockIdx.x - js.first_block[q];
   const int64_t r0 = (t / js.tiles_c[q]) * kPackTile, c0 = (t % js.tiles_c[q]) * kPackTile;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int rr = wv; rr < kPackTile; rr += kPackThreads / 64) {
-    const int64_t r = r0 + rr, c = c0 + lane;
-    const bool in = r < job.rows && c < job.cols;
-    const float v = in ? job.src[r * job.src_ld + c] : 0.0f;
-    tile[rr][lane] = v;
-    if (in && job.dst) pack_store(job.dst, r * job.dst_ld + c, job.dtype, v);
+  const int cq = (threadIdx.x & 15) * 4, rq = threadIdx.x >> 4;
+  const int esz = job.dtype == PHC_DT_F32 ? 4 : 2;
+  const bool src_vec = (job.src_ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(job.src) & 15) == 0);
+  const bool dst_vec = job.dst && ((job.dst_ld * esz) % (4 * esz) == 0) &&
+                       ((reinterpret_cast<uintptr_t>(job.dst) & (4 * esz - 1)) == 0);
+#pragma unroll
+  for (int i = 0; i < kPackTile / 16; ++i) {
+    const int rr = rq + 16 * i;
+    const int64_t r = r0 + rr, c = c0 + cq;
+    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const bool row_in = r < job.rows;
+    const bool full = row_in && c + 3 < job.cols;
+    if (full && src_vec) {
+      const float4 x = *reinterpret_cast<const float4 *>(job.src + r * job.src_ld + c);
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    } else if (row_in) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < job.cols) v[k] = job.src[r * job.src_ld + c + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tile[rr][cq + k] = v[k];
+    if (job.dst && row_in) {
+      if (full) {
+        pack_store4(job.dst, r * job.dst_ld + c, job.dtype, v, dst_vec);
+      } else {
+        for (int k = 0; k < 4; ++k)
+          if (c + k < job.cols) pack_store(job.dst, r * job.dst_ld + c + k, job.dtype, v[k]);
+      }
+    }
   }
   if (!job.dst_t) return;
   __syncthreads();
-  for (int cc = wv; cc < kPackTile; cc += kPackThreads / 64) {  // dst_t row c0 + cc, columns r0 + lane
-    const int64_t c = c0 + cc, r = r0 + lane;
-    if (c < job.cols && r < job.rows) pack_store(job.dst_t, c * job.dst_t_ld + r, job.dtype, tile[lane][cc]);
+  const bool t_vec = ((job.dst_t_ld * esz) % (4 * esz) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(job.dst_t) & (4 * esz - 1)) == 0);
+#pragma unroll
+  for (int i = 0; i < kPackTile / 16; ++i) {  // dst_t row c0 + cc, columns r0 + rq4 .. +3
+    const int cc = (threadIdx.x >> 4) + 16 * i, rq4 = (threadIdx.x & 15) * 4;
+    const int64_t c = c0 + cc, r = r0 + rq4;
+    if (c >= job.cols) continue;
+    const float v[4] = {tile[rq4][cc], tile[rq4 + 1][cc], tile[rq4 + 2][cc], tile[rq4 + 3][cc]};
+    if (r + 3 < job.rows) {
+      pack_store4(job.dst_t, c * job.dst_t_ld + r, job.dtype, v, t_vec);
+    } else {
+      for (int k = 0; k < 4; ++k)
+        if (r + k < job.rows) pack_store(job.dst_t, c * job.dst_t_ld + r + k, job.dtype, v[k]);
+    }
   }
 }
 

@@ -405,15 +405,21 @@ __device__ __forceinline__ void env_bookkeeping(const EnvView &e, int64_t ei, co
   st_row[0] = o.r_pos; st_row[1] = o.r_rot; st_row[2] = o.r_vel; st_row[3] = o.r_ang; st_row[4] = o.pr;
 }
 
-// one stats row per workgroup, summed over its envs in LDS (no atomics)
+// one stats row per workgroup, summed over its envs in LDS (no atomics); `prev` = the row's old
+// value, loaded at kernel start (stats_prefetch) so the read-modify-write adds no memory round trip
+// to the kernel's tail
+__device__ __forceinline__ double stats_prefetch(const EnvView &e) {
+  return (e.stats && threadIdx.x < 10) ? e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] : 0.0;
+}
+
 template <int kEnvs>
-__device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10]) {
+__device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10], double prev) {
   __syncthreads();
   if (threadIdx.x < 10) {
     double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < kEnvs; ++j) acc += sh[j][threadIdx.x];
-    e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] += acc;
+    e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] = prev + acc;
   }
 }
 
@@ -436,6 +442,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   return;
 #endif
 
+  const double st_prev = stats_prefetch(e);
   // per-env scalars (broadcast loads: every lane of the half-wave reads the same word)
   const int prog = (int)e.progress[ei] + 1;
   const float st = e.start[ei];
@@ -508,7 +515,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
 #pragma unroll
       for (int k = 0; k < 10; ++k) sh_stats[g][k] = st_row[k];
     }
-    flush_stats<kEnvsPerBlock>(e, sh_stats);
+    flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
   }
 }
 
