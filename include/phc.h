@@ -210,12 +210,15 @@ int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_lib *lib, c
  * humanoid_phc.py:274-281; ground plane :255-262).  Featherstone ABA over the 24-body tree (6-DoF
  * root, 23 ball joints), implicit joint-space PD to pd_target [N,69] (exp-map targets, stiffness /
  * damping x kp_scale / kd_scale), penalty ground contact with capped viscous friction,
- * control_freq_inv x substeps semi-implicit Euler substeps of sim_dt / substeps.  Reads the root
- * record of rigid_body_state and dof_state, writes rigid_body_state [N,24,13], root_state (if set),
- * dof_state [N,69,2] and dof_force [N,69] (the applied PD torques of the last substep).
+ * control_freq_inv x substeps semi-implicit Euler substeps of sim_dt / substeps, optional penalty
+ * self-collision, per-link angular damping, angular-velocity clamp.  Reads the root record of
+ * rigid_body_state and dof_state, writes rigid_body_state [N,24,13], root_state (if set),
+ * dof_state [N,69,2] and dof_force [N,69] (the applied PD torques of the last substep).  Rigid-body
+ * linear velocities are those of each body's centre of mass (PhysX's convention; the root record's
+ * is read back as such).
  * body_model: device float [PHC_NUM_BODIES][PHC_BODY_MODEL_STRIDE] (layout in phc_physics.hip,
  * packed by puffer-phc_amd/physics.py from assets/smpl_body_model.json). */
-#define PHC_BODY_MODEL_STRIDE 64
+#define PHC_BODY_MODEL_STRIDE 80
 typedef struct phc_physics_params {
   float sim_dt;             /* 1/60 (isaacgym_env.py:38) */
   int32_t control_freq_inv; /* 2 */
@@ -228,7 +231,13 @@ typedef struct phc_physics_params {
   float friction;           /* Coulomb coefficient (ground plane friction 1.0) */
   float friction_damping;   /* N s/m: tangential force = -min(friction_damping, mu fn / |vt|) vt */
   float gravity;            /* m/s^2 along z (-9.81) */
-  float reserved;
+  float angular_damping;    /* per-link angular damping (AssetOptions.angular_damping 0.01,
+                               humanoid_phc.py:212): torque -d I_com omega on every body */
+  float max_angular_velocity; /* AssetOptions.max_angular_velocity 100 (humanoid_phc.py:213): the
+                                 root's and every joint's angular velocity clamped to this magnitude */
+  int32_t self_collision;   /* RobotConfig.has_self_collision: penalty contact between the body pairs
+                               of the model's collision masks (the reference's shape filter bits,
+                               humanoid_phc.py:370-381, minus jointed parent / child pairs) */
 } phc_physics_params;
 int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const float *body_model,
                      const phc_physics_params *p, void *stream);

@@ -8,7 +8,8 @@ with friction 1, restitution 0 (:255-262).  PhysX is a closed binary and not in 
 **parity with PhysX is unpinned**: this module restates the algorithm the HIP kernel
 (puffer-phc_amd/csrc/phc_physics.hip) implements — Featherstone's articulated-body algorithm over
 the 24-body tree with a 6-DoF floating root and 23 three-DoF ball joints, implicit joint-space PD,
-penalty ground contact with capped viscous friction, semi-implicit Euler substeps — in float64 with
+penalty ground contact with capped viscous friction, penalty self-collision between the filtered
+capsule pairs, angular damping and the angular-velocity cap, semi-implicit Euler substeps — in float64 with
 generic 6x6 spatial matrices, as the checker the kernel is compared against.  It is pinned by
 physical laws instead (tests/test_physics_oracle.py): closed-form free fall, conservation of
 spatial momentum and energy of the unforced free-floating tree, the PD limit, a standing humanoid.
@@ -18,7 +19,8 @@ Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may import this
 Conventions (shared with the kernel): quaternions x, y, z, w; body frames at the MJCF body origins;
 spatial vectors [angular; linear] in body coordinates; a joint's generalized velocity is the child's
 angular velocity relative to its parent in child coordinates; dof_pos is the exp map (rotation
-vector) of the joint rotation; rigid-body linear velocity is that of the body origin.
+vector) of the joint rotation; rigid-body records hold the body origin's position and the centre
+of mass's linear velocity (PhysX's convention).
 """
 
 import json
@@ -32,7 +34,11 @@ MODEL_JSON = os.path.join(os.path.dirname(__file__), "..", "puffer-phc_amd", "as
 
 DEFAULT_PARAMS = dict(sim_dt=1.0 / 60.0, control_freq_inv=2, substeps=8, kp_scale=1.0, kd_scale=1.0,
                       contact_stiffness=5.0e4, contact_damping=1.0e3, friction=1.0, friction_damping=1.0e3,
-                      gravity=-9.81)
+                      gravity=-9.81, angular_damping=0.01, max_angular_velocity=100.0, self_collision=True)
+
+# shape filters of the capsule humanoid (puffer_phc/envs/humanoid_phc.py:374): shapes whose words
+# share a bit do not collide; PhysX never collides a link with its parent
+FILTER = (0, 0, 7, 16, 12, 0, 56, 2, 33, 128, 0, 192, 0, 64, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
 
 
 # ------------------------------------------------------------------ model --
@@ -60,6 +66,29 @@ def load_model(path=MODEL_JSON):
             p = [list(c + h * np.array([sx, sy, sz])) + [0.0] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]
         pts.append(np.array(p, dtype=np.float64))
     m["points"] = pts
+    # self-collision capsules (p0, p1, radius): sphere = zero-length segment, box = segment on its
+    # longest half-axis shortened by the radius = the smallest other half-extent
+    seg = np.zeros((NUM_BODIES, 2, 3))
+    rad = np.zeros(NUM_BODIES)
+    for i, b in enumerate(bodies):
+        s = b["shape"]
+        if s["type"] == "sphere":
+            seg[i] = [s["center"], s["center"]]
+            rad[i] = s["radius"]
+        elif s["type"] == "capsule":
+            seg[i] = [s["p0"], s["p1"]]
+            rad[i] = s["radius"]
+        else:
+            c, h = np.array(s["center"]), np.array(s["half"])
+            k = int(np.argmax(h))
+            rad[i] = min(h[(k + 1) % 3], h[(k + 2) % 3])
+            d = np.zeros(3)
+            d[k] = max(h[k] - rad[i], 0.0)
+            seg[i] = [c - d, c + d]
+    m["seg"], m["seg_r"] = seg, rad
+    par = m["parent"]
+    m["pairs"] = [(i, j) for i in range(NUM_BODIES) for j in range(NUM_BODIES)
+                  if i != j and par[i] != j and par[j] != i and not (FILTER[i] & FILTER[j])]
     # spatial inertia about the body origin, body coordinates (Featherstone's mcI)
     I6 = np.zeros((NUM_BODIES, 6, 6))
     for i in range(NUM_BODIES):
@@ -150,13 +179,16 @@ class State:
     """root_pos, root_quat (world), root_vel, root_ang_vel (world), joint_quat [E, 24, 4] (index 0
     unused), joint_vel [E, 24, 3] (relative angular velocity, child coordinates)."""
 
-    def __init__(self, root_pos, root_quat, root_vel, root_ang_vel, dof_pos, dof_vel):
+    def __init__(self, root_pos, root_quat, root_vel, root_ang_vel, dof_pos, dof_vel, com0=None):
         n = root_pos.shape[0]
         self.p0 = np.array(root_pos, dtype=np.float64)
         self.q0 = normalize(np.array(root_quat, dtype=np.float64))
         R0 = quat_to_mat(self.q0)
         self.w0 = np.einsum("nji,nj->ni", R0, root_ang_vel)  # body coordinates
+        # root_vel is the centre of mass's velocity (PhysX): the origin's is v_com - w x com
         self.v0 = np.einsum("nji,nj->ni", R0, root_vel)
+        if com0 is not None:
+            self.v0 = self.v0 - np.cross(self.w0, com0)
         self.r = np.zeros((n, NUM_BODIES, 4))
         self.r[..., 3] = 1.0
         self.r[:, 1:] = quat_from_rotvec(np.asarray(dof_pos, dtype=np.float64).reshape(n, NUM_BODIES - 1, 3))
@@ -186,17 +218,76 @@ def forward_kinematics(model, st):
     return Q, R, P, V, Xs
 
 
+def _dot(a, b):
+    return np.einsum("...i,...i->...", a, b)
+
+
+def closest_points(p0, d1, q0, d2):
+    """Clamped closest-point parameters (s, t) of segments p0 + s d1 and q0 + t d2, s, t in [0, 1]
+    (the clamped 2x2 solve, then t clamped and s re-solved); any leading batch shape."""
+    r = p0 - q0
+    a, e, f, c, b = _dot(d1, d1), _dot(d2, d2), _dot(d2, r), _dot(d1, r), _dot(d1, d2)
+    den = a * e - b * b
+    ga, ge = a > 1e-12, e > 1e-12
+    a1, e1 = np.where(ga, a, 1.0), np.where(ge, e, 1.0)
+    s = np.where(den > 1e-12, np.clip((b * f - c * e) / np.where(den > 1e-12, den, 1.0), 0, 1), 0.0)
+    t = (b * s + f) / e1
+    s = np.where(t < 0, np.clip(-c / a1, 0, 1), np.where(t > 1, np.clip((b - c) / a1, 0, 1), s))
+    t = np.clip(t, 0, 1)
+    both = ga & ge
+    s = np.where(both, s, np.where(ga, np.clip(-c / a1, 0, 1), 0.0))
+    t = np.where(both, t, np.where(ga, 0.0, np.clip(f / e1, 0, 1)))
+    return s, t
+
+
+def self_contacts(model, R, P, V, prm):
+    """Penalty self-collision between the filtered body pairs, both bodies as capsules: per ordered
+    pair (i, j) the force on i, normal stiffness x depth + damping x approach rate (>= 0), applied at
+    the middle of the overlap; a body-coordinate wrench about i's origin [E, 24, 6]."""
+    n = P.shape[0]
+    pi = np.array([p[0] for p in model["pairs"]])
+    pj = np.array([p[1] for p in model["pairs"]])
+    ends = P[:, :, None, :] + np.einsum("nbij,bkj->nbki", R, model["seg"])  # [E, 24, 2, 3] world
+    W = np.einsum("nbij,nbj->nbi", R, V[..., :3])
+    Vo = np.einsum("nbij,nbj->nbi", R, V[..., 3:])
+    ri, rj = model["seg_r"][pi], model["seg_r"][pj]
+    a0, b0 = ends[:, pi, 0], ends[:, pj, 0]  # [E, pairs, 3]
+    d1, d2 = ends[:, pi, 1] - a0, ends[:, pj, 1] - b0
+    s, t = closest_points(a0, d1, b0, d2)
+    c1 = a0 + s[..., None] * d1
+    dd = b0 + t[..., None] * d2 - c1
+    dist = np.linalg.norm(dd, axis=-1)
+    pen = ri + rj - dist
+    nrm = np.where((dist > 1e-6)[..., None], dd / np.maximum(dist, 1e-30)[..., None], np.array([0.0, 0.0, 1.0]))
+    x = c1 + nrm * (ri - 0.5 * pen)[..., None]
+    vi = Vo[:, pi] + np.cross(W[:, pi], x - P[:, pi])
+    vj = Vo[:, pj] + np.cross(W[:, pj], x - P[:, pj])
+    vn = _dot(vi - vj, nrm)
+    fm = np.where(pen > 0, np.maximum(0.0, prm["contact_stiffness"] * pen + prm["contact_damping"] * vn), 0.0)
+    Rt = np.swapaxes(R[:, pi], -1, -2)
+    Fb = np.einsum("npij,npj->npi", Rt, -fm[..., None] * nrm)
+    wrench = np.concatenate([np.cross(np.einsum("npij,npj->npi", Rt, x - P[:, pi]), Fb), Fb], -1)
+    f = np.zeros((n, NUM_BODIES, 6))
+    np.add.at(f, (slice(None), pi), wrench)
+    return f
+
+
 def external_forces(model, R, P, V, prm):
-    """Gravity and penalty ground contact as body-coordinate wrenches about each body origin."""
+    """Gravity, angular damping, penalty ground contact and self-collision as body-coordinate
+    wrenches about each body origin."""
     n = P.shape[0]
     f = np.zeros((n, NUM_BODIES, 6))
     g = np.array([0.0, 0.0, prm["gravity"]])
     zhat = np.array([0.0, 0.0, 1.0])
+    if prm["self_collision"]:
+        f += self_contacts(model, R, P, V, prm)
     for i in range(NUM_BODIES):
         Rt = np.swapaxes(R[:, i], -1, -2)
         F = model["mass"][i] * np.einsum("nij,j->ni", Rt, g)
         f[:, i, :3] += np.cross(model["com"][i], F)
         f[:, i, 3:] += F
+        # angular damping (humanoid_phc.py:212): a pure torque -d Ic w
+        f[:, i, :3] -= prm["angular_damping"] * np.einsum("ij,nj->ni", model["inertia"][i], V[:, i, :3])
         for c in model["points"][i]:
             x = P[:, i] + np.einsum("nij,j->ni", R[:, i], c[:3])
             d = c[3] - x[:, 2]  # penetration depth
@@ -211,6 +302,14 @@ def external_forces(model, R, P, V, prm):
             f[:, i, :3] += np.cross(a, Fb)
             f[:, i, 3:] += Fb
     return f
+
+
+def clamp_norm(x, m):
+    """Rows of x scaled down to norm <= m (m <= 0: no cap)."""
+    if m <= 0:
+        return x
+    nrm = np.linalg.norm(x, axis=-1, keepdims=True)
+    return np.where(nrm > m, x * (m / np.maximum(nrm, 1e-30)), x)
 
 
 def substep(model, st, target, prm, dt):
@@ -256,8 +355,9 @@ def substep(model, st, target, prm, dt):
     applied = tau - dt * (kd + dt * kp) * qdd
     # integrate: velocities first, then positions with the new velocities
     st.om[:, 1:] += dt * qdd[:, 1:]
+    st.om = clamp_norm(st.om, prm["max_angular_velocity"])  # AssetOptions.max_angular_velocity, :213
     st.r[:, 1:] = normalize(quat_mul(st.r[:, 1:], quat_from_rotvec(dt * st.om[:, 1:])))
-    st.w0 = st.w0 + dt * a[:, 0, :3]
+    st.w0 = clamp_norm(st.w0 + dt * a[:, 0, :3], prm["max_angular_velocity"])
     st.v0 = st.v0 + dt * a[:, 0, 3:]
     st.p0 = st.p0 + dt * np.einsum("nij,nj->ni", R[:, 0], st.v0)
     st.q0 = normalize(quat_mul(st.q0, quat_from_rotvec(dt * st.w0)))
@@ -265,11 +365,11 @@ def substep(model, st, target, prm, dt):
 
 
 def body_states(model, st):
-    """Isaac Gym rigid-body layout [E, 24, 13]: pos, quat (xyzw), linear vel (origin), angular vel;
-    world frame."""
+    """Isaac Gym rigid-body layout [E, 24, 13]: pos (body origin), quat (xyzw), linear velocity of the
+    centre of mass (PhysX's), angular velocity; world frame."""
     Q, R, P, V, _ = forward_kinematics(model, st)
-    return np.concatenate([P, Q, np.einsum("nbij,nbj->nbi", R, V[..., 3:]), np.einsum("nbij,nbj->nbi", R, V[..., :3])],
-                          -1)
+    vcom = V[..., 3:] + np.cross(V[..., :3], model["com"][None])
+    return np.concatenate([P, Q, np.einsum("nbij,nbj->nbi", R, vcom), np.einsum("nbij,nbj->nbi", R, V[..., :3])], -1)
 
 
 def step(model, rb, dof_state, pd_target, params=None):
@@ -278,7 +378,8 @@ def step(model, rb, dof_state, pd_target, params=None):
     (rigid_body_state, dof_state, dof_force [E, 69])."""
     prm = dict(DEFAULT_PARAMS, **(params or {}))
     n = rb.shape[0]
-    st = State(rb[:, 0, 0:3], rb[:, 0, 3:7], rb[:, 0, 7:10], rb[:, 0, 10:13], dof_state[..., 0], dof_state[..., 1])
+    st = State(rb[:, 0, 0:3], rb[:, 0, 3:7], rb[:, 0, 7:10], rb[:, 0, 10:13], dof_state[..., 0], dof_state[..., 1],
+               com0=model["com"][0])
     target = np.zeros((n, NUM_BODIES, 3))
     target[:, 1:] = np.asarray(pd_target, dtype=np.float64).reshape(n, NUM_BODIES - 1, 3)
     dt = prm["sim_dt"] / prm["substeps"]

@@ -63,7 +63,8 @@ class PhysicsParamsC(ctypes.Structure):
                 ("tree_depth", ctypes.c_int32), ("kp_scale", ctypes.c_float), ("kd_scale", ctypes.c_float),
                 ("contact_stiffness", ctypes.c_float), ("contact_damping", ctypes.c_float),
                 ("friction", ctypes.c_float), ("friction_damping", ctypes.c_float), ("gravity", ctypes.c_float),
-                ("reserved", ctypes.c_float)]
+                ("angular_damping", ctypes.c_float), ("max_angular_velocity", ctypes.c_float),
+                ("self_collision", ctypes.c_int32)]
 
 
 class PdMapC(ctypes.Structure):
@@ -1011,7 +1012,7 @@ def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):
            "phc_physics_replay")
 
 
-BODY_MODEL_STRIDE = 64
+BODY_MODEL_STRIDE = 80
 
 
 def physics_env_struct(rigid_body_state, dof_state, dof_force, root_state=None):

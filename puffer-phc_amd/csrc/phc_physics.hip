@@ -22,10 +22,12 @@
 // root record, dof_state and targets; write the 24 rigid-body records, dof_state, dof_force).  The
 // kernel is VALU-latency bound (about 3k VALU instructions per body per substep).
 //
-// Body model row (floats, PHC_BODY_MODEL_STRIDE = 64):
+// Body model row (floats, PHC_BODY_MODEL_STRIDE = 80):
 //   0 parent  1 level  2 num_children  3..5 children  6..8 joint offset (parent coords)  9 mass
 //   10..12 com  13..18 inertia about the com (xx yy zz xy xz yz)  19..21 kp  22..24 kd  25..27 armature
 //   28 num_points  32..63 contact points (x y z radius) x 8
+//   64..66 / 67..69 self-collision segment end points, 70 its radius (the geom as a capsule)
+//   71 self-collision mask: bit j set = this body collides with body j
 #include "phc_common.h"
 
 #include <hip/hip_ext.h>
@@ -59,6 +61,8 @@ struct PhysConsts {
   int nsub;
   int depth;
   float kp_scale, kd_scale, kn, cn, mu, ct, g;
+  float ang_damp, max_w;
+  int self_col;
 };
 
 struct M3 {
@@ -230,15 +234,19 @@ struct PdArgs {
   const uint8_t *frozen;
 };
 
-// Per-block LDS: the body table with the derived constants (row stride 65 floats: lanes b = 0..23
+// Per-block LDS: the body table with the derived constants (row stride 79 floats: lanes b = 0..23
 // reading the same field hit 24 distinct banks), per env the tree-pass slots (FK record 13 / inward
 // contribution 27 / acceleration 6 floats) and each body's outward-pass operands K = D^-1 A,
 // L = D^-1 B, y = D^-1 u (21 floats), so they do not occupy registers between the passes.
-constexpr int kTab = 65;
+constexpr int kTab = 79;  // odd: the 24 lanes reading one field hit 24 distinct banks
 enum : int {
   T_PARENT = 0, T_LEVEL = 1, T_NCH = 2, T_CH = 3, T_OFF = 6, T_MASS = 9, T_COM = 10, T_A0 = 13 /* 9, full */,
-  T_KP = 22, T_KD = 25, T_DEXT = 28, T_NPTS = 31, T_PTS = 32 /* 32 */
+  T_KP = 22, T_KD = 25, T_DEXT = 28, T_NPTS = 31, T_PTS = 32 /* 32 */, T_IC = 64 /* 6, sym */,
+  T_SEG = 70 /* p0 3, p1 3, radius */, T_MASK = 77
 };
+// per env and body, refreshed every substep for the self-collision pass: world segment end points,
+// radius, world angular velocity, world origin velocity, origin
+constexpr int kSeg = 16;
 constexpr int kOut = 21;
 
 __device__ __forceinline__ v3 ld3(const float *p) { return {p[0], p[1], p[2]}; }
@@ -254,6 +262,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
   __shared__ float tab[kBodies * kTab];
   __shared__ float slots[kPhysEnvs][kBodies][kSlot];
   __shared__ float outw[kPhysEnvs][kBodies][kOut];
+  __shared__ float segw[kPhysEnvs][kBodies][kSeg];
   const int lane = threadIdx.x % kGroup, sub = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kPhysEnvs + sub;
   const bool act = env < e.n && lane < kBodies;
@@ -292,6 +301,9 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     const int npts = min(max((int)md[28], 0), kMaxPoints);
     t[T_NPTS] = (float)npts;
     for (int k = 0; k < 4 * kMaxPoints; ++k) t[T_PTS + k] = md[32 + k];
+    for (int k = 0; k < 6; ++k) t[T_IC + k] = md[13 + k];
+    for (int k = 0; k < 7; ++k) t[T_SEG + k] = md[64 + k];
+    t[T_MASK] = c.self_col ? md[71] : 0.0f;
   }
   __syncthreads();
   const float *T = tab + b * kTab;
@@ -314,8 +326,9 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     p0 = {s[0], s[1], s[2]};
     q0 = qnormalize(q4{s[3], s[4], s[5], s[6]});
     const M3 R0 = m3_quat(q0.x, q0.y, q0.z, q0.w);
-    v0 = m3_tv(R0, v3{s[7], s[8], s[9]});
     w0 = m3_tv(R0, v3{s[10], s[11], s[12]});
+    // the record holds the centre of mass's velocity (PhysX): the origin's is v_com - w x com
+    v0 = vsub(m3_tv(R0, v3{s[7], s[8], s[9]}), cross3(w0, ld3(T + T_COM)));
   } else if (act) {
     const float *d = e.dof_state + (ev * PHC_NUM_DOF + 3 * (b - 1)) * 2;
     r = quat_from_rotvec(v3{d[0], d[2], d[4]});
@@ -377,6 +390,76 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       const v3 com = ld3(T + T_COM);
       const v3 F = m3_tv(R, v3{0.0f, 0.0f, mass * c.g});
       v3 fn_ = cross3(com, F), ff = F;
+      // per-link angular damping (PhysX linear-in-omega damping): torque -d Ic w about the com
+      fn_ = vsub(fn_, vscale(m3_v(sym_full(T + T_IC), w), c.ang_damp));
+      // penalty self-collision: every pair this body's mask names, both bodies as capsules
+      const unsigned mask = (unsigned)T[T_MASK];
+      if (c.self_col) {  // grid-uniform: the barriers below are reached by every wave
+        const v3 s0 = m3_v(R, ld3(T + T_SEG)), s1 = m3_v(R, ld3(T + T_SEG + 3));
+        const v3 p0w = vadd(P, s0), p1w = vadd(P, s1);
+        const float rb = T[T_SEG + 6];
+        const v3 ww = m3_v(R, w), vw0 = m3_v(R, v);
+        float *sw = segw[sub][b];
+        if (act) {
+        sw[0] = p0w.x; sw[1] = p0w.y; sw[2] = p0w.z; sw[3] = p1w.x; sw[4] = p1w.y; sw[5] = p1w.z; sw[6] = rb;
+        sw[7] = ww.x; sw[8] = ww.y; sw[9] = ww.z; sw[10] = vw0.x; sw[11] = vw0.y; sw[12] = vw0.z;
+        sw[13] = P.x; sw[14] = P.y; sw[15] = P.z;
+        }
+        __syncthreads();
+        const v3 mid = vscale(vadd(p0w, p1w), 0.5f);
+        const v3 d1 = vsub(p1w, p0w);
+        const float hb = 0.5f * sqrtf(d1.x * d1.x + d1.y * d1.y + d1.z * d1.z) + rb;
+        for (int j = 0; j < kBodies; ++j) {
+          if (!act || !((mask >> j) & 1u)) continue;
+          const float *o = segw[sub][j];
+          const v3 q0 = ld3(o), q1 = ld3(o + 3);
+          const float rj = o[6];
+          const v3 d2 = vsub(q1, q0);
+          const v3 mj = vscale(vadd(q0, q1), 0.5f);
+          const float hj = 0.5f * sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z) + rj;
+          const v3 dm = vsub(mj, mid);
+          if (dm.x * dm.x + dm.y * dm.y + dm.z * dm.z > (hb + hj) * (hb + hj)) continue;
+          // closest points of the two segments (clamped parameters s, t)
+          const v3 r0 = vsub(p0w, q0);
+          const float a = d1.x * d1.x + d1.y * d1.y + d1.z * d1.z, e = d2.x * d2.x + d2.y * d2.y + d2.z * d2.z;
+          const float f = d2.x * r0.x + d2.y * r0.y + d2.z * r0.z;
+          float sp = 0.0f, tp = 0.0f;
+          if (a > 1e-12f && e > 1e-12f) {
+            const float cc = d1.x * r0.x + d1.y * r0.y + d1.z * r0.z;
+            const float bb = d1.x * d2.x + d1.y * d2.y + d1.z * d2.z;
+            const float den = a * e - bb * bb;
+            sp = den > 1e-12f ? fminf(fmaxf((bb * f - cc * e) / den, 0.0f), 1.0f) : 0.0f;
+            tp = (bb * sp + f) / e;
+            if (tp < 0.0f) {
+              tp = 0.0f;
+              sp = fminf(fmaxf(-cc / a, 0.0f), 1.0f);
+            } else if (tp > 1.0f) {
+              tp = 1.0f;
+              sp = fminf(fmaxf((bb - cc) / a, 0.0f), 1.0f);
+            }
+          } else if (a > 1e-12f) {
+            sp = fminf(fmaxf(-(d1.x * r0.x + d1.y * r0.y + d1.z * r0.z) / a, 0.0f), 1.0f);
+          } else if (e > 1e-12f) {
+            tp = fminf(fmaxf(f / e, 0.0f), 1.0f);
+          }
+          const v3 c1 = vadd(p0w, vscale(d1, sp)), c2 = vadd(q0, vscale(d2, tp));
+          const v3 dd = vsub(c2, c1);
+          const float dist = sqrtf(dd.x * dd.x + dd.y * dd.y + dd.z * dd.z);
+          const float pen = rb + rj - dist;
+          if (pen <= 0.0f) continue;
+          const v3 nrm = dist > 1e-6f ? vscale(dd, 1.0f / dist) : v3{0.0f, 0.0f, 1.0f};
+          const v3 x = vadd(c1, vscale(nrm, rb - 0.5f * pen));  // the contact point (mid penetration)
+          const v3 vb = vadd(vw0, cross3(ww, vsub(x, P)));
+          const v3 vj = vadd(ld3(o + 10), cross3(ld3(o + 7), vsub(x, ld3(o + 13))));
+          const v3 vr = vsub(vb, vj);
+          const float vn = vr.x * nrm.x + vr.y * nrm.y + vr.z * nrm.z;  // penetration rate
+          const float fm = fmaxf(0.0f, c.kn * pen + c.cn * vn);
+          const v3 Fb = m3_tv(R, vscale(nrm, -fm));  // pushes this body away from the partner
+          fn_ = vadd(fn_, cross3(m3_tv(R, vsub(x, P)), Fb));
+          ff = vadd(ff, Fb);
+        }
+        __syncthreads();  // segw is rewritten next substep
+      }
       const v3 zb = {R.m[6], R.m[7], R.m[8]};  // R^T z
       const int npts = (int)T[T_NPTS];
       for (int k = 0; k < ((PHC_PHYS_ABLATE & 2) ? 0 : npts); ++k) {
@@ -556,9 +639,13 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       applied = {tau.x - dt * (kd.x + dt * kp.x) * qdd.x, tau.y - dt * (kd.y + dt * kp.y) * qdd.y,
                  tau.z - dt * (kd.z + dt * kp.z) * qdd.z};
       om = vadd(om, vscale(qdd, dt));
+      const float wn2 = om.x * om.x + om.y * om.y + om.z * om.z;
+      if (wn2 > c.max_w * c.max_w) om = vscale(om, c.max_w * rsqrtf(wn2));  // max_angular_velocity
       r = qnormalize(qmul_std(r, quat_exp_increment(vscale(om, dt))));
     } else if (act) {
       w0 = vadd(w0, vscale(aw, dt));
+      const float wn2 = w0.x * w0.x + w0.y * w0.y + w0.z * w0.z;
+      if (wn2 > c.max_w * c.max_w) w0 = vscale(w0, c.max_w * rsqrtf(wn2));
       v0 = vadd(v0, vscale(av, dt));
       p0 = vadd(p0, vscale(m3_v(m3_quat(Q.x, Q.y, Q.z, Q.w), v0), dt));
       q0 = qnormalize(qmul_std(q0, quat_exp_increment(vscale(w0, dt))));
@@ -568,7 +655,8 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
   if (!act) return;  // no barrier follows
   {
     const M3 R = m3_quat(Q.x, Q.y, Q.z, Q.w);
-    const v3 vw = m3_v(R, v), ww = m3_v(R, w);
+    // the centre of mass's linear velocity (PhysX's rigid-body velocity): v + w x com
+    const v3 vw = m3_v(R, vadd(v, cross3(w, ld3(T + T_COM)))), ww = m3_v(R, w);
     float *o = e.rb + (env * kBodies + b) * kRec;
     o[0] = P.x; o[1] = P.y; o[2] = P.z;
     o[3] = Q.x; o[4] = Q.y; o[5] = Q.z; o[6] = Q.w;
@@ -606,8 +694,8 @@ static int physics_launch(const phc_env_buffers *env, const float *pd_target, co
               p->control_freq_inv, p->substeps);
   PHC_REQUIRE(p->tree_depth >= 1 && p->tree_depth <= 15, "physics_step: tree_depth must be 1..15");
   PHC_REQUIRE(p->contact_stiffness >= 0.0f && p->contact_damping >= 0.0f && p->friction >= 0.0f &&
-                  p->friction_damping >= 0.0f,
-              "physics_step: contact coefficients must be >= 0");
+                  p->friction_damping >= 0.0f && p->angular_damping >= 0.0f && p->max_angular_velocity >= 0.0f,
+              "physics_step: contact / damping coefficients must be >= 0");
   PhysConsts c;
   c.dt = p->sim_dt / (float)p->substeps;
   c.nsub = p->control_freq_inv * p->substeps;
@@ -619,6 +707,9 @@ static int physics_launch(const phc_env_buffers *env, const float *pd_target, co
   c.mu = p->friction;
   c.ct = p->friction_damping;
   c.g = p->gravity;
+  c.ang_damp = p->angular_damping;
+  c.max_w = p->max_angular_velocity > 0.0f ? p->max_angular_velocity : 3.0e38f;
+  c.self_col = p->self_collision;
   const PhysView v = {env->num_envs, env->rigid_body_state, env->root_state, env->dof_state,
                        const_cast<float *>(env->dof_force)};  // read-only for the env step, written here
   const int64_t blocks = (env->num_envs + kPhysEnvs - 1) / kPhysEnvs;

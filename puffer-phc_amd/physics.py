@@ -7,7 +7,8 @@ reads; `ArticulatedPhysics` is the physics object `HumanoidPHC` steps after writ
 in place of the replay stand-in (`HumanoidPHC(cfg, physics=ArticulatedPhysics(cfg))`).  The
 simulator's settings follow the reference where it states them (sim_dt 1/60 and control_freq_inv 2,
 envs/isaacgym_env.py:6-42; PD gains x kp_scale / kd_scale, humanoid_phc.py:274-281; ground friction
-1, :255-262); the contact model and the substep count are this solver's own (PhysX's TGS solver is a
+1, :255-262; angular damping and velocity cap, :212-213; self-collision filters, :370-381); the
+contact model and the substep count are this solver's own (PhysX's TGS solver is a
 closed binary) and documented in DESIGN.md §8.
 """
 
@@ -36,6 +37,50 @@ class PhysicsConfig:
     friction: float = 1.0
     friction_damping: float = 1.0e3
     gravity: float = -9.81
+    # AssetOptions of the humanoid asset (puffer_phc/envs/humanoid_phc.py:212-213): per-link angular
+    # damping (a torque -d Ic w) and the cap on every joint's / the root's angular velocity (rad/s)
+    angular_damping: float = 0.01
+    max_angular_velocity: float = 100.0
+    # RobotConfig.has_self_collision (puffer_phc/config.py:43, humanoid_phc.py:338 and :370-381):
+    # penalty contact between the body pairs the shape filters leave colliding
+    self_collision: bool = True
+
+
+# Shape collision filters of the capsule humanoid (has_mesh False, puffer_phc/envs/
+# humanoid_phc.py:374): two shapes whose filter words share a bit never collide
+SELF_COLLISION_FILTER = (0, 0, 7, 16, 12, 0, 56, 2, 33, 128, 0, 192, 0, 64, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+
+
+def collision_segment(shape):
+    """The geom as a capsule for self-collision: (p0, p1, radius) in body coordinates.  A sphere is
+    a zero-length segment, a capsule itself, a box the segment along its longest half-axis shortened
+    by the radius, the radius the smallest of the other two half-extents (inside the box)."""
+    if shape["type"] == "sphere":
+        c = list(shape["center"])
+        return c, c, shape["radius"]
+    if shape["type"] == "capsule":
+        return list(shape["p0"]), list(shape["p1"]), shape["radius"]
+    if shape["type"] == "box":
+        c, h = np.asarray(shape["center"], dtype=np.float64), np.asarray(shape["half"], dtype=np.float64)
+        k = int(np.argmax(h))
+        r = float(min(h[(k + 1) % 3], h[(k + 2) % 3]))
+        d = np.zeros(3)
+        d[k] = max(h[k] - r, 0.0)
+        return list(c - d), list(c + d), r
+    raise ValueError(f"unsupported geom type {shape['type']!r}")
+
+
+def self_collision_masks(parents, filters=SELF_COLLISION_FILTER):
+    """Per body the bit set of the bodies it collides with: filter words disjoint, not the same
+    body, not joined by a joint (PhysX never collides a link with its parent)."""
+    n = len(parents)
+    masks = [0] * n
+    for i in range(n):
+        for j in range(n):
+            if i == j or parents[i] == j or parents[j] == i or (filters[i] & filters[j]):
+                continue
+            masks[i] |= 1 << j
+    return masks
 
 
 def contact_points(shape):
@@ -52,7 +97,7 @@ def contact_points(shape):
 
 
 class BodyModel:
-    """The [24, 64] float32 body table of phc_physics.hip (row layout documented there)."""
+    """The [24, 80] float32 body table of phc_physics.hip (row layout documented there)."""
 
     def __init__(self, path=MODEL_JSON, device="cuda"):
         with open(path) as f:
@@ -97,6 +142,10 @@ class BodyModel:
             t[i, 25:28] = b["armature"]
             t[i, 28] = len(pts)
             t[i, 32:32 + 4 * len(pts)] = np.asarray(pts, dtype=np.float32).reshape(-1)
+            s0, s1, rad = collision_segment(b["shape"])
+            t[i, 64:67], t[i, 67:70], t[i, 70] = s0, s1, rad
+        self.masks = self_collision_masks([b["parent"] for b in bodies])
+        t[:, 71] = self.masks  # < 2^24: exact in float32
         self.names = [b["name"] for b in bodies]
         self.total_mass = float(sum(b["mass"] for b in bodies))
         # zero pose (every joint rotation the identity): body origins are the summed offsets, and
@@ -141,7 +190,8 @@ class ArticulatedPhysics:
         return _native.PhysicsParamsC(float(c.sim_dt), int(c.control_freq_inv), int(c.substeps), int(self.model.depth),
                                       float(c.kp_scale), float(c.kd_scale), float(c.contact_stiffness),
                                       float(c.contact_damping), float(c.friction), float(c.friction_damping),
-                                      float(c.gravity), 0.0)
+                                      float(c.gravity), float(c.angular_damping), float(c.max_angular_velocity),
+                                      int(bool(c.self_collision)))
 
     def step(self, env):
         """One step from env.pd_target (written by the caller)."""

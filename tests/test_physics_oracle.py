@@ -6,6 +6,8 @@ checks hold for any correct articulated-body solver with this integrator:
     in the substep (ratio ~4 when the substep shrinks 4x) — a wrong inertia, bias force or transform
     leaves an O(1) residual instead;
   * the PD drive: a joint settles at its target with gravity off;
+  * self-collision: the filtered pairs, the closest-point solve, internal (action = reaction) forces;
+  * angular damping dissipates, the velocity cap holds, records carry centre-of-mass velocities;
   * a standing humanoid on the ground neither sinks nor explodes;
 and the body-model extraction and its device packing are checked against the MJCF's numbers."""
 
@@ -35,7 +37,7 @@ def _momentum(model, rb):
         R = P.quat_to_mat(rb[:, i, 3:7])
         c = rb[:, i, 0:3] + np.einsum("nij,j->ni", R, model["com"][i])
         w = rb[:, i, 10:13]
-        vc = rb[:, i, 7:10] + np.cross(w, c - rb[:, i, 0:3])
+        vc = rb[:, i, 7:10]  # the record's linear velocity is the centre of mass's
         Iw = np.einsum("nij,jk,nlk->nil", R, model["inertia"][i], R)
         m = model["mass"][i]
         lin += m * vc
@@ -86,7 +88,8 @@ def test_unforced_tree_conserves_momentum_first_order(model):
     shorter substep."""
     rb, dof = _random_state(model, 2, 0, 5.0)
     free = dict(model, armature=model["armature"] * 0)
-    prm = dict(gravity=0.0, kp_scale=0.0, kd_scale=0.0)
+    prm = dict(gravity=0.0, kp_scale=0.0, kd_scale=0.0, angular_damping=0.0, max_angular_velocity=0.0,
+               self_collision=False)
     l0, a0, k0 = _momentum(model, rb)
     errs = []
     for sub in (8, 32):
@@ -140,7 +143,7 @@ def test_device_table_layout(model):
 
     bm = BodyModel(device="cpu")
     t = bm.host
-    assert bm.depth == 8 and t.shape == (24, 64)
+    assert bm.depth == 8 and t.shape == (24, 80)
     np.testing.assert_array_equal(t[1:, 0], model["parent"][1:])
     np.testing.assert_allclose(t[:, 9], model["mass"], rtol=1e-6)
     np.testing.assert_allclose(t[:, 6:9], model["offset"], atol=1e-7)
@@ -151,6 +154,96 @@ def test_device_table_layout(model):
         np.testing.assert_allclose(t[i, 32:32 + 4 * k].reshape(k, 4), model["points"][i], atol=1e-7)
         kids = [j for j in range(24) if model["parent"][j] == i and j > 0]
         assert int(t[i, 2]) == len(kids) and t[i, 3:3 + len(kids)].tolist() == kids
+        np.testing.assert_allclose(t[i, 64:70].reshape(2, 3), model["seg"][i], atol=1e-7)
+        np.testing.assert_allclose(t[i, 70], model["seg_r"][i], rtol=1e-6)
+        assert int(t[i, 71]) == sum(1 << j for (a, j) in model["pairs"] if a == i)
+
+
+def test_self_collision_pairs_follow_the_filters(model):
+    """humanoid_phc.py:374's filter words: shapes sharing a bit never collide, nor do a parent and
+    its child; the pair set is symmetric and the zero pose has no overlapping pair."""
+    pairs = set(model["pairs"])
+    assert all((j, i) in pairs for i, j in pairs)
+    names = json.load(open(P.MODEL_JSON))["bodies"]
+    idx = {b["name"]: k for k, b in enumerate(names)}
+    assert (idx["L_Knee"], idx["L_Toe"]) not in pairs  # filter 7 & 12 share bit 4
+    assert (idx["L_Knee"], idx["R_Ankle"]) not in pairs  # 7 & 2
+    assert (idx["L_Hand"], idx["Pelvis"]) in pairs and (idx["L_Hand"], idx["R_Hand"]) in pairs
+    assert (idx["L_Elbow"], idx["L_Wrist"]) not in pairs  # joined
+    assert len(pairs) == 2 * 245
+    rb, dof = P.rest_state(model, 1, 0.0)
+    st = P.State(rb[:, 0, 0:3], rb[:, 0, 3:7], rb[:, 0, 7:10], rb[:, 0, 10:13], dof[..., 0], dof[..., 1])
+    _, R, Pp, V, _ = P.forward_kinematics(model, st)
+    assert np.abs(P.self_contacts(model, R, Pp, V, P.DEFAULT_PARAMS)).max() == 0.0
+
+
+def test_closest_points_against_brute_force():
+    rng = np.random.default_rng(4)
+    n = 200
+    p0, q0 = rng.normal(0, 1, (n, 3)), rng.normal(0, 1, (n, 3))
+    d1, d2 = rng.normal(0, 1, (n, 3)), rng.normal(0, 1, (n, 3))
+    d1[:20] = 0.0  # a point against a segment
+    d2[20:40] = 0.0
+    d2[40:60] = 2.5 * d1[40:60]  # parallel segments
+    s, t = P.closest_points(p0, d1, q0, d2)
+    got = np.linalg.norm(p0 + s[:, None] * d1 - q0 - t[:, None] * d2, axis=-1)
+    g = np.linspace(0, 1, 201)
+    a = p0[:, None, None, :] + g[None, :, None, None] * d1[:, None, None, :]
+    b = q0[:, None, None, :] + g[None, None, :, None] * d2[:, None, None, :]
+    brute = np.linalg.norm(a - b, axis=-1).reshape(n, -1).min(-1)
+    assert np.all(got <= brute + 1e-12) and np.all(brute - got < 2e-2 * (1 + brute))
+
+
+def test_self_contact_forces_are_internal(model):
+    """Strongly bent poses make limbs overlap: every contact acts on both bodies of its pair at one
+    point with opposite forces, so the world net force and net torque of the self-contacts vanish."""
+    rng = np.random.default_rng(8)
+    n = 64
+    rb, dof = P.rest_state(model, n, 1.0)
+    dof[..., 0] = rng.normal(0, 1.2, (n, P.NUM_DOF))
+    dof[..., 1] = rng.normal(0, 2.0, (n, P.NUM_DOF))
+    st = P.State(rb[:, 0, 0:3], rb[:, 0, 3:7], rb[:, 0, 7:10], rb[:, 0, 10:13], dof[..., 0], dof[..., 1])
+    _, R, Pp, V, _ = P.forward_kinematics(model, st)
+    f = P.self_contacts(model, R, Pp, V, P.DEFAULT_PARAMS)
+    Fw = np.einsum("nbij,nbj->nbi", R, f[..., 3:])
+    Tw = np.einsum("nbij,nbj->nbi", R, f[..., :3]) + np.cross(Pp, Fw)  # about the world origin
+    touching = np.abs(Fw).sum((1, 2)) > 1.0
+    assert touching.sum() >= n // 4
+    scale = np.abs(Fw).sum((1, 2)).max()
+    assert np.abs(Fw.sum(1)).max() < 1e-9 * scale and np.abs(Tw.sum(1)).max() < 1e-8 * scale
+
+
+def test_angular_damping_and_velocity_cap(model):
+    """Airborne, gravity / gains off: angular damping only removes kinetic energy; a joint spun
+    past max_angular_velocity leaves the step at the cap."""
+    rb, dof = _random_state(model, 2, 5, 5.0)
+    free = dict(model, armature=model["armature"] * 0)
+    base = dict(gravity=0.0, kp_scale=0.0, kd_scale=0.0, self_collision=False, max_angular_velocity=0.0)
+    _, _, k0 = _momentum(model, rb)
+    ke = {}
+    for d in (0.0, 2.0):
+        r, q, _ = P.step(free, rb.copy(), dof.copy(), np.zeros((2, P.NUM_DOF)), dict(base, angular_damping=d, substeps=32))
+        ke[d] = _momentum(model, r)[2]
+    assert np.all(ke[2.0] < ke[0.0] - 1e-3 * k0)
+    dof[0, 6, 1] = 400.0
+    _, q, _ = P.step(free, rb, dof, np.zeros((2, P.NUM_DOF)), dict(base, max_angular_velocity=100.0))
+    w = np.linalg.norm(q[:, :, 1].reshape(2, 23, 3), axis=-1)
+    assert w.max() <= 100.0 + 1e-9 and abs(w[0, 2] - 100.0) < 1e-9
+
+
+def test_record_velocity_is_the_centre_of_mass_velocity(model):
+    """A spinning free body: each record's linear velocity is d/dt of its centre of mass."""
+    rb, dof = _random_state(model, 1, 9, 5.0)
+    prm = dict(gravity=0.0, kp_scale=0.0, kd_scale=0.0, self_collision=False, angular_damping=0.0,
+               max_angular_velocity=0.0, control_freq_inv=1, substeps=64, sim_dt=1e-3)
+
+    def coms(r):
+        return r[0, :, 0:3] + np.einsum("bij,bj->bi", P.quat_to_mat(r[0, :, 3:7]), model["com"])
+
+    r1, d1, _ = P.step(model, rb, dof, np.zeros((1, P.NUM_DOF)), prm)
+    r2, _, _ = P.step(model, r1, d1, np.zeros((1, P.NUM_DOF)), prm)
+    fd = (coms(r2) - coms(rb)) / 2e-3
+    np.testing.assert_allclose(r1[0, :, 7:10], fd, atol=2e-3 * (1 + np.abs(fd).max()))
 
 
 def test_product_rest_state_matches_oracle(model):
