@@ -233,8 +233,9 @@ __device__ __forceinline__ void read_frag(const char *lds_tile, int row, int chu
 
 // Tile geometry: BM x BN block tile, WGM x WGN waves, each owning a TM x TN = (BM / WGM) x
 // (BN / WGN) sub-tile of (TM / 16) x (TN / 16) MFMA blocks; STAGES operand buffers in LDS.
-template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_, int BK_ = 64> struct Tile {
+template <int BM_, int BN_, int WGM_, int WGN_, int STAGES_, int BK_ = 64, int WPE_ = 1> struct Tile {
   static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, STAGES = STAGES_, BK = BK_;
+  static constexpr int kWavesPerEU = WPE_;  // occupancy floor handed to the register allocator
   static constexpr int kWaves = WGM * WGN, kThreads = kWaves * 64;
   static constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   static constexpr int kStageBytes = (BM + BN) * BK * 2;
@@ -355,6 +356,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
+  {
   const int kt_n = g.k / TL::BK;
   auto stage = [&](int kt, char *st, int parts = 3) {  // parts: 1 = A tile, 2 = B tile, 4 / 8 = A halves
     if (parts & 1) stage_tile<BM, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
@@ -390,8 +392,9 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
       rd = rd == S - 1 ? 0 : rd + 1;
     }
   }
+  }
 
-  if (g.discard) {  // measurement aid: main loop only (keeps the accumulators alive)
+  if (g.discard == 1) {  // measurement aid: main loop only (keeps the accumulators alive)
     float t = 0.0f;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -453,8 +456,26 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   };
   using RawV = typename std::conditional<VW == 8, uint4, uint2>::type;  // VW half-precision values
   using RawN = typename std::conditional<VW == 8, u4v, u2v>::type;
+  // the grad epilogues' aux (pre-activation) rows of a pass: the first batch is issued before the
+  // pass's image write so its HBM latency overlaps the LDS round trip
+  constexpr int U = (kGrad && VW == 8) ? PHC_GEMM_GRAD_U8 : 4;  // 16-B aux rows in flight per batch
+  static_assert(IT % U == 0, "row batches");
+  const bool pipe = kGrad && g.aux_half;
+  RawV raw[2][kGrad ? U : 1];
+  auto load_raw = [&](int pass, int b) {
+    if constexpr (kGrad) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = m0 + trow(pass, b * U + u);
+        const T *src = static_cast<const T *>(g.aux) + ab + row * as;
+        raw[b & 1][u] = (g.nt & 4) ? __builtin_bit_cast(RawV, __builtin_nontemporal_load(reinterpret_cast<const RawN *>(src)))
+                                   : *reinterpret_cast<const RawV *>(src);
+      }
+    }
+  };
 #pragma unroll
   for (int pass = 0; pass < TL::kEpPasses; ++pass) {
+    if (full && pipe) load_raw(pass, 0);
     lds_barrier();  // operand tiles / the previous pass's image are no longer read
 #pragma unroll
     for (int i = pass * TL::kEpMI; i < (pass + 1) * TL::kEpMI; ++i)
@@ -471,28 +492,12 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
       // whole tile in range, VW whole columns per thread: offsets are base + row * stride, rows
       // in batches of U; a half-precision aux is software-pipelined (batch b + 1's loads in
       // flight while batch b is processed), an fp32 one loaded per batch
-      constexpr int U = (kGrad && VW == 8) ? PHC_GEMM_GRAD_U8 : 4;  // 16-B aux rows in flight per batch
-      static_assert(IT % U == 0, "row batches");
-      const bool pipe = kGrad && g.aux_half;
-      RawV raw[2][kGrad ? U : 1];
-      auto load_raw = [&](int b) {
-        if constexpr (kGrad) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int64_t row = m0 + trow(pass, b * U + u);
-            const T *src = static_cast<const T *>(g.aux) + ab + row * as;
-            raw[b & 1][u] = (g.nt & 4) ? __builtin_bit_cast(RawV, __builtin_nontemporal_load(reinterpret_cast<const RawN *>(src)))
-                                       : *reinterpret_cast<const RawV *>(src);
-          }
-        }
-      };
-      if (pipe) load_raw(0);
 #pragma unroll
       for (int i0 = 0; i0 < IT; i0 += U) {
         float av[U][VW];
         if constexpr (kGrad) {
           if (pipe) {
-            if (i0 + U < IT) load_raw(i0 / U + 1);
+            if (i0 + U < IT) load_raw(pass, i0 / U + 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               T h[VW];
@@ -534,7 +539,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
 #pragma unroll
             for (int q = 0; q < VW; ++q) v[q] += biasv[q];
             if constexpr (EPI == PHC_EPI_BIAS_SILU) {
-              if (g.aux) aux_store_v<T, VW>(g, ab + row * as, v);
+              if (g.aux && g.discard != 2) aux_store_v<T, VW>(g, ab + row * as, v);
 #pragma unroll
               for (int q = 0; q < VW; ++q) v[q] = gemm_silu(v[q]);
             } else if constexpr (EPI == PHC_EPI_BIAS_RELU) {
@@ -542,7 +547,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
               for (int q = 0; q < VW; ++q) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
             }
           }
-          gemm_store_v<OutT, VW>(g.out, ob + row * os, v, g.nt & 1);
+          if (g.discard != 2) gemm_store_v<OutT, VW>(g.out, ob + row * os, v, g.nt & 1);
         }
       }
       continue;
@@ -634,24 +639,25 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   }
 }
 
-// One tile per workgroup, XCD-major renumbering (bijective for any grid size); or, with fewer
-// workgroups than tiles (phc_gemm_desc.max_workgroups), a persistent loop: step s hands tiles
+// One tile per workgroup, XCD-major renumbering (bijective for any grid size); or (PERSIST, with
+// fewer workgroups than tiles: phc_gemm_desc.max_workgroups) a persistent loop: step s hands tiles
 // [s * nwg, (s + 1) * nwg) out XCD-major, so the workgroups sharing an XCD's L2 walk neighbouring
-// tiles of the same A panels at every step.
-template <typename T, typename OutT, int EPI, typename TL>
-__global__ __launch_bounds__(TL::kThreads) void k_twin_gemm(GemmArgs g) {
+// tiles of the same A panels at every step.  Separate instantiations: inlined into one kernel the
+// persistent copy's hoisted epilogue addresses spilled registers of the one-tile copy as well.
+template <typename T, typename OutT, int EPI, typename TL, bool PERSIST>
+__global__ __launch_bounds__(TL::kThreads) __attribute__((amdgpu_waves_per_eu(TL::kWavesPerEU, 8))) void k_twin_gemm(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][A BM rows | B BN rows]
   const int nwg = gridDim.x, orig = blockIdx.x;
-  const int total = g.tiles_m * g.tiles_n * g.batch;
-  if (nwg >= total) {
+  if constexpr (!PERSIST) {
     twin_gemm_tile<T, OutT, EPI, TL>(g, smem, xcd_first(nwg, orig % 8) + orig / 8);
-    return;
-  }
-  const int x = orig % 8, l = orig / 8;
-  for (int base = 0; base < total; base += nwg) {
-    const int cnt = total - base < nwg ? total - base : nwg;
-    if (l < xcd_count(cnt, x)) twin_gemm_tile<T, OutT, EPI, TL>(g, smem, base + xcd_first(cnt, x) + l);
-    lds_barrier();  // the epilogue image is read out before the next tile's operands land
+  } else {
+    const int total = g.tiles_m * g.tiles_n * g.batch;
+    const int x = orig % 8, l = orig / 8;
+    for (int base = 0; base < total; base += nwg) {
+      const int cnt = total - base < nwg ? total - base : nwg;
+      if (l < xcd_count(cnt, x)) twin_gemm_tile<T, OutT, EPI, TL>(g, smem, base + xcd_first(cnt, x) + l);
+      lds_barrier();  // the epilogue image is read out before the next tile's operands land
+    }
   }
 }
 
@@ -954,10 +960,12 @@ static thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;  // this launch
 
 template <typename T, typename OutT, int EPI, typename TL>
 static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
-  auto kernel = k_twin_gemm<T, OutT, EPI, TL>;
+  const bool persist = blocks < (int64_t)g.tiles_m * g.tiles_n * g.batch;
+  auto kernel = persist ? k_twin_gemm<T, OutT, EPI, TL, true> : k_twin_gemm<T, OutT, EPI, TL, false>;
   static bool attr = [&] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              TL::kLdsBytes);
+    for (auto k : {k_twin_gemm<T, OutT, EPI, TL, true>, k_twin_gemm<T, OutT, EPI, TL, false>})
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                TL::kLdsBytes);
     return true;
   }();
   (void)attr;
@@ -1093,8 +1101,12 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   g.partial = bias_grad ? static_cast<float *>(workspace) : nullptr;
   g.tiles_m = (int)tiles_m;
   g.tiles_n = (int)tiles_n;
-  static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
-  g.discard = discard ? 1 : 0;
+  // measurement aid: 1 = main loop only, 2 = the whole epilogue but no global stores
+  static const int discard = [] {
+    const char *e = getenv("PHC_GEMM_DISCARD");
+    return e ? (atoi(e) == 2 ? 2 : 1) : 0;
+  }();
+  g.discard = discard;
   // Non-temporal epilogue traffic: an output of a whole PPO minibatch (tens to hundreds of MB,
   // far past the 4 MB per-XCD L2) streams out without evicting the operand panels the other CUs
   // are still re-reading; the pre-activation (written by the forward, read back once by the backward) always does.  Small

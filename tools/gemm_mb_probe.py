@@ -16,6 +16,10 @@ phc_amd_path.register()
 from puffer_phc_amd import _native as N  # noqa: E402
 
 dev = "cuda:0"
+if os.environ.get("MAXWG"):  # persistent tile loop over this many workgroups
+    import functools
+
+    N.twin_gemm = functools.partial(N.twin_gemm, max_workgroups=int(os.environ["MAXWG"]))
 dt = torch.float16
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 DIMS = [960, 2048, 1536, 1024, 1024, 512, 512]  # padded input width, then the six layer widths
