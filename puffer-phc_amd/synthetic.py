@@ -51,3 +51,28 @@ def synthetic_clips(num_motions, min_len=60, max_len=300, seed=0, device="cuda",
     trans[:, 2] += 0.9
     fps = torch.full((num_motions,), 30.0)
     return q.contiguous(), trans.to(device).contiguous(), counts.to(device), fps.to(device)
+
+
+def standing_clips(num_motions, frames=300, height=0.94, sway=0.0, seed=0, device="cuda", key_every=30, joints=24):
+    """Clips of the humanoid standing in the upright zero pose (every global rotation the identity)
+    with its root `height` above the ground — the physics body model's rest height is 0.937 m
+    (physics.BodyModel.rest_root_height) — optionally swaying: keyframes every `key_every` frames
+    drawn within a `sway`-radian cone around the upright pose, the root fixed.  The articulated
+    physics' balance task (profiles/r03_train_articulated_standing.log).  Same outputs as
+    synthetic_clips."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    counts = torch.full((num_motions,), int(frames), dtype=torch.int64)
+    nkeys = frames // key_every + 2
+    keys = torch.zeros((num_motions, nkeys, joints, 4), dtype=torch.float64)
+    keys[..., 3] = 1.0
+    if sway > 0:
+        keys[..., :3] += torch.randn((num_motions, nkeys, joints, 3), generator=g, dtype=torch.float64) * (0.5 * sway)
+        keys /= keys.norm(dim=-1, keepdim=True)
+    t = torch.arange(frames)
+    k0 = t // key_every
+    frac = ((t % key_every).double() / key_every)[None, :, None, None]
+    q = _slerp64(keys[:, k0], keys[:, k0 + 1], frac).reshape(-1, joints, 4)
+    trans = torch.zeros((num_motions * frames, 3), dtype=torch.float64)
+    trans[:, 2] = height
+    fps = torch.full((num_motions,), 30.0)
+    return q.to(device).contiguous(), trans.to(device).contiguous(), counts.to(device), fps.to(device)

@@ -58,6 +58,14 @@ def make_motion_data(env_cfg):
 
         q, t, c, fps = synthetic_clips(env_cfg.num_envs, seed=env_cfg.seed, device=env_cfg.device)
         return PackedMotions.from_global_rotations(q, t, c, fps)
+    if isinstance(mf, str) and mf.startswith("standing:"):  # standing:<num_motions>[:<sway radians>]
+        from puffer_phc_amd.motion_lib import PackedMotions
+        from puffer_phc_amd.synthetic import standing_clips
+
+        parts = mf.split(":")
+        sway = float(parts[2]) if len(parts) > 2 else 0.0
+        q, t, c, fps = standing_clips(int(parts[1]), sway=sway, seed=env_cfg.seed, device=env_cfg.device)
+        return PackedMotions.from_global_rotations(q, t, c, fps)
     return None
 
 
@@ -83,7 +91,7 @@ def train(args, vec_env, policy):
                 eval_stats.update_env_and_close()
             vec_env.env.resample_motions()
             vec_env.reset()
-        clean_pufferl.evaluate(components, state)
+        _, env_infos = clean_pufferl.evaluate(components, state)
         rms = getattr(components.policy.policy, "update_obs_rms", None)
         if rms:
             rms(components.experience.obs)
@@ -94,8 +102,11 @@ def train(args, vec_env, policy):
             decay = max(math.exp(-cfg.lr_decay_rate * state.epoch), cfg.lr_decay_floor)
             components.optimizer.param_groups[0]["lr"] = cfg.learning_rate * decay
         if D.rank() == 0:
+            ep = {k: sum(float(x) for x in v) / len(v) for k, v in env_infos.items() if len(v)}
             print(f"epoch {state.epoch} step {state.global_step} SPS {state.profile.SPS:.0f} "
-                  f"pg {losses.policy_loss:.4f} v {losses.value_loss:.4f} kl {losses.approx_kl:.5f}", flush=True)
+                  f"pg {losses.policy_loss:.4f} v {losses.value_loss:.4f} kl {losses.approx_kl:.5f} "
+                  f"ep_len {ep.get('episode_length', float('nan')):.1f} ep_ret {ep.get('episode_return', float('nan')):.3f} "
+                  f"rew_pos {ep.get('rew_body_pos', float('nan')):.4f}", flush=True)
     if args.final_eval:
         eval_stats = EvalStats(vec_env, progress=D.rank() == 0)
         eval_rollout(vec_env, policy, eval_stats)

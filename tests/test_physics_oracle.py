@@ -257,3 +257,20 @@ def test_product_rest_state_matches_oracle(model):
     want, _ = P.rest_state(model, 1, 0.05)
     np.testing.assert_allclose(rb[:, 0, 2].numpy(), want[0, 0, 2], atol=1e-6)
     assert float(dof.abs().max()) == 0.0 and rb.shape == (3, 24, 13)
+
+
+def test_standing_clips_match_the_rest_pose(model):
+    """synthetic.standing_clips (the balance task of profiles/r03_train_articulated_*.log): without
+    sway every frame is the upright zero pose at the body model's rest height (feet on the
+    ground, not through it); with sway the rotations stay within the cone."""
+    torch = pytest.importorskip("torch")
+    from puffer_phc_amd.synthetic import standing_clips
+
+    q, t, c, fps = standing_clips(3, frames=40, device="cpu")
+    assert q.shape == (120, 24, 4) and t.shape == (120, 3) and c.tolist() == [40] * 3
+    assert torch.equal(q[..., 3], torch.ones(120, 24, dtype=torch.float64)) and float(q[..., :3].abs().max()) == 0
+    rb, _ = P.rest_state(model, 1, 0.0)
+    assert 0.0 <= float(t[0, 2]) - rb[0, 0, 2] < 0.01
+    q, t, _, _ = standing_clips(2, frames=90, sway=0.1, device="cpu")
+    ang = 2 * torch.acos(q[..., 3].abs().clamp(max=1))
+    assert 0.01 < float(ang.max()) < 0.6 and torch.equal(t[:, :2], torch.zeros(180, 2, dtype=torch.float64))
