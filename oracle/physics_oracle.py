@@ -241,12 +241,13 @@ def closest_points(p0, d1, q0, d2):
 
 
 def self_contacts(model, R, P, V, prm):
-    """Penalty self-collision between the filtered body pairs, both bodies as capsules: per ordered
-    pair (i, j) the force on i, normal stiffness x depth + damping x approach rate (>= 0), applied at
-    the middle of the overlap; a body-coordinate wrench about i's origin [E, 24, 6]."""
+    """Penalty self-collision between the filtered body pairs, both bodies as capsules: per pair
+    i < j one contact (the closest points of the two segments), normal force stiffness x depth +
+    damping x approach rate (>= 0) at the middle of the overlap, pushing i away from j and j away
+    from i (action = reaction); body-coordinate wrenches about each body's origin [E, 24, 6]."""
     n = P.shape[0]
-    pi = np.array([p[0] for p in model["pairs"]])
-    pj = np.array([p[1] for p in model["pairs"]])
+    pi = np.array([p[0] for p in model["pairs"] if p[0] < p[1]])
+    pj = np.array([p[1] for p in model["pairs"] if p[0] < p[1]])
     ends = P[:, :, None, :] + np.einsum("nbij,bkj->nbki", R, model["seg"])  # [E, 24, 2, 3] world
     W = np.einsum("nbij,nbj->nbi", R, V[..., :3])
     Vo = np.einsum("nbij,nbj->nbi", R, V[..., 3:])
@@ -264,11 +265,12 @@ def self_contacts(model, R, P, V, prm):
     vj = Vo[:, pj] + np.cross(W[:, pj], x - P[:, pj])
     vn = _dot(vi - vj, nrm)
     fm = np.where(pen > 0, np.maximum(0.0, prm["contact_stiffness"] * pen + prm["contact_damping"] * vn), 0.0)
-    Rt = np.swapaxes(R[:, pi], -1, -2)
-    Fb = np.einsum("npij,npj->npi", Rt, -fm[..., None] * nrm)
-    wrench = np.concatenate([np.cross(np.einsum("npij,npj->npi", Rt, x - P[:, pi]), Fb), Fb], -1)
     f = np.zeros((n, NUM_BODIES, 6))
-    np.add.at(f, (slice(None), pi), wrench)
+    for idx, sign in ((pi, 1.0), (pj, -1.0)):
+        Rt = np.swapaxes(R[:, idx], -1, -2)
+        Fb = np.einsum("npij,npj->npi", Rt, -sign * fm[..., None] * nrm)
+        wrench = np.concatenate([np.cross(np.einsum("npij,npj->npi", Rt, x - P[:, idx]), Fb), Fb], -1)
+        np.add.at(f, (slice(None), idx), wrench)
     return f
 
 

@@ -244,9 +244,9 @@ enum : int {
   T_KP = 22, T_KD = 25, T_DEXT = 28, T_NPTS = 31, T_PTS = 32 /* 32 */, T_IC = 64 /* 6, sym */,
   T_SEG = 70 /* p0 3, p1 3, radius */, T_MASK = 77
 };
-// per env and body, refreshed every substep for the self-collision pass: world segment end points,
-// radius, world angular velocity, world origin velocity, origin
-constexpr int kSeg = 16;
+// per env and body, refreshed every substep for the self-collision pass: bounding sphere, world
+// segment (start, direction), radius, world angular velocity, world origin velocity, origin
+constexpr int kSeg = 20;
 constexpr int kOut = 21;
 
 __device__ __forceinline__ v3 ld3(const float *p) { return {p[0], p[1], p[2]}; }
@@ -261,8 +261,15 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     PhysView e, const float *__restrict__ model, const float *__restrict__ target, PdArgs pa, PhysConsts c) {
   __shared__ float tab[kBodies * kTab];
   __shared__ float slots[kPhysEnvs][kBodies][kSlot];
-  __shared__ float outw[kPhysEnvs][kBodies][kOut];
-  __shared__ float segw[kPhysEnvs][kBodies][kSeg];
+  __shared__ __attribute__((aligned(16))) float outw[kPhysEnvs][kBodies][kOut];
+  // the self-collision records share the outward-pass operands' memory: written and read between
+  // the outward pass of one substep and the inward pass of the next (the block stays within 20 KB
+  // of LDS: 8 workgroups per CU, 2 waves per SIMD)
+  static_assert(kSeg <= kOut, "segw aliases outw");
+  float(*segw)[kBodies][kSeg] = reinterpret_cast<float(*)[kBodies][kSeg]>(&outw[0][0][0]);
+  __shared__ float fsc[kPhysEnvs][kBodies][6];  // self-contact wrench per body (world torque, force)
+  __shared__ unsigned short pairs[kBodies * (kBodies - 1) / 2];  // colliding pairs i | j << 5, i < j
+  __shared__ int npairs_s;
   const int lane = threadIdx.x % kGroup, sub = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kPhysEnvs + sub;
   const bool act = env < e.n && lane < kBodies;
@@ -306,6 +313,23 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     t[T_MASK] = c.self_col ? md[71] : 0.0f;
   }
   __syncthreads();
+  // the pair list (identical for every env): body t's partners j > t at offset = the pair counts
+  // of the bodies before it
+  if (threadIdx.x < kBodies) {
+    const int t = threadIdx.x;
+    const unsigned above = ~((2u << t) - 1u);
+    int off = 0;
+    for (int i = 0; i < t; ++i) off += __popc((unsigned)tab[i * kTab + T_MASK] & ~((2u << i) - 1u));
+    unsigned m = (unsigned)tab[t * kTab + T_MASK] & above & ((1u << kBodies) - 1u);
+    while (m) {
+      const int j = __builtin_ctz(m);
+      m &= m - 1u;
+      pairs[off++] = (unsigned short)(t | (j << 5));
+    }
+    if (t == kBodies - 1) npairs_s = off;
+  }
+  __syncthreads();
+  const int npairs = npairs_s;
   const float *T = tab + b * kTab;
   const int parent = (int)T[T_PARENT];
   const int level = act ? (int)T[T_LEVEL] : -1;
@@ -392,73 +416,89 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       v3 fn_ = cross3(com, F), ff = F;
       // per-link angular damping (PhysX linear-in-omega damping): torque -d Ic w about the com
       fn_ = vsub(fn_, vscale(m3_v(sym_full(T + T_IC), w), c.ang_damp));
-      // penalty self-collision: every pair this body's mask names, both bodies as capsules
-      const unsigned mask = (unsigned)T[T_MASK];
+      // penalty self-collision over the pair list, both bodies as capsules
       if (c.self_col) {  // grid-uniform: the barriers below are reached by every wave
-        const v3 s0 = m3_v(R, ld3(T + T_SEG)), s1 = m3_v(R, ld3(T + T_SEG + 3));
-        const v3 p0w = vadd(P, s0), p1w = vadd(P, s1);
-        const float rb = T[T_SEG + 6];
-        const v3 ww = m3_v(R, w), vw0 = m3_v(R, v);
         float *sw = segw[sub][b];
         if (act) {
-        sw[0] = p0w.x; sw[1] = p0w.y; sw[2] = p0w.z; sw[3] = p1w.x; sw[4] = p1w.y; sw[5] = p1w.z; sw[6] = rb;
-        sw[7] = ww.x; sw[8] = ww.y; sw[9] = ww.z; sw[10] = vw0.x; sw[11] = vw0.y; sw[12] = vw0.z;
-        sw[13] = P.x; sw[14] = P.y; sw[15] = P.z;
+          const v3 s0 = m3_v(R, ld3(T + T_SEG)), s1 = m3_v(R, ld3(T + T_SEG + 3));
+          const v3 p0w = vadd(P, s0), d1 = vsub(s1, s0);
+          const float rb = T[T_SEG + 6];
+          const v3 ww = m3_v(R, w), vw0 = m3_v(R, v);
+          // [0, 4): bounding sphere (centre, radius) for the broad phase; then the segment (start,
+          // direction), the radius, the world twist and the origin for the narrow phase
+          sw[0] = p0w.x + 0.5f * d1.x; sw[1] = p0w.y + 0.5f * d1.y; sw[2] = p0w.z + 0.5f * d1.z;
+          sw[3] = 0.5f * sqrtf(d1.x * d1.x + d1.y * d1.y + d1.z * d1.z) + rb;
+          sw[4] = p0w.x; sw[5] = p0w.y; sw[6] = p0w.z; sw[7] = d1.x; sw[8] = d1.y; sw[9] = d1.z; sw[10] = rb;
+          sw[11] = ww.x; sw[12] = ww.y; sw[13] = ww.z; sw[14] = vw0.x; sw[15] = vw0.y; sw[16] = vw0.z;
+          sw[17] = P.x; sw[18] = P.y; sw[19] = P.z;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) fsc[sub][b][k] = 0.0f;
         }
         __syncthreads();
-        const v3 mid = vscale(vadd(p0w, p1w), 0.5f);
-        const v3 d1 = vsub(p1w, p0w);
-        const float hb = 0.5f * sqrtf(d1.x * d1.x + d1.y * d1.y + d1.z * d1.z) + rb;
-        for (int j = 0; j < kBodies; ++j) {
-          if (!act || !((mask >> j) & 1u)) continue;
-          const float *o = segw[sub][j];
-          const v3 q0 = ld3(o), q1 = ld3(o + 3);
-          const float rj = o[6];
-          const v3 d2 = vsub(q1, q0);
-          const v3 mj = vscale(vadd(q0, q1), 0.5f);
-          const float hj = 0.5f * sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z) + rj;
-          const v3 dm = vsub(mj, mid);
-          if (dm.x * dm.x + dm.y * dm.y + dm.z * dm.z > (hb + hj) * (hb + hj)) continue;
-          // closest points of the two segments (clamped parameters s, t)
-          const v3 r0 = vsub(p0w, q0);
-          const float a = d1.x * d1.x + d1.y * d1.y + d1.z * d1.z, e = d2.x * d2.x + d2.y * d2.y + d2.z * d2.z;
-          const float f = d2.x * r0.x + d2.y * r0.y + d2.z * r0.z;
-          float sp = 0.0f, tp = 0.0f;
-          if (a > 1e-12f && e > 1e-12f) {
-            const float cc = d1.x * r0.x + d1.y * r0.y + d1.z * r0.z;
-            const float bb = d1.x * d2.x + d1.y * d2.y + d1.z * d2.z;
-            const float den = a * e - bb * bb;
-            sp = den > 1e-12f ? fminf(fmaxf((bb * f - cc * e) / den, 0.0f), 1.0f) : 0.0f;
-            tp = (bb * sp + f) / e;
-            if (tp < 0.0f) {
-              tp = 0.0f;
-              sp = fminf(fmaxf(-cc / a, 0.0f), 1.0f);
-            } else if (tp > 1.0f) {
-              tp = 1.0f;
-              sp = fminf(fmaxf((bb - cc) / a, 0.0f), 1.0f);
+        // each of the env's 32 lanes takes every 32nd pair: broad phase on the bounding spheres,
+        // narrow phase (clamped segment-segment closest points) on the overlapping ones, the
+        // equal and opposite contact forces added into both bodies' LDS wrench slots (world
+        // force, world torque about the body origin)
+        if (env < e.n) {
+          for (int q = lane; q < npairs; q += kGroup) {
+            const int pr = pairs[q], bi = pr & 31, bj = pr >> 5;
+            const float *oi = segw[sub][bi], *oj = segw[sub][bj];
+            const float4 bsi = *reinterpret_cast<const float4 *>(oi), bsj = *reinterpret_cast<const float4 *>(oj);
+            const float bx = bsj.x - bsi.x, by = bsj.y - bsi.y, bz = bsj.z - bsi.z, br = bsi.w + bsj.w;
+            if (bx * bx + by * by + bz * bz > br * br) continue;
+            const v3 p0 = ld3(oi + 4), d1 = ld3(oi + 7), q0 = ld3(oj + 4), d2 = ld3(oj + 7);
+            const float ri = oi[10], rj = oj[10];
+            const v3 r0 = vsub(p0, q0);
+            const float a = d1.x * d1.x + d1.y * d1.y + d1.z * d1.z, ee = d2.x * d2.x + d2.y * d2.y + d2.z * d2.z;
+            const float f = d2.x * r0.x + d2.y * r0.y + d2.z * r0.z;
+            float sp = 0.0f, tp = 0.0f;
+            if (a > 1e-12f && ee > 1e-12f) {
+              const float cc = d1.x * r0.x + d1.y * r0.y + d1.z * r0.z;
+              const float bb = d1.x * d2.x + d1.y * d2.y + d1.z * d2.z;
+              const float den = a * ee - bb * bb;
+              sp = den > 1e-12f ? fminf(fmaxf((bb * f - cc * ee) / den, 0.0f), 1.0f) : 0.0f;
+              tp = (bb * sp + f) / ee;
+              if (tp < 0.0f) {
+                tp = 0.0f;
+                sp = fminf(fmaxf(-cc / a, 0.0f), 1.0f);
+              } else if (tp > 1.0f) {
+                tp = 1.0f;
+                sp = fminf(fmaxf((bb - cc) / a, 0.0f), 1.0f);
+              }
+            } else if (a > 1e-12f) {
+              sp = fminf(fmaxf(-(d1.x * r0.x + d1.y * r0.y + d1.z * r0.z) / a, 0.0f), 1.0f);
+            } else if (ee > 1e-12f) {
+              tp = fminf(fmaxf(f / ee, 0.0f), 1.0f);
             }
-          } else if (a > 1e-12f) {
-            sp = fminf(fmaxf(-(d1.x * r0.x + d1.y * r0.y + d1.z * r0.z) / a, 0.0f), 1.0f);
-          } else if (e > 1e-12f) {
-            tp = fminf(fmaxf(f / e, 0.0f), 1.0f);
+            const v3 c1 = vadd(p0, vscale(d1, sp)), c2 = vadd(q0, vscale(d2, tp));
+            const v3 dd = vsub(c2, c1);
+            const float dist = sqrtf(dd.x * dd.x + dd.y * dd.y + dd.z * dd.z);
+            const float pen = ri + rj - dist;
+            if (pen <= 0.0f) continue;
+            const v3 nrm = dist > 1e-6f ? vscale(dd, 1.0f / dist) : v3{0.0f, 0.0f, 1.0f};
+            const v3 x = vadd(c1, vscale(nrm, ri - 0.5f * pen));  // the contact point (mid overlap)
+            const v3 xi = vsub(x, ld3(oi + 17)), xj = vsub(x, ld3(oj + 17));
+            const v3 vi = vadd(ld3(oi + 14), cross3(ld3(oi + 11), xi));
+            const v3 vj = vadd(ld3(oj + 14), cross3(ld3(oj + 11), xj));
+            const v3 vr = vsub(vi, vj);
+            const float vn = vr.x * nrm.x + vr.y * nrm.y + vr.z * nrm.z;  // approach rate
+            const float fm = fmaxf(0.0f, c.kn * pen + c.cn * vn);
+            const v3 Fi = vscale(nrm, -fm);  // pushes i away from j; j gets -Fi
+            const v3 ti = cross3(xi, Fi), tj = cross3(xj, Fi);
+            float *wi = fsc[sub][bi], *wj = fsc[sub][bj];
+            atomicAdd(wi + 0, ti.x); atomicAdd(wi + 1, ti.y); atomicAdd(wi + 2, ti.z);
+            atomicAdd(wi + 3, Fi.x); atomicAdd(wi + 4, Fi.y); atomicAdd(wi + 5, Fi.z);
+            atomicAdd(wj + 0, -tj.x); atomicAdd(wj + 1, -tj.y); atomicAdd(wj + 2, -tj.z);
+            atomicAdd(wj + 3, -Fi.x); atomicAdd(wj + 4, -Fi.y); atomicAdd(wj + 5, -Fi.z);
           }
-          const v3 c1 = vadd(p0w, vscale(d1, sp)), c2 = vadd(q0, vscale(d2, tp));
-          const v3 dd = vsub(c2, c1);
-          const float dist = sqrtf(dd.x * dd.x + dd.y * dd.y + dd.z * dd.z);
-          const float pen = rb + rj - dist;
-          if (pen <= 0.0f) continue;
-          const v3 nrm = dist > 1e-6f ? vscale(dd, 1.0f / dist) : v3{0.0f, 0.0f, 1.0f};
-          const v3 x = vadd(c1, vscale(nrm, rb - 0.5f * pen));  // the contact point (mid penetration)
-          const v3 vb = vadd(vw0, cross3(ww, vsub(x, P)));
-          const v3 vj = vadd(ld3(o + 10), cross3(ld3(o + 7), vsub(x, ld3(o + 13))));
-          const v3 vr = vsub(vb, vj);
-          const float vn = vr.x * nrm.x + vr.y * nrm.y + vr.z * nrm.z;  // penetration rate
-          const float fm = fmaxf(0.0f, c.kn * pen + c.cn * vn);
-          const v3 Fb = m3_tv(R, vscale(nrm, -fm));  // pushes this body away from the partner
-          fn_ = vadd(fn_, cross3(m3_tv(R, vsub(x, P)), Fb));
-          ff = vadd(ff, Fb);
         }
-        __syncthreads();  // segw is rewritten next substep
+        __syncthreads();
+        if (act) {  // this body's accumulated contact wrench, to body coordinates
+          const float *ws = fsc[sub][b];
+          fn_ = vadd(fn_, m3_tv(R, ld3(ws)));
+          ff = vadd(ff, m3_tv(R, ld3(ws + 3)));
+        }
+        __syncthreads();  // segw / fsc are rewritten next substep
       }
       const v3 zb = {R.m[6], R.m[7], R.m[8]};  // R^T z
       const int npts = (int)T[T_NPTS];
