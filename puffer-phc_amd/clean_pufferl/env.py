@@ -76,12 +76,17 @@ class PHCPufferEnv:
     def step(self, actions):
         if isinstance(actions, np.ndarray):
             self.actions.copy_(torch.from_numpy(actions))
-        elif actions.data_ptr() != self.actions.data_ptr():
+            actions = self.actions
+        elif not (actions.is_cuda == self.actions.is_cuda and actions.dtype == torch.float32
+                  and actions.is_contiguous() and tuple(actions.shape) == tuple(self.actions.shape)):
             self.actions.copy_(actions)
-        # clipping happens inside phc_actions_to_pd (cfg.clip_actions is always honoured);
-        # the fused kernel also performs the env.reset(reset_indices) of :114-116, which leaves
-        # rew_buf untouched, so no defensive copy of the rewards is needed
-        self.env.step(self.actions, auto_reset=True)
+            actions = self.actions
+        # a device float32 [N, 69] tensor is read in place by the step kernel (the reference's
+        # `self.actions[:] = actions` copy, clean_pufferl/env.py, is a 1.1 MB device copy per step
+        # with no other reader); clipping happens inside the action -> PD map (cfg.clip_actions
+        # is always honoured); the fused kernel also performs the env.reset(reset_indices) of
+        # :114-116, which leaves rew_buf untouched, so no defensive copy of the rewards is needed
+        self.env.step(actions, auto_reset=True)
         rew = self.rewards
         self.amp_obs = self.env.amp_obs if self.cfg.use_amp_obs else None
         info = []
