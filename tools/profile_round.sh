@@ -32,8 +32,9 @@ done
 # HBM bytes per launch (+ the trace's mean duration) of the same launches bench.py times
 python tools/pmc_summary.py "$O/pmc_gemm_FETCH_SIZE" "$O/pmc_gemm_WRITE_SIZE" train_gemm "$O/traffic_gemm_4096.json" "$O/trace_ppo"
 for E in 4096 32768; do
-  python tools/pmc_summary.py "$O/pmc_env_${E}_FETCH_SIZE" "$O/pmc_env_${E}_WRITE_SIZE" k_env_step "$O/traffic_$E.json" \
-    "$O/trace_env_$E" $((10886 * E))
+  # the default env phase is the fused replay step (phc_env_step_replay: k_env_step<true, true>)
+  python tools/pmc_summary.py "$O/pmc_env_${E}_FETCH_SIZE" "$O/pmc_env_${E}_WRITE_SIZE" k_env_step "$O/traffic_fused_$E.json" \
+    "$O/trace_env_$E" $((11714 * E))
 done
 # the AMP + bf16 configuration (BASELINE C5): kernel stats, to show which kernels the discriminator runs on
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/trace_ppo_amp_bf16" -o run --output-format csv -- \
