@@ -238,10 +238,7 @@ __global__ __launch_bounds__(kActThreads) void k_policy_act(phc_policy_act_args 
   if (active) {
     const float *w = a.w_mu + (int64_t)j * H + kh * (H / 2);
     const float *h0 = &hs[4 * g][kh * (H / 2)];
-#pragma unroll 8
-    for (int kk = 0; kk < H / 2; kk += 4) {
-      float4 wv;  // W_mu may be a view into a flat parameter buffer: 4-byte alignment only
-      wv.x = w[kk]; wv.y = w[kk + 1]; wv.z = w[kk + 2]; wv.w = w[kk + 3];
+    auto step = [&](int kk, float4 wv) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float4 h = *reinterpret_cast<const float4 *>(h0 + r * H + kk);
@@ -250,6 +247,13 @@ __global__ __launch_bounds__(kActThreads) void k_policy_act(phc_policy_act_args 
         acc[r] += h.z * wv.z;
         acc[r] += h.w * wv.w;
       }
+    };
+    if ((reinterpret_cast<uintptr_t>(a.w_mu) & 15) == 0) {  // the aligned copy: one dwordx4 per step
+#pragma unroll 8
+      for (int kk = 0; kk < H / 2; kk += 4) step(kk, *reinterpret_cast<const float4 *>(w + kk));
+    } else {  // a view into a flat parameter buffer: 4-byte alignment only
+#pragma unroll 8
+      for (int kk = 0; kk < H / 2; kk += 4) step(kk, float4{w[kk], w[kk + 1], w[kk + 2], w[kk + 3]});
     }
     if (kh == 1) {
 #pragma unroll

@@ -10,7 +10,7 @@ from torch import nn
 from .discriminator_policy import DiscriminatorPolicy
 from .pufferl_policy import Linear, layer_init
 from .. import _native as N
-from .twin_mlp import (TwinWeights, half_input_width, head_linear, twin_ln_silu, twin_ln_silu_supported,
+from .twin_mlp import (TwinWeights, _use_mfma, half_input_width, head_linear, twin_ln_silu, twin_ln_silu_supported,
                        twin_trunks)
 
 
@@ -38,6 +38,7 @@ class PHCPolicy(DiscriminatorPolicy):
         self.fused = True
         self.fused_ln = True  # LayerNorm + SiLU of both trunks in one kernel (False: torch modules)
         self._critic_trunk = None
+        self._w_mu_aligned = None  # registered on the device by the first act_rollout
 
     def grad_ready_order(self):
         """Parameters in the order the fused minibatch backward finishes their gradients (the
@@ -83,10 +84,17 @@ class PHCPolicy(DiscriminatorPolicy):
         xc = self.obs_half_input(obs)
         if xc is None:
             return False
-        y = twin_trunks(xc, self._twin)
+        w = self.mu[0].weight
+        if self._w_mu_aligned is None or self._w_mu_aligned.device != w.device:
+            self._twin.extras = [(p, d) for p, d in self._twin.extras if p is not w]
+            self._w_mu_aligned = self._twin.add_extra(w)
+        y = twin_trunks(xc, self._twin)  # refreshes the MFMA operands and the aligned mu weight
         la, lc = self.actor_mlp[h], self.critic_mlp[h]
         vh, mh = self.critic_mlp[h + 2], self.mu[0]
-        N.policy_act(y, (la.weight, la.bias), (lc.weight, lc.bias), la.eps, mh.weight, mh.bias, vh.weight, vh.bias,
+        # the mu weight's aligned copy, refreshed with the trunk operands by twin_trunks above (or
+        # refresh_twin before a graph replay); the plain parameter on other paths
+        w_mu = self._w_mu_aligned if _use_mfma(self._twin, xc.dtype) else mh.weight
+        N.policy_act(y, (la.weight, la.bias), (lc.weight, lc.bias), la.eps, w_mu, mh.bias, vh.weight, vh.bias,
                      self.sigma, noise, actions, logprob, value, mu=mu,
                      std_max=1e-6 if self._deterministic_action is True else float("inf"))
         return True

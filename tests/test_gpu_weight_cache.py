@@ -164,12 +164,15 @@ def test_rollout_graph_sees_optimizer_updates():
     with torch.cuda.graph(graph):
         body()
     graph.replay()
-    v0 = val.clone()
+    v0, a0 = val.clone(), act.clone()
     fg.flat.copy_(torch.randn(fg.flat.shape, device=DEV))
     opt.fused_step(1e9)
     twin_mlp.refresh_twin(inner._twin, torch.float16)  # what RolloutStep.run does before a replay
     graph.replay()
-    v1 = val.clone()
+    v1, a1 = val.clone(), act.clone()
     body()
-    assert not torch.equal(v0, v1)
-    assert torch.equal(v1, val)
+    assert not torch.equal(v0, v1) and not torch.equal(a0, a1)
+    assert torch.equal(v1, val) and torch.equal(a1, act)
+    # the mu head reads its 16-B aligned copy (float4 loads), refreshed with the trunk operands
+    assert inner._w_mu_aligned.data_ptr() % 16 == 0
+    assert torch.equal(inner._w_mu_aligned, inner.mu[0].weight.detach())
