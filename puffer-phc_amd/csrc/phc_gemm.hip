@@ -332,6 +332,20 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
   }
 }
 
+// Grad epilogues (SiLU' / ReLU' with a half-precision aux) of 256 x 256 tiles stage the aux
+// (pre-activation) rows through LDS: the rows of epilogue passes 0-2 move by LDS-DMA during the
+// last K-step (into the operand buffer that step does not read and the 32 KB above the operand
+// buffers), those of pass 3 during pass 1; the image then takes four 64-KB passes.  The epilogue
+// reads aux from LDS instead of waiting on HBM round trips per row batch.
+template <int EPI, typename TL, typename OutT> struct EpStage {
+  static constexpr bool kOn = (EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD) && TL::BM == 256 && TL::BN == 256 &&
+                              TL::STAGES == 2 && TL::BK == 64 && TL::kWaves == 8 && sizeof(OutT) == 2;
+  static constexpr int kPasses = kOn ? 4 : TL::kEpPasses;
+  static constexpr int kSlotBytes = 64 * 256 * 2;  // one pass's aux rows: 64 x 256 half-precision values
+  static constexpr int kLdsBytes = kOn ? TL::kOpBytes + kSlotBytes : TL::kLdsBytes;
+  static_assert(!kOn || TL::kOpBytes + kSlotBytes <= 163840, "LDS");
+};
+
 // One output tile: main loop + fused epilogue.  `wg` is the tile's linear index (n fastest within
 // an A panel, then m, then batch); smem holds the operand stages and, after the main loop, the
 // epilogue image.
@@ -349,6 +363,33 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   const int n0 = tn * BN;
   const char *A = g.a + bt * g.a_bs * 2;
   const char *B = g.b + bt * g.b_bs * 2;
+  using ES = EpStage<EPI, TL, OutT>;
+  constexpr int EP = ES::kPasses, WR = TL::TM / EP;
+  const int kt_last = (g.k / TL::BK - 1) & 1;  // the operand buffer the last K-step reads
+  const bool stage_aux = ES::kOn && g.aux_half && g.tc % BN == 0 && g.n % BN == 0 && m0 + BM <= g.m;
+  // aux slot s: the halves of the buffer the last K-step does not read, then the spare 32 KB
+  auto aux_slot = [&](int sl) -> char * {
+    return sl < 2 ? smem + (kt_last ^ 1) * TL::kStageBytes + sl * ES::kSlotBytes : smem + TL::kOpBytes;
+  };
+  // LDS-DMA of pass p's 64 aux rows (512 B each, image-row order) into a slot: wave-instruction i
+  // moves rows 2i, 2i + 1; 4 per wave
+  auto stage_aux_pass = [&](int p, char *slot) {
+    if constexpr (ES::kOn) {
+      const int64_t lc0 = (int64_t)bt * g.n + n0;
+      const bool split = g.aux_layout == PHC_LAYOUT_SPLIT;
+      const int64_t base0 = split ? lc0 : (lc0 / g.tc) * g.m * g.tc + lc0 % g.tc;
+      const int64_t stride = split ? (int64_t)g.tg * g.tc : g.tc;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = wave * 4 + u;
+        const int rr = 2 * i + (lane >> 5);
+        const int64_t tr = m0 + (rr / WR) * TL::TM + p * WR + rr % WR;
+        const T *src = static_cast<const T *>(g.aux) + base0 + tr * stride + (lane & 31) * 8;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (lds_void *)(slot + i * 1024), 16, 0, 0);
+      }
+    }
+  };
 
   f4 acc[MI][NI];
 #pragma unroll
@@ -369,6 +410,11 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
     stage(0, smem);
     for (int kt = 0; kt < kt_n; ++kt) {
       dma_barrier();  // tile kt landed; buffer (kt+1)&1 is no longer read
+      if (stage_aux && kt == kt_n - 1) {  // nothing else to stage: the epilogue's aux rows
+        stage_aux_pass(0, aux_slot(0));
+        stage_aux_pass(1, aux_slot(1));
+        stage_aux_pass(2, aux_slot(2));
+      }
       gemm_step<T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt + 1 < kt_n,
                        stage, kt + 1, wave, lane, acc);
     }
@@ -414,8 +460,10 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   constexpr int VW = sizeof(OutT) == 2 ? PHC_GEMM_EPI_VW : 4;
   static_assert(VW == 4 || VW == 8, "4 or 8 columns per thread");
   constexpr int kColThreads = BN / VW, kRowGroups = TL::kThreads / kColThreads;
-  constexpr int WR = TL::kEpWaveRows, IT = TL::kEpRows / kRowGroups;
-  float *ep = reinterpret_cast<float *>(smem);
+  constexpr int kEpRows = BM / EP, kEpMI = MI / EP, IT = kEpRows / kRowGroups;
+  static_assert(MI % EP == 0 && kEpRows * BN * 4 <= TL::kOpBytes, "epilogue passes");
+  static_assert(!ES::kOn || kEpRows * BN * 4 <= TL::kStageBytes, "a staged-aux image pass fits one operand buffer");
+  float *ep = reinterpret_cast<float *>(smem + (stage_aux ? kt_last * TL::kStageBytes : 0));
   const int cv = (tid % kColThreads) * VW, rg = tid / kColThreads;
   const int gcol = n0 + cv;
   const bool vec = gcol + VW - 1 < g.n && g.tc % VW == 0;
@@ -474,20 +522,28 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
     }
   };
 #pragma unroll
-  for (int pass = 0; pass < TL::kEpPasses; ++pass) {
-    if (full && pipe) load_raw(pass, 0);
-    lds_barrier();  // operand tiles / the previous pass's image are no longer read
+  for (int pass = 0; pass < EP; ++pass) {
+    if (full && pipe && !stage_aux) load_raw(pass, 0);
+    lds_barrier();  // operand tiles / the previous pass's image (and aux slot) are no longer read
+    if (stage_aux && pass == 1) stage_aux_pass(3, aux_slot(0));  // pass 0's slot is free
 #pragma unroll
-    for (int i = pass * TL::kEpMI; i < (pass + 1) * TL::kEpMI; ++i)
+    for (int i = pass * kEpMI; i < (pass + 1) * kEpMI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int r = wm * WR + (i - pass * TL::kEpMI) * 16 + 4 * (lane >> 4) + e;
+          const int r = wm * WR + (i - pass * kEpMI) * 16 + 4 * (lane >> 4) + e;
           const int c = wn * TL::TN + j * 16 + (lane & 15);
           ep[r * BN + (c ^ (((r >> 2) & 3) << 4))] = acc[i][j][e];
         }
+    if (stage_aux) {
+      // this wave's aux DMA for the pass has landed (all waves' after the barrier): passes 0-2 were
+      // issued in the last K-step; pass 3's in pass 1, before the 2 x IT stores of passes 1 and 2
+      if (pass == 0 || g.discard) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (pass == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * IT) : "memory");
+    }
     lds_barrier();
+    const char *aux_lds = stage_aux ? aux_slot(pass == 3 ? 0 : pass) : nullptr;
     if (full) {
       // whole tile in range, VW whole columns per thread: offsets are base + row * stride, rows
       // in batches of U; a half-precision aux is software-pipelined (batch b + 1's loads in
@@ -496,7 +552,17 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
       for (int i0 = 0; i0 < IT; i0 += U) {
         float av[U][VW];
         if constexpr (kGrad) {
-          if (pipe) {
+          if (stage_aux) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int r = rg + kRowGroups * (i0 + u);
+              T h[VW];
+              const uint4 q4 = *reinterpret_cast<const uint4 *>(aux_lds + r * (BN * 2) + cv * 2);
+              __builtin_memcpy(h, &q4, sizeof(h));
+#pragma unroll
+              for (int q = 0; q < VW; ++q) av[u][q] = (float)h[q];
+            }
+          } else if (pipe) {
             if (i0 + U < IT) load_raw(pass, i0 / U + 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -962,17 +1028,17 @@ template <typename T, typename OutT, int EPI, typename TL>
 static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
   const bool persist = blocks < (int64_t)g.tiles_m * g.tiles_n * g.batch;
   auto kernel = persist ? k_twin_gemm<T, OutT, EPI, TL, true> : k_twin_gemm<T, OutT, EPI, TL, false>;
+  constexpr int lds = EpStage<EPI, TL, OutT>::kLdsBytes;
   static bool attr = [&] {
     for (auto k : {k_twin_gemm<T, OutT, EPI, TL, true>, k_twin_gemm<T, OutT, EPI, TL, false>})
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                TL::kLdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     return true;
   }();
   (void)attr;
   if (g_ev0)
-    hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g_ev0, g_ev1, 0, g);
+    hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), lds, st, g_ev0, g_ev1, 0, g);
   else
-    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), lds, st, g);
 }
 
 template <typename T, typename OutT, int EPI>
