@@ -79,10 +79,12 @@ def create(exp_id, train_cfg, env_cfg, vecenv, policy, optimizer=None, wandb=Non
     vecenv.async_reset(train_cfg.seed)
     obs_shape = vecenv.single_observation_space.shape
     atn_shape = vecenv.single_action_space.shape
+    lstm = getattr(policy, "lstm", None)  # RecurrentPolicy: per-env (h, c) buffers (core.py:66-77)
     experience = Experience(train_cfg.batch_size, train_cfg.bptt_horizon, train_cfg.minibatch_size, obs_shape,
                             atn_shape=atn_shape, device=train_cfg.device, use_amp_obs=env_cfg.use_amp_obs,
                             amp_obs_size=getattr(vecenv.amp_observation_space, "shape", (1960,))[0]
-                            if env_cfg.use_amp_obs else 1960)
+                            if env_cfg.use_amp_obs else 1960, lstm=lstm,
+                            lstm_total_agents=vecenv.num_agents if lstm is not None else 0)
     D.broadcast_params(policy)
     uncompiled_policy = policy
     if train_cfg.compile:
@@ -291,8 +293,19 @@ def evaluate(components, info):
             with profile.eval_misc:
                 n_valid = int(mask.sum().item())
                 local_steps += n_valid
-            with profile.eval_forward, torch.no_grad(), autocast(train_cfg):
-                actions, logprob, _, value = policy(o)
+            if experience.lstm_h is not None:  # recurrent policies, in fp32 (core.py:149-160)
+                with profile.eval_forward, torch.no_grad():
+                    lstm_h, lstm_c = experience.lstm_h, experience.lstm_c
+                    reset = torch.logical_or(d.bool(), t.bool())  # zero the state of envs that reset
+                    if bool(reset.any()):
+                        lstm_h[:, env_id[reset]] = 0
+                        lstm_c[:, env_id[reset]] = 0
+                    actions, logprob, _, value, (h, c) = policy(o, (lstm_h[:, env_id], lstm_c[:, env_id]))
+                    lstm_h[:, env_id] = h
+                    lstm_c[:, env_id] = c
+            else:
+                with profile.eval_forward, torch.no_grad(), autocast(train_cfg):
+                    actions, logprob, _, value = policy(o)
             with profile.eval_misc:
                 amp_obs = components.vecenv.amp_obs if info.use_amp_obs else None
                 experience.store(o, amp_obs, value.flatten(), actions, logprob, r, d, t, env_id, mask, n_valid)
@@ -377,7 +390,9 @@ def train(components, info, utilization=None):
         fused_loss = (cfg.fused_loss and hasattr(pol, "forward_train") and getattr(pol, "fused", False)
                       and experience.lstm_h is None)
         obs_dim = components.vecenv.single_observation_space.shape[0]
+        recurrent = experience.lstm_h is not None
         for _epoch in range(cfg.update_epochs):
+            lstm_state = None  # each epoch's minibatches carry (h, c) from one to the next (core.py:268)
             for mb in range(experience.num_minibatches):
                 with profile.train_misc:
                     if experience.b_obs_half is not None:
@@ -392,8 +407,13 @@ def train(components, info, utilization=None):
                     ret = experience.b_returns[mb]
                 fused_obj = fused_loss and obs.is_cuda
                 fused_mb = False
-                with profile.train_forward, autocast(cfg):
-                    if fused_obj and fused_ppo_supported(pol, obs):
+                with profile.train_forward, (contextlib.nullcontext() if recurrent else autocast(cfg)):
+                    if recurrent:
+                        # [minibatch_rows, bptt, obs] segments through the LSTM (core.py:287-289)
+                        _, newlogprob, entropy, newvalue, lstm_state = components.policy(
+                            experience.b_obs[mb], info=lstm_state, action=experience.b_actions[mb])
+                        lstm_state = (lstm_state[0].detach(), lstm_state[1].detach())
+                    elif fused_obj and fused_ppo_supported(pol, obs):
                         # the whole minibatch (trunks + LayerNorm/heads + PPO objective) as one
                         # autograd node (policies/fused_ppo.py)
                         fused_mb = True

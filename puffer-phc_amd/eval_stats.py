@@ -247,15 +247,28 @@ def eval_rollout(vec_env, policy, eval_stats, max_steps=None):
     pol.set_deterministic_action(True)
     obs, _ = vec_env.reset()
     steps = 0
+    recurrent = hasattr(policy, "lstm")
+    state = None
     try:
         while max_steps is None or steps < max_steps:
             with torch.no_grad():
-                action, _, _, _ = policy(obs)
-            obs, _, _, _, _ = vec_env.step(action)
+                if recurrent:  # the LSTM state carried per env, zeroed on reset (train.py:398-415)
+                    action, _, _, _, state = policy(obs, state)
+                else:
+                    action, _, _, _ = policy(obs)
+            obs, _, done, trunc, _ = vec_env.step(action)
             steps += 1
-            done, _ = eval_stats.post_step_eval()
+            if recurrent:
+                reset = torch.logical_or(done.bool(), trunc.bool())
+                if bool(reset.any()):
+                    state[0][:, reset] = 0
+                    state[1][:, reset] = 0
+            done, next_batch = eval_stats.post_step_eval()
             if done:
                 break
+            if recurrent and next_batch and state is not None:
+                state[0].zero_()
+                state[1].zero_()
     finally:
         pol.set_deterministic_action(False)
     return steps

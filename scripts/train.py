@@ -70,10 +70,22 @@ def make_motion_data(env_cfg):
 
 
 def make_policy(env, args):
-    if args.policy_name != "PHCPolicy" or args.rnn_name:
-        raise NotImplementedError("LSTM policies are out of scope (README: they did not help)")
-    return Policy(PHCPolicy(env, hidden_size=args.policy.hidden_size, layer_sizes=args.policy.layer_sizes)).to(
-        args.train.device)
+    """scripts/train.py:259-272: PHCPolicy (the fused MFMA path) or an LSTM policy, optionally under
+    the Recurrent wrapper (`--policy-name LSTMCriticPolicy --rnn-name Recurrent`)."""
+    from puffer_phc_amd import policies
+
+    if args.policy_name == "PHCPolicy":
+        inner = PHCPolicy(env, hidden_size=args.policy.hidden_size, layer_sizes=args.policy.layer_sizes)
+    elif args.policy_name in ("LSTMCriticPolicy", "LSTMActorPolicy"):
+        inner = getattr(policies, args.policy_name)(env, hidden_size=args.policy.hidden_size)
+    else:
+        raise ValueError(f"unknown policy {args.policy_name!r} (PHCPolicy | LSTMCriticPolicy | LSTMActorPolicy)")
+    if args.rnn_name:
+        if args.rnn_name != "Recurrent":
+            raise ValueError(f"unknown rnn {args.rnn_name!r} (Recurrent)")
+        rnn = policies.Recurrent(env, inner, input_size=args.rnn.input_size, hidden_size=args.rnn.hidden_size)
+        return policies.RecurrentPolicy(rnn).to(args.train.device)
+    return Policy(inner).to(args.train.device)
 
 
 def train(args, vec_env, policy):
@@ -91,6 +103,10 @@ def train(args, vec_env, policy):
                 eval_stats.update_env_and_close()
             vec_env.env.resample_motions()
             vec_env.reset()
+            exp = components.experience
+            if exp.lstm_h is not None:  # reset the envs and the LSTM hidden states (train.py:329-333)
+                exp.lstm_h.zero_()
+                exp.lstm_c.zero_()
         _, env_infos = clean_pufferl.evaluate(components, state)
         rms = getattr(components.policy.policy, "update_obs_rms", None)
         if rms:
@@ -138,10 +154,18 @@ def evaluate_policy(vec_env, policy, out_prefix="eval"):
 def rollout(vec_env, policy, steps=1000):
     policy.policy.set_deterministic_action(True)
     obs, _ = vec_env.reset()
+    state = None
     for _ in range(steps):
         with torch.no_grad():
-            action, _, _, _ = policy(obs)
+            if hasattr(policy, "lstm"):
+                action, _, _, _, state = policy(obs, state)
+            else:
+                action, _, _, _ = policy(obs)
         obs, _, done, trunc, info = vec_env.step(action)
+        if state is not None:
+            reset = torch.logical_or(done.bool(), trunc.bool())
+            state[0][:, reset] = 0
+            state[1][:, reset] = 0
         if info:
             print(info[0])
     policy.policy.set_deterministic_action(False)
