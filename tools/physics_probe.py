@@ -18,7 +18,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 dev = "cuda:0"
 bm = BodyModel(device=dev)
-phys = ArticulatedPhysics(PhysicsConfig(), model=bm)
+phys = ArticulatedPhysics(PhysicsConfig(self_collision=os.environ.get("PHC_SELF_COL", "1") == "1"), model=bm)
 rb_t, dof_t = rest_state(bm, n, 0.0, device=dev)
 rb_t[:, 0, 0] += torch.arange(n, device=dev, dtype=torch.float32) * 2.0
 rng = np.random.default_rng(0)
