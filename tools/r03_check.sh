@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round-3 GPU pass: store-pattern probe, GEMM A/B of two library builds, GEMM tests, full GPU suite + bench.
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$ROOT"; O=$ROOT/gpurun_out; mkdir -p "$O"
+timeout -k 10 60 ./tools/store_probe 256 > "$O/store_probe.log" 2>&1 || { echo "store_probe failed"; exit 3; }
+ROUNDS=2 VARIANTS="libphc_hip_lds.so libphc_hip_fwd.so libphc_hip.so" bash tools/lib_ab.sh || exit 4
+timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_twin_mlp.py -x -q --timeout 120 --timeout-method thread > "$O/pytest_gemm.log" 2>&1
+rc=$?; echo "gemm tests rc=$rc"; tail -5 "$O/pytest_gemm.log"; [ $rc -eq 0 ] || exit 5
+TESTS=1 PROFILE=0 MODES=ppo bash tools/gpu_check.sh

@@ -23,6 +23,29 @@ __global__ __launch_bounds__(512) void k_store(uint4 *out, int64_t row_stride_16
     }
     return;
   }
+  if (nt >= 4) {  // the register-direct epilogue's pattern over 256 x 256 f16 tile images (8 waves of 128 x 64)
+    const int lane = tid & 63, w = tid >> 6, wm = w / 4, wn = w % 4;
+    for (int img = 0; img < rows_per_block / 256; ++img) {
+      const int64_t r0 = (int64_t)blockIdx.x * rows_per_block + img * 256 + wm * 128;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          int r, c16;  // row in the wave's 128, 16-B column chunk in the 512-B row
+          if (nt == 4) {  // MFMA-native: lane = row (lane & 15), 4 lanes per row spread over the wave's rows
+            const int g = lane >> 4;
+            r = i * 16 + (lane & 15);
+            c16 = wn * 8 + jp * 4 + ((g & 1) << 1) + (g >> 1);
+          } else {  // 4 consecutive lanes per row: 64 B coalesced per lane quad
+            r = i * 16 + (lane >> 2);
+            c16 = wn * 8 + jp * 4 + (lane & 3);
+          }
+          uint4 *p = out + (r0 + r) * row_stride_16 + c16;
+          __builtin_nontemporal_store(__builtin_bit_cast(u4v, v), reinterpret_cast<u4v *>(p));
+        }
+    }
+    return;
+  }
   const int col = tid % 32, rg = tid / 32;  // 32 threads x 16 B = one 512-B row segment, 16 rows per pass
   const int64_t block_row0 = (int64_t)blockIdx.x * rows_per_block;
   for (int r = rg; r < rows_per_block; r += 16) {
@@ -44,7 +67,7 @@ int main(int argc, char **argv) {
   hipEventCreate(&e1);
   const int lds = 128 * 1024;
   hipFuncSetAttribute(reinterpret_cast<const void *>(k_store), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  for (int nt = 0; nt < 4; ++nt)
+  for (int nt = 0; nt < 6; ++nt)
     for (int blocks : {32, 128, 256, 1024}) {
       for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(k_store, dim3(blocks), dim3(512), lds, 0, out, stride16, rows, nt, 0);
       hipEventRecord(e0);
