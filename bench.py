@@ -26,7 +26,10 @@ Roofline: with the replay physics the whole env phase is ONE launch, phc_env_ste
 env-step (BYTES_PER_ENV_STEP_FUSED); with articulated physics the env step is phc_env_step,
 10,886 B (7,122 read + 3,764 written).  achieved = bytes x envs / average kernel
 time from HIP start/stop events recorded by each launch's own dispatch (hipExtLaunchKernel) for
-every launch in the timed region.  `traffic` = HBM bytes per launch from rocprofv3 PMC counters
+a uniform sample of the launches in the timed region: every ENV_TIMER_PERIOD-th env step and
+every GEMM_TIMER_PERIOD-th trunk GEMM (11, coprime to a minibatch's 13 GEMM launches, so every
+layer's launch is sampled in turn).  A timed dispatch leaves the stream idle for 5-10 us around
+it; timing every launch added ~2.5 ms to a 72 ms PPO iteration (rocprofv3 trace, round 3).  `traffic` = HBM bytes per launch from rocprofv3 PMC counters
 (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) read from profiles/traffic[_fused]_<envs>.json
 when present, else null.
 
@@ -60,6 +63,9 @@ BYTES_PER_ENV_STEP_FUSED = 11714
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16 / bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
 DEFAULTS = {"env": (200, 20), "rollout": (64, 8), "ppo": (3, 1)}
+# kernel-timer sampling (module docstring): every 4th env-step / physics launch, every 11th trunk GEMM
+ENV_TIMER_PERIOD = 4
+GEMM_TIMER_PERIOD = 11
 
 
 def parse():
@@ -427,14 +433,14 @@ def main():
     torch.cuda.synchronize()
     from puffer_phc_amd._native import KernelTimer, gemm_set_timer
 
-    timer = env.env.kernel_timer = KernelTimer(capacity=max(4096, 64 * args.steps))
-    # every phc_twin_gemm launch outside the replayed rollout graph (the training trunks' fused-
-    # epilogue GEMMs) timed by its own dispatch events, with its 2 m n k FLOPs
-    gtimer = KernelTimer(capacity=max(4096, 256 * args.steps))
+    timer = env.env.kernel_timer = KernelTimer(capacity=max(4096, 64 * args.steps), period=ENV_TIMER_PERIOD)
+    # phc_twin_gemm launches outside the replayed rollout graph (the training trunks' fused-epilogue
+    # GEMMs), every GEMM_TIMER_PERIOD-th timed by its own dispatch events, with its 2 m n k FLOPs
+    gtimer = KernelTimer(capacity=max(4096, 256 * args.steps), period=GEMM_TIMER_PERIOD)
     gemm_set_timer(gtimer)
     ptimer = None
     if args.physics == "articulated":  # every phc_physics_step launch, timed by its dispatch events
-        ptimer = env.env.physics.timer = KernelTimer(capacity=max(4096, 64 * args.steps))
+        ptimer = env.env.physics.timer = KernelTimer(capacity=max(4096, 64 * args.steps), period=ENV_TIMER_PERIOD)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -449,7 +455,8 @@ def main():
     elapsed = time.perf_counter() - t0
     skipped = runner.skipped()
     skipped = None if skipped is None else skipped - runner._skip0
-    env_steps = timer.count  # phc_env_step launches in the timed region, each timed by its dispatch events
+    env_steps = timer.count  # sampled phc_env_step launches of the timed region, timed by their dispatch events
+    env_offered, gemm_offered = timer.offered, gtimer.offered
     kern_s = timer.total_ms() / max(env_steps, 1) * 1e-3
     env.env.kernel_timer = None
     gemm_set_timer(None)
@@ -538,7 +545,7 @@ def main():
                               "env phase)" if fused else "phc_env_step",
                     "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "kernel_us": kern_s * 1e6, "launches_timed": env_steps,
+                    "kernel_us": kern_s * 1e6, "launches_timed": env_steps, "launches_in_region": env_offered,
                     "algorithmic_bytes_per_env_step": env_bytes}
         if gemm_launches:
             # the dominant kernel of the PPO / rollout modes: the trunk GEMMs (MFMA-bound)
@@ -554,6 +561,7 @@ def main():
                                "achieved": tfs, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
                                "frac": tfs / MFMA_F16_PEAK_TFS, "traffic": gtraffic, "traffic_unit": "bytes",
                                "kernel_us": gemm_s / gemm_launches * 1e6, "launches_timed": gemm_launches,
+                               "launches_in_region": gemm_offered,
                                "algorithmic_flops_per_launch": gemm_flops / gemm_launches}
             out["roofline_env_step"] = env_roof
         else:

@@ -130,6 +130,11 @@ phc_kernel_timer *phc_timer_create(int32_t capacity);
 void phc_timer_destroy(phc_kernel_timer *timer);
 void phc_timer_reset(phc_kernel_timer *timer);
 int32_t phc_timer_count(const phc_kernel_timer *timer);
+/* Sample: time only every period-th launch offered to the timer (1 = every launch, the default).
+ * A timed dispatch leaves the stream idle for 5-10 us around it; sampling keeps a timed region's
+ * wall time close to an untimed one's.  phc_timer_offered counts every launch offered. */
+void phc_timer_set_period(phc_kernel_timer *timer, int32_t period);
+int64_t phc_timer_offered(const phc_kernel_timer *timer);
 double phc_timer_total_ms(phc_kernel_timer *timer);
 double phc_timer_work(const phc_kernel_timer *timer); /* algorithmic work of the timed launches (GEMM: FLOPs) */
 /* phc_twin_gemm launches outside graph capture record into `timer` (NULL: off) with their

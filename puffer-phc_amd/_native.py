@@ -180,6 +180,8 @@ _EXPORTS = {
     "phc_timer_destroy": (None, [c_vp]),
     "phc_timer_reset": (None, [c_vp]),
     "phc_timer_count": (ctypes.c_int32, [c_vp]),
+    "phc_timer_set_period": (None, [c_vp, ctypes.c_int32]),
+    "phc_timer_offered": (ctypes.c_int64, [c_vp]),
     "phc_timer_total_ms": (ctypes.c_double, [c_vp]),
     "phc_timer_work": (ctypes.c_double, [c_vp]),
     "phc_gemm_set_timer": (None, [c_vp]),
@@ -427,17 +429,25 @@ class KernelTimer:
     """Start/stop events recorded by the kernel dispatch (phc_timer_*): per-launch kernel time
     without the event-record overhead of stream events."""
 
-    def __init__(self, capacity=4096):
+    def __init__(self, capacity=4096, period=1):
         self.handle = lib().phc_timer_create(int(capacity))
         if not self.handle:
             _check(-1, "phc_timer_create")
+        if period > 1:  # time every period-th launch only (phc_timer_set_period)
+            lib().phc_timer_set_period(self.handle, int(period))
 
     def reset(self):
         lib().phc_timer_reset(self.handle)
 
     @property
     def count(self):
+        """Launches timed."""
         return lib().phc_timer_count(self.handle)
+
+    @property
+    def offered(self):
+        """Launches offered to the timer (timed or skipped by the sampling period)."""
+        return lib().phc_timer_offered(self.handle)
 
     def total_ms(self):
         ms = lib().phc_timer_total_ms(self.handle)

@@ -33,7 +33,24 @@ struct phc_kernel_timer {
   std::vector<hipEvent_t> start, stop;
   int32_t used = 0;
   double work = 0.0;
+  int32_t period = 1;  // time every period-th launch (phc_timer_set_period)
+  int64_t seen = 0;    // launches offered to the timer
 };
+
+// The start / stop events for this launch when the timer samples it (every period-th launch offered,
+// while capacity lasts), else null events: the dispatch then records nothing.  A timed dispatch
+// costs the stream 5-10 us of idle time around it (bench.py's PPO iteration: ~140 us per minibatch
+// with every GEMM timed), so bench.py samples instead of timing every launch.
+inline bool phc_timer_take(phc_kernel_timer *t, hipEvent_t *ev0, hipEvent_t *ev1) {
+  *ev0 = *ev1 = nullptr;
+  if (!t) return false;
+  const bool take = t->seen++ % t->period == 0 && t->used < (int32_t)t->start.size();
+  if (!take) return false;
+  *ev0 = t->start[t->used];
+  *ev1 = t->stop[t->used];
+  t->used += 1;
+  return true;
+}
 
 namespace phc {
 

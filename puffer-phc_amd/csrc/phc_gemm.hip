@@ -52,12 +52,6 @@ constexpr int kGBK = 64;
 #ifndef PHC_GEMM_SPLIT_A
 #define PHC_GEMM_SPLIT_A 0
 #endif
-#ifndef PHC_GEMM_DIRECT
-#define PHC_GEMM_DIRECT 1  // forward epilogues straight from the accumulators (0: through the LDS image)
-#endif
-#ifndef PHC_GEMM_DIRECT_GRAD
-#define PHC_GEMM_DIRECT_GRAD 1  // the SiLU' / ReLU' epilogues too (0: LDS image with the LDS-staged aux)
-#endif
 #ifndef PHC_GEMM_SPLIT_DMA
 #define PHC_GEMM_SPLIT_DMA 2
 #endif
@@ -280,7 +274,7 @@ template <int L, int NMAX> __device__ __forceinline__ void wait_vmcnt_tiles(int 
 // MFMA sub-steps of 32; within it the (MI / 2) pairs of A fragments are walked as groups of
 // 2 x NI MFMAs, the fragments of group q + 1 read from LDS while the MFMAs of group q run (two
 // fragment register sets; B fragments re-read per sub-step).
-template <typename T, typename TL, bool SWAP, typename Stage>
+template <typename T, typename TL, typename Stage>
 __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__restrict__ wr, bool issue,
                                           const Stage &stage, int next, int wave, int lane,
                                           f4 (&acc)[TL::MI][TL::NI]) {
@@ -325,302 +319,16 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
     for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        // SWAP: the B fragment as the MFMA's first operand, so the block comes out transposed (the
-        // register-direct epilogue's layout: a lane holds one row, four consecutive columns)
         f4 &c = acc[2 * p + ii][j];
-        const V8 &x = SWAP ? fb[s & 1][j] : fa[q & 1][ii];
-        const V8 &y = SWAP ? fa[q & 1][ii] : fb[s & 1][j];
         if constexpr (std::is_same<T, _Float16>::value)
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
         else
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q & 1][ii], fb[s & 1][j], c, 0, 0, 0);
       }
     if (PHC_GEMM_PRIO) {
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(0);
     }
-  }
-}
-
-// Register-direct forward epilogue.  With the operands swapped in the MFMA, lane l holds, for
-// every 16 x 16 block (i, j) of its wave's TM x TN sub-tile, row 16 i + (l & 15) and the four
-// consecutive columns 16 j + 4 (l >> 4) .. + 3.  Bias and activation are applied there; fp32
-// outputs leave as one 16-B store per block; half-precision outputs are packed to 8-B halves and
-// v_permlane16_swap exchanges them between the blocks 2 jp and 2 jp + 1 (lanes 16-31 / 48-63 of
-// the first with lanes 0-15 / 32-47 of the second), after which every lane holds 8 consecutive
-// columns of one row: 16-B stores, each wave-instruction covering 64 contiguous bytes of 16 rows.
-// No LDS image, no barrier: the stores of the tile issue as soon as its MFMAs retire.  Tiles
-// that are not wholly in range store element by element.
-template <typename T> __device__ __forceinline__ unsigned pack2(float a, float b) {
-  const T h[2] = {(T)a, (T)b};
-  unsigned u;
-  __builtin_memcpy(&u, h, sizeof(u));
-  return u;
-}
-
-template <typename T, typename OutT, int EPI, typename TL>
-__device__ __forceinline__ void twin_epilogue_direct(const GemmArgs &g, f4 (&acc)[TL::MI][TL::NI], int64_t m0, int n0,
-                                                     int bt, int wave, int lane) {
-  constexpr int MI = TL::MI, NI = TL::NI, JP = NI / 2;
-  constexpr bool kBias = EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU || EPI == PHC_EPI_BIAS_RELU;
-  const int wm = wave / TL::WGN, wn = wave % TL::WGN, q4 = lane >> 4;
-  const int rt = wm * TL::TM + (lane & 15);  // tile row of block row 0
-  const int ct = wn * TL::TN + 4 * q4;       // tile column of block column 0 (pre-exchange layout)
-  const bool store_out = g.discard != 2;
-  const bool store_aux = EPI == PHC_EPI_BIAS_SILU && g.aux && g.discard != 2;
-  float bias[NI][4];
-#pragma unroll
-  for (int j = 0; j < NI; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = n0 + ct + 16 * j + e;
-      bias[j][e] = kBias && c < g.n ? g.bias[bt * g.n + c] : 0.0f;
-    }
-  // bias + activation of one accumulator quad: x = pre-activation, returns the output values
-  auto act = [&](const f4 &a, const float *b, float *x, float *y) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      x[e] = a[e] + b[e];
-      if constexpr (EPI == PHC_EPI_BIAS_SILU) y[e] = gemm_silu(x[e]);
-      else if constexpr (EPI == PHC_EPI_BIAS_RELU) y[e] = x[e] > 0.0f ? x[e] : 0.0f;
-      else y[e] = x[e];
-    }
-  };
-  constexpr int VW = sizeof(OutT) == 2 ? 8 : 4;
-  const bool full = m0 + TL::BM <= g.m && n0 + TL::BN <= g.n && g.tc % VW == 0;
-  if (!full) {  // ragged tile: element by element, pre-exchange layout
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        float x[4], y[4];
-        act(acc[i][j], bias[j], x, y);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t row = m0 + rt + 16 * i;
-          const int c = n0 + ct + 16 * j + e;
-          if (row >= g.m || c >= g.n) continue;
-          const int lc = bt * g.n + c;
-          if (store_aux) aux_store1<T>(g, gemm_twin_off(g, g.aux_layout, row, lc), x[e]);
-          if (store_out) gemm_store<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, lc), y[e]);
-        }
-      }
-    return;
-  }
-  // element offset of (row, tile column c) = base + row * stride, in either twin layout
-  auto lin = [&](int layout, int c, int64_t &base, int64_t &stride) {
-    const int lc = bt * g.n + n0 + c;
-    if (layout == PHC_LAYOUT_SPLIT) {
-      base = lc;
-      stride = (int64_t)g.tg * g.tc;
-    } else {
-      const int grp = lc / g.tc;
-      base = (int64_t)grp * g.m * g.tc + (lc - grp * g.tc);
-      stride = g.tc;
-    }
-  };
-  if (sizeof(OutT) == 4 || (store_aux && !g.aux_half)) {
-    // fp32 outputs / fp32 aux: 4 consecutive columns per block, no exchange (half outputs of this
-    // case, an fp32 aux beside f16 operands, only in tests: stored element-wise)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      int64_t ob, os, ab = 0, as = 0;
-      lin(g.out_layout, ct + 16 * j, ob, os);
-      if (store_aux) lin(g.aux_layout, ct + 16 * j, ab, as);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int64_t row = m0 + rt + 16 * i;
-        float x[4], y[4];
-        act(acc[i][j], bias[j], x, y);
-        if (store_aux) aux_store4<T>(g, ab + row * as, x);
-        if (store_out) {
-          if constexpr (sizeof(OutT) == 4) {
-            f4 *dst = reinterpret_cast<f4 *>(static_cast<float *>(g.out) + ob + row * os);
-            const f4 v = f4{y[0], y[1], y[2], y[3]};
-            if (g.nt & 1) __builtin_nontemporal_store(v, dst);
-            else *dst = v;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) static_cast<OutT *>(g.out)[ob + row * os + e] = (OutT)y[e];
-          }
-        }
-      }
-    }
-    return;
-  }
-  if constexpr (sizeof(OutT) == 2) {
-    // half precision: after the exchange lane q4 holds columns (q4 >> 1) * 8 .. + 7 of block 2 jp + (q4 & 1)
-    auto exchange_store = [&](const float *x, const float *y, void *base, int64_t off, bool nt) {
-      const auto lo = __builtin_amdgcn_permlane16_swap(pack2<OutT>(x[0], x[1]), pack2<OutT>(y[0], y[1]), false, false);
-      const auto hi = __builtin_amdgcn_permlane16_swap(pack2<OutT>(x[2], x[3]), pack2<OutT>(y[2], y[3]), false, false);
-      const u4v w = u4v{lo[0], hi[0], lo[1], hi[1]};
-      u4v *dst = reinterpret_cast<u4v *>(static_cast<OutT *>(base) + off);
-      if (nt) __builtin_nontemporal_store(w, dst);
-      else *dst = w;
-    };
-#pragma unroll
-    for (int jp = 0; jp < JP; ++jp) {
-      const int cs = wn * TL::TN + (2 * jp + (q4 & 1)) * 16 + (q4 >> 1) * 8;
-      int64_t ob, os, ab = 0, as = 0;
-      lin(g.out_layout, cs, ob, os);
-      if (store_aux) lin(g.aux_layout, cs, ab, as);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int64_t row = m0 + rt + 16 * i;
-        float x0[4], y0[4], x1[4], y1[4];
-        act(acc[i][2 * jp], bias[2 * jp], x0, y0);
-        act(acc[i][2 * jp + 1], bias[2 * jp + 1], x1, y1);
-        if (store_aux) exchange_store(x0, x1, g.aux, ab + row * as, g.nt & 2);
-        if (store_out) exchange_store(y0, y1, g.out, ob + row * os, g.nt & 1);
-      }
-    }
-  }
-}
-
-// Register-direct grad epilogue (SiLU' / ReLU'): the fp32 accumulators are exchanged first (blocks
-// 2 jp, 2 jp + 1 by v_permlane16_swap, as above), so every lane holds 8 consecutive columns of one
-// row per (i, jp); the aux (pre-activation / ReLU output) rows are loaded in that layout, 16 B per
-// lane, all of the tile's loads issued before the first is consumed; out = acc * act'(aux + bias)
-// leaves as 16-B stores; the column sums (bias gradient) are reduced over the lanes of a column
-// by xor-shuffles and over the waves of a column by the LDS operand buffer the last K-step did
-// not read (`spare`), one partial row per m tile as the LDS-image epilogue writes them.
-template <typename T, typename OutT, int EPI, typename TL>
-__device__ __forceinline__ void twin_epilogue_direct_grad(const GemmArgs &g, f4 (&acc)[TL::MI][TL::NI], char *spare,
-                                                          int64_t m0, int n0, int tm, int bt, int wave, int lane) {
-  constexpr int MI = TL::MI, NI = TL::NI, JP = NI / 2;
-  static_assert(sizeof(OutT) == 2 || sizeof(OutT) == 4, "out type");
-  static_assert(TL::STAGES == 2, "spare = the operand buffer the last K-step does not read");
-  const int wm = wave / TL::WGN, wn = wave % TL::WGN, q4 = lane >> 4;
-  const int rt = wm * TL::TM + (lane & 15);
-  const bool full = m0 + TL::BM <= g.m && n0 + TL::BN <= g.n && g.tc % 8 == 0 && g.aux_half;
-  auto lin = [&](int layout, int c, int64_t &base, int64_t &stride) {
-    const int lc = bt * g.n + n0 + c;
-    if (layout == PHC_LAYOUT_SPLIT) {
-      base = lc;
-      stride = (int64_t)g.tg * g.tc;
-    } else {
-      const int grp = lc / g.tc;
-      base = (int64_t)grp * g.m * g.tc + (lc - grp * g.tc);
-      stride = g.tc;
-    }
-  };
-  int cs[JP];
-#pragma unroll
-  for (int jp = 0; jp < JP; ++jp) cs[jp] = wn * TL::TN + (2 * jp + (q4 & 1)) * 16 + (q4 >> 1) * 8;
-  // exchange: afterwards acc[i][2 jp] / acc[i][2 jp + 1] hold columns cs[jp] .. + 3 / + 4 .. + 7
-  auto exchange = [&](int i) {
-#pragma unroll
-    for (int jp = 0; jp < JP; ++jp)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[i][2 * jp][e]),
-                                                        __builtin_bit_cast(unsigned, acc[i][2 * jp + 1][e]), false, false);
-        acc[i][2 * jp][e] = __builtin_bit_cast(float, r[0]);
-        acc[i][2 * jp + 1][e] = __builtin_bit_cast(float, r[1]);
-      }
-  };
-  float csum[JP][8], b[JP][8];
-#pragma unroll
-  for (int jp = 0; jp < JP; ++jp)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = n0 + cs[jp] + q;
-      b[jp][q] = g.bias && c < g.n ? g.bias[bt * g.n + c] : 0.0f;
-      csum[jp][q] = 0.0f;
-    }
-  auto grad = [&](float x, float v) {
-    if constexpr (EPI == PHC_EPI_SILU_GRAD) {
-      const float sg = gemm_sigmoid(x);
-      return v * sg * (1.0f + x * (1.0f - sg));
-    } else {
-      return x > 0.0f ? v : 0.0f;
-    }
-  };
-  if (full) {
-    // aux rows through a ring of MI / 2 row blocks: block i + MI / 2 is loaded as soon as block i
-    // has been consumed, so half the tile's loads are in flight while the other half is processed
-    constexpr int RING = MI / 2;
-    int64_t ab[JP], as[JP], ob[JP], os[JP];
-#pragma unroll
-    for (int jp = 0; jp < JP; ++jp) {
-      lin(g.aux_layout, cs[jp], ab[jp], as[jp]);
-      lin(g.out_layout, cs[jp], ob[jp], os[jp]);
-    }
-    u4v raw[RING][JP];
-    auto load = [&](int i) {
-#pragma unroll
-      for (int jp = 0; jp < JP; ++jp) {
-        const u4v *src = reinterpret_cast<const u4v *>(static_cast<const T *>(g.aux) + ab[jp] + (m0 + rt + 16 * i) * as[jp]);
-        raw[i % RING][jp] = (g.nt & 4) ? __builtin_nontemporal_load(src) : *src;
-      }
-    };
-#pragma unroll
-    for (int i = 0; i < RING; ++i) load(i);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      exchange(i);
-      const int64_t row = m0 + rt + 16 * i;
-      float a[JP][8];
-#pragma unroll
-      for (int jp = 0; jp < JP; ++jp) {
-        T h[8];
-        __builtin_memcpy(h, &raw[i % RING][jp], sizeof(h));
-#pragma unroll
-        for (int q = 0; q < 8; ++q) a[jp][q] = (float)h[q];
-      }
-      if (i + RING < MI) load(i + RING);
-#pragma unroll
-      for (int jp = 0; jp < JP; ++jp) {
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = grad(a[jp][e] + b[jp][e], acc[i][2 * jp][e]);
-          v[4 + e] = grad(a[jp][4 + e] + b[jp][4 + e], acc[i][2 * jp + 1][e]);
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) csum[jp][q] += v[q];
-        if (g.discard != 2) gemm_store_v<OutT, 8>(g.out, ob[jp] + row * os[jp], v, g.nt & 1);
-      }
-    }
-  } else {
-    for (int i = 0; i < MI; ++i) {
-      exchange(i);
-      const int64_t row = m0 + rt + 16 * i;
-#pragma unroll
-      for (int jp = 0; jp < JP; ++jp)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int c = n0 + cs[jp] + q;
-          if (row >= g.m || c >= g.n) continue;
-          const float x = aux_load1<T>(g, gemm_twin_off(g, g.aux_layout, row, bt * g.n + c)) + b[jp][q];
-          const float v = grad(x, q < 4 ? acc[i][2 * jp][q] : acc[i][2 * jp + 1][q - 4]);
-          csum[jp][q] += v;
-          gemm_store<OutT>(g.out, gemm_twin_off(g, g.out_layout, row, bt * g.n + c), v);
-        }
-    }
-  }
-  if (!g.partial) return;
-  // column sums: the 16 rows of a lane group by xor-shuffles, then the WGM waves of a column by LDS
-#pragma unroll
-  for (int jp = 0; jp < JP; ++jp)
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) csum[jp][q] += __shfl_xor(csum[jp][q], o, 64);
-  float *red = reinterpret_cast<float *>(spare);  // [WGM][BN]
-  if ((lane & 15) == 0) {
-#pragma unroll
-    for (int jp = 0; jp < JP; ++jp)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) red[wm * TL::BN + cs[jp] + q] = csum[jp][q];
-  }
-  lds_barrier();
-  const int tid = threadIdx.x;
-  if (tid < TL::BN) {
-    float o = 0.0f;
-#pragma unroll
-    for (int w = 0; w < TL::WGM; ++w) o += red[w * TL::BN + tid];
-    if (n0 + tid < g.n) g.partial[(int64_t)tm * (g.batch * g.n) + bt * g.n + n0 + tid] = o;
   }
 }
 
@@ -630,7 +338,7 @@ __device__ __forceinline__ void twin_epilogue_direct_grad(const GemmArgs &g, f4 
 // buffers), those of pass 3 during pass 1; the image then takes four 64-KB passes.  The epilogue
 // reads aux from LDS instead of waiting on HBM round trips per row batch.
 template <int EPI, typename TL, typename OutT> struct EpStage {
-  static constexpr bool kOn = !PHC_GEMM_DIRECT_GRAD && (EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD) && TL::BM == 256 && TL::BN == 256 &&
+  static constexpr bool kOn = (EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD) && TL::BM == 256 && TL::BN == 256 &&
                               TL::STAGES == 2 && TL::BK == 64 && TL::kWaves == 8 && sizeof(OutT) == 2;
   static constexpr int kPasses = kOn ? 4 : TL::kEpPasses;
   static constexpr int kSlotBytes = 64 * 256 * 2;  // one pass's aux rows: 64 x 256 half-precision values
@@ -646,8 +354,6 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
   constexpr bool kGrad = EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD;  // aux read + column sums
   constexpr bool kBiasFwd = EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU || EPI == PHC_EPI_BIAS_RELU;
-  // the forward epilogues straight from the accumulators (operand-swapped MFMAs, no LDS image)
-  constexpr bool kDirect = (kGrad ? PHC_GEMM_DIRECT_GRAD : PHC_GEMM_DIRECT) && NI % 2 == 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
   const int tn = wg % g.tiles_n;
@@ -709,7 +415,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
         stage_aux_pass(1, aux_slot(1));
         stage_aux_pass(2, aux_slot(2));
       }
-      gemm_step<T, TL, kDirect>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt + 1 < kt_n,
+      gemm_step<T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt + 1 < kt_n,
                        stage, kt + 1, wave, lane, acc);
     }
   } else {
@@ -727,7 +433,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const int wr = rd == 0 ? S - 1 : rd - 1;
-      gemm_step<T, TL, kDirect>(smem + rd * TL::kStageBytes, smem + wr * TL::kStageBytes, kt + S - 1 < kt_n, stage,
+      gemm_step<T, TL>(smem + rd * TL::kStageBytes, smem + wr * TL::kStageBytes, kt + S - 1 < kt_n, stage,
                        kt + S - 1, wave, lane, acc);
       rd = rd == S - 1 ? 0 : rd + 1;
     }
@@ -741,11 +447,6 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
 #pragma unroll
       for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (t == 1234.5f) static_cast<float *>(g.out)[0] = t;
-    return;
-  }
-  if constexpr (kDirect) {
-    if constexpr (kGrad) twin_epilogue_direct_grad<T, OutT, EPI, TL>(g, acc, smem + (((g.k / TL::BK - 1) & 1) ^ 1) * TL::kStageBytes, m0, n0, tm, bt, wave, lane);
-    else twin_epilogue_direct<T, OutT, EPI, TL>(g, acc, m0, n0, bt, wave, lane);
     return;
   }
   // ---- epilogue.  The accumulators (lane: column lane & 15, rows 4 * (lane >> 4) + e of each
@@ -1488,14 +1189,11 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   const int64_t out_bytes = d->m * (int64_t)d->batch * d->n * (d->out_dtype == PHC_DT_F32 ? 4 : 2);
   g.nt = (out_bytes >= nt_out_min ? 1 : 0) | ((nt_aux & 1) ? 2 : 0) | ((nt_aux & 2) ? 4 : 0);
   g_ev0 = g_ev1 = nullptr;
-  if (g_gemm_timer && g_gemm_timer->used < (int32_t)g_gemm_timer->start.size()) {
+  if (g_gemm_timer) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
-      g_ev0 = g_gemm_timer->start[g_gemm_timer->used];
-      g_ev1 = g_gemm_timer->stop[g_gemm_timer->used];
-      g_gemm_timer->used += 1;
+    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
+        phc_timer_take(g_gemm_timer, &g_ev0, &g_ev1))
       g_gemm_timer->work += 2.0 * (double)d->m * d->n * d->k * d->batch;
-    }
   }
   launch_gemm(d->dtype, d->out_dtype, d->epilogue, cfg, g, blocks, st);
   g_ev0 = g_ev1 = nullptr;
@@ -1542,14 +1240,11 @@ extern "C" int phc_weight_grad(const phc_wgrad_desc *d, void *stream) {
   g.discard = discard ? 1 : 0;
   hipStream_t st = as_stream(stream);
   g_ev0 = g_ev1 = nullptr;
-  if (g_gemm_timer && g_gemm_timer->used < (int32_t)g_gemm_timer->start.size()) {
+  if (g_gemm_timer) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
-      g_ev0 = g_gemm_timer->start[g_gemm_timer->used];
-      g_ev1 = g_gemm_timer->stop[g_gemm_timer->used];
-      g_gemm_timer->used += 1;
+    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
+        phc_timer_take(g_gemm_timer, &g_ev0, &g_ev1))
       g_gemm_timer->work += 2.0 * (double)d->m * d->n * d->rows * d->batch;
-    }
   }
   if (d->dtype == PHC_DT_F16) launch_wgrad<_Float16>(g, blocks, st);
   else launch_wgrad<__bf16>(g, blocks, st);
@@ -1609,14 +1304,11 @@ extern "C" int phc_weight_grad_group(const phc_wgrad_problem *probs, int32_t cou
   ga.discard = discard ? 1 : 0;
   hipStream_t st = as_stream(stream);
   g_ev0 = g_ev1 = nullptr;
-  if (g_gemm_timer && g_gemm_timer->used < (int32_t)g_gemm_timer->start.size()) {
+  if (g_gemm_timer) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
-      g_ev0 = g_gemm_timer->start[g_gemm_timer->used];
-      g_ev1 = g_gemm_timer->stop[g_gemm_timer->used];
-      g_gemm_timer->used += 1;
+    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
+        phc_timer_take(g_gemm_timer, &g_ev0, &g_ev1))
       g_gemm_timer->work += flops;
-    }
   }
   if (dtype == PHC_DT_F16) launch_wgrad_group<_Float16>(ga, blocks, st);
   else launch_wgrad_group<__bf16>(ga, blocks, st);

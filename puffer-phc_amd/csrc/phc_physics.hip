@@ -753,13 +753,8 @@ static int physics_launch(const phc_env_buffers *env, const float *pd_target, co
   const PhysView v = {env->num_envs, env->rigid_body_state, env->root_state, env->dof_state,
                        const_cast<float *>(env->dof_force)};  // read-only for the env step, written here
   const int64_t blocks = (env->num_envs + kPhysEnvs - 1) / kPhysEnvs;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  if (timer && timer->used < (int32_t)timer->start.size()) {
-    ev0 = timer->start[timer->used];
-    ev1 = timer->stop[timer->used];
-    timer->used += 1;
-    timer->work += (double)env->num_envs;  // env-steps
-  }
+  hipEvent_t ev0, ev1;
+  if (phc_timer_take(timer, &ev0, &ev1)) timer->work += (double)env->num_envs;  // env-steps
   const PdArgs pa{pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
                   pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr};
   hipExtLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), ev0, ev1, 0, v,

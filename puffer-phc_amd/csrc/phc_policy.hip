@@ -90,41 +90,53 @@ __global__ __launch_bounds__(256) void k_obs_half_rows(const float *__restrict__
       dv[c][e] = in ? sqrtf(var[col] + eps) : 1.0f;
     }
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * rows_per_wave;
-#pragma unroll 2
-  for (int rr = 0; rr < rows_per_wave; ++rr) {
-    const int64_t r = row0 + rr;
-    if (r >= m) break;
-    const int64_t src = rows ? rows[r] : r;
-    const float *x = obs + src * d;
+  // rows in groups of G: every load of a group is issued before the first is consumed
+  constexpr int G = NC <= 2 ? 4 : 2;
+  for (int rr0 = 0; rr0 < rows_per_wave; rr0 += G) {
+    float xv[G][NC][8];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int ch = lane + 64 * c;
-      if (ch >= chunks) continue;
-      const int c0 = ch * 8;
-      float xv[8];
-      if (c0 + 8 <= d && (((uintptr_t)(x + c0)) & 7) == 0) {
+    for (int u = 0; u < G; ++u) {
+      const int64_t r = row0 + rr0 + u;
+      const bool live = rr0 + u < rows_per_wave && r < m;
+      const float *x = obs + (live ? (rows ? rows[r] : r) : 0) * d;
 #pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          const float2 t = *reinterpret_cast<const float2 *>(x + c0 + e);
-          xv[e] = t.x; xv[e + 1] = t.y;
+      for (int c = 0; c < NC; ++c) {
+        const int c0 = (lane + 64 * c) * 8;
+        if (live && c0 + 8 <= d && (((uintptr_t)(x + c0)) & 7) == 0) {
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            const float2 t = *reinterpret_cast<const float2 *>(x + c0 + e);
+            xv[u][c][e] = t.x; xv[u][c][e + 1] = t.y;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xv[u][c][e] = live && c0 + e < d ? x[c0 + e] : 0.0f;
         }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xv[e] = c0 + e < d ? x[c0 + e] : 0.0f;
       }
-      T o[8];
+    }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = 0.0f;
-        if (c0 + e < d) {
-          v = (xv[e] - mv[c][e]) / dv[c][e];  // same expression as k_rms_normalize
-          v = v < -clip ? -clip : (v > clip ? clip : v);
+    for (int u = 0; u < G; ++u) {
+      const int64_t r = row0 + rr0 + u;
+      if (rr0 + u >= rows_per_wave || r >= m) break;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ch = lane + 64 * c;
+        if (ch >= chunks) continue;
+        const int c0 = ch * 8;
+        T o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = 0.0f;
+          if (c0 + e < d) {
+            v = (xv[u][c][e] - mv[c][e]) / dv[c][e];  // same expression as k_rms_normalize
+            v = v < -clip ? -clip : (v > clip ? clip : v);
+          }
+          o[e] = (T)v;
         }
-        o[e] = (T)v;
+        uint4 raw;
+        __builtin_memcpy(&raw, o, sizeof(raw));
+        *reinterpret_cast<uint4 *>(out + r * ldo + c0) = raw;
       }
-      uint4 raw;
-      __builtin_memcpy(&raw, o, sizeof(raw));
-      *reinterpret_cast<uint4 *>(out + r * ldo + c0) = raw;
     }
   }
 }

@@ -613,8 +613,15 @@ extern "C" void phc_timer_reset(phc_kernel_timer *t) {
   if (t) {
     t->used = 0;
     t->work = 0.0;
+    t->seen = 0;
   }
 }
+
+extern "C" void phc_timer_set_period(phc_kernel_timer *t, int32_t period) {
+  if (t) t->period = period > 1 ? period : 1;
+}
+
+extern "C" int64_t phc_timer_offered(const phc_kernel_timer *t) { return t ? t->seen : 0; }
 
 extern "C" double phc_timer_work(const phc_kernel_timer *t) { return t ? t->work : 0.0; }
 
@@ -637,12 +644,8 @@ extern "C" int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_l
   if (int rc = check_env(env)) return rc;
   if (int rc = check_lib(lib)) return rc;
   PHC_REQUIRE(p && p->dt > 0.0f, "env_step: bad params");
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  if (timer && timer->used < (int32_t)timer->start.size()) {
-    ev0 = timer->start[timer->used];
-    ev1 = timer->stop[timer->used];
-    timer->used += 1;
-  }
+  hipEvent_t ev0, ev1;
+  phc_timer_take(timer, &ev0, &ev1);
   const dim3 block(kBlock), grid(grid_envs(env->num_envs));
   hipStream_t st = as_stream(stream);
   const EnvView ev = env_view(env);
@@ -667,12 +670,8 @@ extern "C" int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_
   PHC_REQUIRE(p && p->dt > 0.0f && rp, "env_step_replay: bad params");
   PHC_REQUIRE(lib->dof_vel, "env_step_replay: motion lib needs dof_vel");
   PHC_REQUIRE(!pd || (pd->actions && pd->pd_target && pd->offset && pd->scale), "env_step_replay: bad pd map");
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  if (timer && timer->used < (int32_t)timer->start.size()) {
-    ev0 = timer->start[timer->used];
-    ev1 = timer->stop[timer->used];
-    timer->used += 1;
-  }
+  hipEvent_t ev0, ev1;
+  phc_timer_take(timer, &ev0, &ev1);
   ReplayArgs ra{rp->pos_sigma, rp->force_scale, (unsigned long long)rp->seed, (unsigned long long)rp->counter,
                 pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
                 pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr};
