@@ -562,16 +562,18 @@ def train(components, info, utilization=None):
                 acc[9] = mbl_ref.double()  # the reference logs the rollout's value (constant)
             elif not cfg.bound_loss_grad:
                 acc[9] = 0.0
-            a = acc.cpu().numpy()
+            # explained variance (core.py:397-399) in fp32 on the device; the loss row, var_y and
+            # it come back in ONE device -> host copy (each readback drains the stream)
+            y_pred = experience.sorted_values
+            y_true = experience.returns
+            var_y = torch.var(y_true, unbiased=False)
+            ev_t = 1 - torch.var(y_true - y_pred, unbiased=False) / var_y
+            a = torch.cat([acc, torch.stack([var_y, ev_t]).double()]).cpu().numpy()
             losses = LossComponents(policy_loss=a[0], value_loss=a[1], entropy=a[2], old_approx_kl=a[3],
                                     approx_kl=a[4], clipfrac=a[5], before_clip_grad_norm=a[6],
                                     l2_init_reg_loss=a[7], disc_loss=a[8], mean_bound_loss=a[9],
                                     disc_agent_acc=a[10], disc_demo_acc=a[11])
-            y_pred = experience.sorted_values
-            y_true = experience.returns
-            var_y = torch.var(y_true, unbiased=False)
-            ev = (1 - torch.var(y_true - y_pred, unbiased=False) / var_y) if float(var_y) != 0 else float("nan")
-            losses.explained_variance = float(ev)
+            losses.explained_variance = float(a[13]) if a[12] != 0 else float("nan")
             info.epoch += 1
             info.losses = losses
             done_training = info.global_step >= cfg.total_timesteps
