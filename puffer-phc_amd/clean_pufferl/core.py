@@ -498,7 +498,9 @@ def train(components, info, utilization=None):
                             loss = loss + disc_loss * cfg.disc_coef
                     if not cfg.bound_loss_grad:
                         mbl = mbl_ref  # constant: changes the loss value only, never a gradient
-                        if cfg.bound_coef > 0 and mbl is not None:
+                        # (the loss value itself is not read: the logged bound term is mbl_ref, so
+                        # the fused path skips the two scalar launches of the sum)
+                        if cfg.bound_coef > 0 and mbl is not None and not fused_mb:
                             loss = loss + mbl * cfg.bound_coef
                     elif fused_obj:
                         mbl = mbl_f  # already inside `loss` (bound_coef term of the fused objective)
@@ -516,7 +518,7 @@ def train(components, info, utilization=None):
                     opt, scaler = components.optimizer, components.scaler
                     if isinstance(opt, FlatAdam):
                         flat.overlap_begin()  # data parallel: per-layer all-reduces during the backward
-                        opt.scale(loss).backward()  # loss * S under fp16 loss scaling
+                        opt.backward(loss)  # d(loss * S): S under fp16 loss scaling
                         flat.overlap_finish()
                         gnorm = opt.fused_step(cfg.max_grad_norm)[0]  # unscale, clip, skip-on-inf, Adam
                     elif scaler is None:

@@ -140,6 +140,18 @@ class FlatAdam(torch.optim.Adam):
         """loss * current loss scale (identity without loss scaling)."""
         return loss * self._f[0] if self.use_loss_scale else loss
 
+    def backward(self, loss):
+        """(loss * loss scale).backward() without the scalar kernels: the scale (a 0-dim view of
+        the device state, or a cached 1) is handed to autograd as the loss's gradient, so no
+        ones-fill, product or product-backward launches precede the policy's backward."""
+        if self.use_loss_scale:
+            seed = self._f[0]
+        else:
+            seed = getattr(self, "_one", None)
+            if seed is None or seed.device != loss.device:
+                seed = self._one = torch.ones((), device=loss.device)
+        torch.autograd.backward(loss, grad_tensors=seed.to(loss.dtype) if loss.dtype != seed.dtype else seed)
+
     @property
     def loss_scale(self):
         return self._f[0:1]
