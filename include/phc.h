@@ -353,6 +353,11 @@ typedef struct phc_gemm_desc {
                              workgroups, each looping over tiles (persistent) */
 } phc_gemm_desc;
 size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_t n);
+/* SILU_GRAD / RELU_GRAD: with a workspace and bias_grad NULL, the launch leaves the bias gradient
+ * as per-m-tile column sums, fp32 [phc_twin_gemm_m_tiles(m, n, batch)][batch * n] at the start
+ * of the workspace, for the caller to sum (e.g. inside its own phc_reduce_into launch); with
+ * bias_grad set they are summed into it by a second launch. */
+int64_t phc_twin_gemm_m_tiles(int64_t m, int32_t n, int32_t batch);
 int phc_twin_gemm(const phc_gemm_desc *desc, float *bias_grad, void *workspace, void *stream);
 
 /* R21: the twin trunks' weight gradients (the reference's autograd of nn.Linear,

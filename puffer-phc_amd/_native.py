@@ -203,6 +203,7 @@ _EXPORTS = {
                                         ctypes.c_int32, ctypes.c_int32, c_vp, c_vp]),
     "phc_twin_gemm_workspace_bytes": (ctypes.c_size_t, [c_i64, ctypes.c_int32, ctypes.c_int32]),
     "phc_twin_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDescC), c_vp, c_vp, c_vp]),
+    "phc_twin_gemm_m_tiles": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "phc_weight_grad": (ctypes.c_int, [ctypes.POINTER(WgradDescC), c_vp]),
     "phc_weight_grad_group": (ctypes.c_int, [ctypes.POINTER(WgradProblemC), ctypes.c_int32, c_i64, ctypes.c_int32,
                                               ctypes.c_int32, c_vp]),
@@ -567,11 +568,18 @@ def _operand(t, name):
     return t3.data_ptr(), bs, t3.stride(1), t3.shape[0], t3.shape[1], t3.shape[2]
 
 
+def twin_gemm_m_tiles(m, n, batch):
+    """Rows of the bias-gradient partials a grad-epilogue launch of this shape leaves."""
+    return int(lib().phc_twin_gemm_m_tiles(int(m), int(n), int(batch)))
+
+
 def twin_gemm(a, b, epilogue, out, twin, bias=None, aux=None, aux_layout=GROUPED, out_layout=GROUPED,
-              bias_grad=None, max_workgroups=0):
+              bias_grad=None, max_workgroups=0, bias_partial=None):
     """out = epilogue(a[b] @ b[b]^T) for a [batch?, m, k], b [batch?, n, k] (phc_twin_gemm).
     twin = (groups, cols) of the output / aux tensors' logical columns.  max_workgroups > 0:
-    a persistent grid of that many workgroups looping over the tiles."""
+    a persistent grid of that many workgroups looping over the tiles.  Grad epilogues: bias_grad
+    [batch * n] receives the column sums; or bias_partial, fp32 [twin_gemm_m_tiles(m, n, batch),
+    batch * n], the per-m-tile column sums for the caller to reduce (no second launch)."""
     pa, abs_, lda, ba, m, k = _operand(a, "a")
     pb, bbs, ldb, bb, n, kb = _operand(b, "b")
     if kb != k or (ba != bb and ba != 1 and bb != 1):
@@ -593,6 +601,8 @@ def twin_gemm(a, b, epilogue, out, twin, bias=None, aux=None, aux_layout=GROUPED
     if bias_grad is not None:
         _ptr(bias_grad, torch.float32, (batch * n,), "bias_grad")
         ws = _workspace(lib().phc_twin_gemm_workspace_bytes(m, batch, n), a.device).data_ptr()
+    elif bias_partial is not None:
+        ws = _ptr(bias_partial, torch.float32, (twin_gemm_m_tiles(m, n, batch), batch * n), "bias_partial")
     _check(lib().phc_twin_gemm(ctypes.byref(d), bias_grad.data_ptr() if bias_grad is not None else None, ws,
                                _stream()),
            "phc_twin_gemm")

@@ -1113,6 +1113,13 @@ extern "C" size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_
   return (size_t)((m + 127) / 128) * batch * n * sizeof(float);  // one partial row per m tile (BM >= 128)
 }
 
+extern "C" int64_t phc_twin_gemm_m_tiles(int64_t m, int32_t n, int32_t batch) {
+  if (m <= 0 || n <= 0 || batch <= 0) return 0;
+  int bm, bn;
+  gemm_tile_dims(gemm_config(m, n, batch), &bm, &bn);
+  return (m + bm - 1) / bm;
+}
+
 extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *workspace, void *stream) {
   PHC_REQUIRE(d, "twin_gemm: null descriptor");
   PHC_REQUIRE(d->a && d->b && d->out, "twin_gemm: null operand");
@@ -1135,6 +1142,7 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   PHC_REQUIRE(d->aux_dtype == PHC_DT_F32 || d->aux_dtype == d->dtype, "twin_gemm: aux must be f32 or the operand type");
   PHC_REQUIRE(!bias_grad || (grad_epi && workspace),
               "twin_gemm: bias_grad needs the SILU_GRAD / RELU_GRAD epilogue and a workspace");
+  PHC_REQUIRE(!workspace || grad_epi, "twin_gemm: a workspace receives the grad epilogues' bias-gradient partials");
   hipStream_t st = as_stream(stream);
   const int cfg = gemm_config(d->m, d->n, d->batch);
   int bm, bn;
@@ -1164,7 +1172,7 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   g.out_layout = d->out_layout;
   g.tg = d->twin_groups;
   g.tc = d->twin_cols;
-  g.partial = bias_grad ? static_cast<float *>(workspace) : nullptr;
+  g.partial = static_cast<float *>(workspace);  // per-m-tile bias-gradient column sums (grad epilogues)
   g.tiles_m = (int)tiles_m;
   g.tiles_n = (int)tiles_n;
   // measurement aid: 1 = main loop only, 2 = the whole epilogue but no global stores

@@ -406,14 +406,21 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None, store=Fal
             else:
                 put(l, _mfma_wgrad_parts(g, zs[l - 1]) if direct else _mfma_wgrad_parts(g, zs[l - 1]).sum(1), db)
             k = WT[l - 1].shape[1]
-            db = torch.empty(2 * k, dtype=torch.float32, device=g.device)
+            # direct mode: the bias gradient stays as the epilogue's per-m-tile partial rows
+            # [tiles, 2k], summed by the final phc_reduce_into launch (no column-sum launch per layer)
+            if direct:
+                db = torch.empty((N.twin_gemm_m_tiles(M, k, 2), 2 * k), dtype=torch.float32, device=g.device)
+                bias_out = dict(bias_partial=db)
+            else:
+                db = torch.empty(2 * k, dtype=torch.float32, device=g.device)
+                bias_out = dict(bias_grad=db)
             if l > 1:
                 gp = torch.empty((2, M, k), dtype=dt, device=g.device)
-                N.twin_gemm(g, WT[l - 1], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[l - 1], bias_grad=db)
+                N.twin_gemm(g, WT[l - 1], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[l - 1], **bias_out)
             else:  # into the first layer's SPLIT [M, 2k] layout, the operand of its weight gradient
                 gp = torch.empty((M, 2 * k), dtype=dt, device=g.device)
                 N.twin_gemm(g, WT[0], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[0], aux_layout=N.SPLIT,
-                            out_layout=N.SPLIT, bias_grad=db)
+                            out_layout=N.SPLIT, **bias_out)
                 if grouped:
                     d, W = wdst(0)
                     problems[0] = (0, gp, xc, (gp, xc, d, k, K0))
