@@ -25,7 +25,7 @@ from ..optim import FlatAdam
 from ..policies.fused_ppo import fused_ppo_loss, fused_ppo_supported
 from ..policies.twin_mlp import refresh_twin
 from .ppo_loss import ppo_coefs, ppo_objective
-from .structs import Experience, LossComponents, Profile, StatsData, TrainComponents, TrainInfo, Utilization
+from .structs import Experience, LossComponents, PendingLossComponents, Profile, StatsData, TrainComponents, TrainInfo, Utilization
 from .utils import count_params, save_checkpoint, seed_everything
 
 # core.py:38 / structs.py:21: "high" float32 matmul precision.  On gfx950 hipBLASLt serves it
@@ -364,6 +364,16 @@ def compute_advantages(components, info):
     return advantages
 
 
+def _fill_losses(losses, a):
+    """The logged loss row (train's device accumulators, var_y, explained variance) into the
+    LossComponents fields."""
+    for i, k in enumerate(("policy_loss", "value_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
+                           "before_clip_grad_norm", "l2_init_reg_loss", "disc_loss", "mean_bound_loss",
+                           "disc_agent_acc", "disc_demo_acc")):
+        setattr(losses, k, a[i])
+    losses.explained_variance = float(a[13]) if a[12] != 0 else float("nan")
+
+
 def train(components, info, utilization=None):
     """PPO update (core.py:206-440)."""
     cfg, profile = info.config, info.profile
@@ -565,17 +575,22 @@ def train(components, info, utilization=None):
             elif not cfg.bound_loss_grad:
                 acc[9] = 0.0
             # explained variance (core.py:397-399) in fp32 on the device; the loss row, var_y and
-            # it come back in ONE device -> host copy (each readback drains the stream)
+            # it come back in ONE device -> host copy, non-blocking into pinned memory: the values
+            # are read (and waited for) only when the losses are first looked at
             y_pred = experience.sorted_values
             y_true = experience.returns
             var_y = torch.var(y_true, unbiased=False)
             ev_t = 1 - torch.var(y_true - y_pred, unbiased=False) / var_y
-            a = torch.cat([acc, torch.stack([var_y, ev_t]).double()]).cpu().numpy()
-            losses = LossComponents(policy_loss=a[0], value_loss=a[1], entropy=a[2], old_approx_kl=a[3],
-                                    approx_kl=a[4], clipfrac=a[5], before_clip_grad_norm=a[6],
-                                    l2_init_reg_loss=a[7], disc_loss=a[8], mean_bound_loss=a[9],
-                                    disc_agent_acc=a[10], disc_demo_acc=a[11])
-            losses.explained_variance = float(a[13]) if a[12] != 0 else float("nan")
+            row = torch.cat([acc, torch.stack([var_y, ev_t]).double()])
+            if row.is_cuda:
+                host = torch.empty(row.shape, dtype=row.dtype, pin_memory=True)
+                host.copy_(row, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record()
+                losses = PendingLossComponents(host, done, _fill_losses)
+            else:
+                losses = LossComponents()
+                _fill_losses(losses, row.numpy())
             info.epoch += 1
             info.losses = losses
             done_training = info.global_step >= cfg.total_timesteps

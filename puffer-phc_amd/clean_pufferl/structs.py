@@ -158,6 +158,26 @@ class LossComponents:
     l2_init_reg_loss: float = 0.0
 
 
+class PendingLossComponents(LossComponents):
+    """LossComponents whose values are still on their way from the device: a non-blocking copy
+    into pinned host memory and the event after it.  The first attribute read waits for that
+    event and fills the fields (fill(self, values)), so train() returns without draining the
+    stream and the host goes on queueing the next rollout while the GPU finishes the update."""
+
+    def __init__(self, host, event, fill):  # noqa: D107 (the dataclass fields are set by fill)
+        object.__setattr__(self, "_pending", (host, event, fill))
+
+    def __getattribute__(self, name):
+        d = object.__getattribute__(self, "__dict__")
+        pend = d.get("_pending")
+        if pend is not None and not name.startswith("__"):
+            d["_pending"] = None
+            host, event, fill = pend
+            event.synchronize()
+            fill(self, host.numpy())
+        return object.__getattribute__(self, name)
+
+
 @dataclass
 class StatsData:
     episode_length: List[float] = field(default_factory=list)
