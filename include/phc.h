@@ -175,10 +175,10 @@ enum {
 int phc_amp_obs(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_amp_buffers *amp, float dt,
                 int32_t mode, void *stream);
 
-/* R13: clip(a,-1,1), pd = offset + scale*a, frozen dofs = 0
+/* R13: clip(a,-1,1) when `clip` (EnvConfig.clip_actions), pd = offset + scale*a, frozen dofs = 0
  * (clean_pufferl/env.py:91-93, humanoid_phc.py:106-128, 1216-1226). */
 int phc_actions_to_pd(const float *actions, float *pd_target, int64_t n, const float *offset,
-                      const float *scale, const uint8_t *frozen, void *stream);
+                      const float *scale, const uint8_t *frozen, int32_t clip, void *stream);
 
 /* Physics stand-in (NOT a reference interface; BASELINE configs[1] "physics stubbed"):
  * writes rigid bodies = reference state at the env's next control time + N(0, sigma) noise,
@@ -194,6 +194,7 @@ typedef struct phc_pd_map {
   const float *offset;  /* [69] */
   const float *scale;   /* [69] */
   const uint8_t *frozen; /* [69] nullable */
+  int32_t clip;          /* 1: clip(a, -1, 1) first (EnvConfig.clip_actions, clean_pufferl/env.py:91) */
 } phc_pd_map;
 
 typedef struct phc_replay_params {

@@ -538,9 +538,10 @@ FROZEN_DOFS = np.concatenate([np.arange(DOF_NAMES.index(n) * 3, DOF_NAMES.index(
                               for n in ("L_Hand", "R_Hand", "L_Toe", "R_Toe")])
 
 
-def actions_to_pd(actions):
-    """puffer_phc/clean_pufferl/env.py:91-93 + humanoid_phc.py:106-128, 1216-1226."""
-    a = np.clip(f32(actions), -1, 1)
+def actions_to_pd(actions, clip=True):
+    """puffer_phc/clean_pufferl/env.py:91-93 (np.clip only when cfg.clip_actions) + humanoid_phc.py:106-128,
+    1216-1226."""
+    a = np.clip(f32(actions), -1, 1) if clip else f32(actions)
     off, scale = pd_action_scale()
     pd = off + scale * a
     pd[:, FROZEN_DOFS] = 0

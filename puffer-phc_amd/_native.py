@@ -68,7 +68,8 @@ class PhysicsParamsC(ctypes.Structure):
 
 
 class PdMapC(ctypes.Structure):
-    _fields_ = [("actions", c_vp), ("pd_target", c_vp), ("offset", c_vp), ("scale", c_vp), ("frozen", c_vp)]
+    _fields_ = [("actions", c_vp), ("pd_target", c_vp), ("offset", c_vp), ("scale", c_vp), ("frozen", c_vp),
+                ("clip", ctypes.c_int32)]
 
 
 class ReplayParamsC(ctypes.Structure):
@@ -192,7 +193,7 @@ _EXPORTS = {
                                        c_vp]),
     "phc_amp_obs": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                     ctypes.POINTER(AmpBuffersC), ctypes.c_float, ctypes.c_int32, c_vp]),
-    "phc_actions_to_pd": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "phc_actions_to_pd": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, ctypes.c_int32, c_vp]),
     "phc_compact_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_compact_rows": (ctypes.c_int, [ctypes.POINTER(RowFieldC), ctypes.c_int32, c_vp, c_i64, c_vp, c_i64, c_vp,
                                          c_vp, c_vp]),
@@ -1059,13 +1060,14 @@ def physics_step(env_c, pd_target, body_model, params, timer=None):
         _check(lib().phc_physics_step(*args, _stream()), "phc_physics_step")
 
 
-def pd_map(actions, pd_out, offset, scale, frozen):
-    """phc_pd_map of R13 (the action -> PD-target map folded into its consumer kernel)."""
+def pd_map(actions, pd_out, offset, scale, frozen, clip=True):
+    """phc_pd_map of R13 (the action -> PD-target map folded into its consumer kernel); clip =
+    EnvConfig.clip_actions (clean_pufferl/env.py:91)."""
     n = actions.shape[0]
     return PdMapC(_ptr(actions, torch.float32, (n, NUM_DOF), "actions"),
                   _ptr(pd_out, torch.float32, (n, NUM_DOF), "pd_target"),
                   _ptr(offset, torch.float32, (NUM_DOF,), "offset"), _ptr(scale, torch.float32, (NUM_DOF,), "scale"),
-                  _ptr(_as_u8(frozen), torch.uint8, (NUM_DOF,), "frozen", nullable=True))
+                  _ptr(_as_u8(frozen), torch.uint8, (NUM_DOF,), "frozen", nullable=True), int(bool(clip)))
 
 
 def env_step_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter, pd=None, timer=None):
@@ -1088,14 +1090,14 @@ def physics_step_actions(env_c, pd, body_model, params, timer=None):
            "phc_physics_step_actions")
 
 
-def actions_to_pd(actions, pd_out, offset, scale, frozen):
+def actions_to_pd(actions, pd_out, offset, scale, frozen, clip=True):
     n = actions.shape[0]
     _check(lib().phc_actions_to_pd(_ptr(actions, torch.float32, (n, NUM_DOF), "actions"),
                                    _ptr(pd_out, torch.float32, (n, NUM_DOF), "pd_target"), n,
                                    _ptr(offset, torch.float32, (NUM_DOF,), "offset"),
                                    _ptr(scale, torch.float32, (NUM_DOF,), "scale"),
                                    _ptr(_as_u8(frozen), torch.uint8, (NUM_DOF,), "frozen", nullable=True),
-                                   _stream()),
+                                   int(bool(clip)), _stream()),
            "phc_actions_to_pd")
 
 

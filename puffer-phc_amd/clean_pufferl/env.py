@@ -77,7 +77,7 @@ class PHCPufferEnv:
         if isinstance(actions, np.ndarray):
             self.actions.copy_(torch.from_numpy(actions))
             actions = self.actions
-        elif not (actions.is_cuda == self.actions.is_cuda and actions.dtype == torch.float32
+        elif not (actions.device == self.actions.device and actions.dtype == torch.float32
                   and actions.is_contiguous() and tuple(actions.shape) == tuple(self.actions.shape)):
             self.actions.copy_(actions)
             actions = self.actions

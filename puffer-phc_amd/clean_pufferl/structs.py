@@ -168,9 +168,11 @@ class PendingLossComponents(LossComponents):
         object.__setattr__(self, "_pending", (host, event, fill))
 
     def __getattribute__(self, name):
+        # every read but the marker itself resolves the copy first, dunders included: vars(),
+        # __dict__, dataclasses.asdict / copy / pickle all see the filled fields
         d = object.__getattribute__(self, "__dict__")
         pend = d.get("_pending")
-        if pend is not None and not name.startswith("__"):
+        if pend is not None and name != "_pending":
             d["_pending"] = None
             host, event, fill = pend
             event.synchronize()

@@ -34,8 +34,8 @@ def try_load_checkpoint(policy, optimizer, train_cfg, exp_id):
     trainer_path = os.path.join(path, "trainer_state.pt")
     if not os.path.exists(trainer_path):
         return None
-    state = torch.load(trainer_path, map_location=train_cfg.device, weights_only=False)
-    ckpt = torch.load(os.path.join(path, state["model_name"]), map_location=train_cfg.device, weights_only=False)
+    state = torch.load(trainer_path, map_location=train_cfg.device, weights_only=True)
+    ckpt = torch.load(os.path.join(path, state["model_name"]), map_location=train_cfg.device, weights_only=True)
     policy.load_state_dict(ckpt["state_dict"])
     optimizer.load_state_dict(state["optimizer_state_dict"])
     return state

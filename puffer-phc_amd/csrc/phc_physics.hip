@@ -232,6 +232,7 @@ struct PdArgs {
   float *pd;
   const float *off, *scale;
   const uint8_t *frozen;
+  int clip;
 };
 
 // Per-block LDS: the body table with the derived constants (row stride 79 floats: lanes b = 0..23
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         float x = pa.actions[i0 + k];
-        x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+        if (pa.clip) x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
         const int d = 3 * (b - 1) + k;
         tv[k] = (pa.frozen && pa.frozen[d]) ? 0.0f : pa.off[d] + pa.scale[d] * x;
         if (env < e.n) pa.pd[i0 + k] = tv[k];
@@ -756,7 +757,7 @@ static int physics_launch(const phc_env_buffers *env, const float *pd_target, co
   hipEvent_t ev0, ev1;
   if (phc_timer_take(timer, &ev0, &ev1)) timer->work += (double)env->num_envs;  // env-steps
   const PdArgs pa{pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
-                  pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr};
+                  pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr, pd ? pd->clip : 1};
   hipExtLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), ev0, ev1, 0, v,
                         body_model, pd_target, pa, c);
   return check_launch("physics_step");

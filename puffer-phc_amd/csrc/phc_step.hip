@@ -222,6 +222,7 @@ struct ReplayArgs {
   float *pd;
   const float *off, *scale;
   const uint8_t *frozen;
+  int clip;
 };
 
 // The replayed sim state of one (env, body): the reference record at the env's next control time
@@ -280,11 +281,12 @@ __device__ __forceinline__ void store_replay(const EnvView &e, int64_t env, int 
   }
 }
 
-// R13 (clean_pufferl/env.py:91-93, humanoid_phc.py:1216-1226): clip(a, -1, 1), pd = offset +
-// scale a, frozen dofs 0
+// R13 (clean_pufferl/env.py:91-93, humanoid_phc.py:1216-1226): clip(a, -1, 1) when cfg.clip_actions,
+// pd = offset + scale a, frozen dofs 0
 __device__ __forceinline__ float action_to_pd(float x, int d, const float *__restrict__ off,
-                                              const float *__restrict__ scale, const uint8_t *__restrict__ frozen) {
-  x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+                                              const float *__restrict__ scale, const uint8_t *__restrict__ frozen,
+                                              int clip) {
+  if (clip) x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
   return (frozen && frozen[d]) ? 0.0f : off[d] + scale[d] * x;
 }
 
@@ -293,7 +295,7 @@ __device__ __forceinline__ void map_actions(const ReplayArgs &r, int64_t env, in
   if (!r.actions || b < 1) return;
   const int64_t i0 = env * PHC_NUM_DOF + 3 * (b - 1);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) r.pd[i0 + k] = action_to_pd(r.actions[i0 + k], 3 * (b - 1) + k, r.off, r.scale, r.frozen);
+  for (int k = 0; k < 3; ++k) r.pd[i0 + k] = action_to_pd(r.actions[i0 + k], 3 * (b - 1) + k, r.off, r.scale, r.frozen, r.clip);
 }
 
 // --------------------------------------------------------------- env step --
@@ -539,10 +541,10 @@ __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l,
 __global__ __launch_bounds__(kBlock) void k_actions_to_pd(const float *__restrict__ a, float *__restrict__ pd,
                                                           int64_t total, const float *__restrict__ off,
                                                           const float *__restrict__ scale,
-                                                          const uint8_t *__restrict__ frozen) {
+                                                          const uint8_t *__restrict__ frozen, int clip) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= total) return;
-  pd[i] = action_to_pd(a[i], (int)(i % PHC_NUM_DOF), off, scale, frozen);
+  pd[i] = action_to_pd(a[i], (int)(i % PHC_NUM_DOF), off, scale, frozen, clip);
 }
 
 static int grid_envs(int64_t n) { return (int)((n + kEnvsPerBlock - 1) / kEnvsPerBlock); }
@@ -674,7 +676,7 @@ extern "C" int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_
   phc_timer_take(timer, &ev0, &ev1);
   ReplayArgs ra{rp->pos_sigma, rp->force_scale, (unsigned long long)rp->seed, (unsigned long long)rp->counter,
                 pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
-                pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr};
+                pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr, pd ? pd->clip : 1};
   const dim3 block(kBlock), grid(grid_envs(env->num_envs));
   hipStream_t st = as_stream(stream);
   const EnvView ev = env_view(env);
@@ -716,19 +718,19 @@ extern "C" int phc_physics_replay(const phc_env_buffers *env, const phc_motion_l
   PHC_REQUIRE(lib->dof_vel, "physics_replay: motion lib needs dof_vel");
   PHC_REQUIRE(p, "physics_replay: bad params");
   ReplayArgs ra{pos_sigma, force_scale, (unsigned long long)seed, (unsigned long long)counter,
-                nullptr, nullptr, nullptr, nullptr, nullptr};
+                nullptr, nullptr, nullptr, nullptr, nullptr, 1};
   hipLaunchKernelGGL(k_physics_replay, dim3(grid_envs(env->num_envs)), dim3(kBlock), 0, as_stream(stream),
                      env_view(env), lib_view(lib), make_consts(p), ra);
   return check_launch("physics_replay");
 }
 
 extern "C" int phc_actions_to_pd(const float *actions, float *pd, int64_t n, const float *offset,
-                                 const float *scale, const uint8_t *frozen, void *stream) {
+                                 const float *scale, const uint8_t *frozen, int32_t clip, void *stream) {
   PHC_REQUIRE(n >= 0, "actions_to_pd: negative n");
   if (n == 0) return PHC_OK;
   PHC_REQUIRE(actions && pd && offset && scale, "actions_to_pd: null argument");
   const int64_t total = n * PHC_NUM_DOF;
   hipLaunchKernelGGL(k_actions_to_pd, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                     as_stream(stream), actions, pd, total, offset, scale, frozen);
+                     as_stream(stream), actions, pd, total, offset, scale, frozen, (int)(clip != 0));
   return check_launch("actions_to_pd");
 }

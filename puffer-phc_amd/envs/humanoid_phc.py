@@ -86,8 +86,12 @@ class HumanoidPHC:
         if physics is None and cfg.physics == "articulated":
             from ..physics import ArticulatedPhysics, PhysicsConfig
 
+            # RobotConfig.has_self_collision: the reference's --disable_self_collision flag clears it
+            # and the asset's filter words then keep every shape pair apart (humanoid_phc.py:338, 370-381)
             physics = ArticulatedPhysics(PhysicsConfig(substeps=cfg.physics_substeps, kp_scale=cfg.kp_scale,
-                                                       kd_scale=cfg.kd_scale), device=self.device)
+                                                       kd_scale=cfg.kd_scale,
+                                                       self_collision=bool(cfg.robot.has_self_collision)),
+                                         device=self.device)
         self.physics = physics or ReplayPhysics(cfg.replay_pos_sigma, cfg.replay_force_scale, cfg.seed)
         self._rng_seed = int(cfg.seed) * 7919 + 17
         self._rng_counter = 0
@@ -291,7 +295,9 @@ class HumanoidPHC:
         # (the reference resets after HumanoidPHC.step returns): no in-launch reset there
         fused_reset = auto_reset and not self.flag_im_eval
         params = self._step_params_auto if fused_reset else self._step_params
-        pd = _native.pd_map(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale, self._pd_frozen)
+        clip = bool(self.cfg.clip_actions)  # clean_pufferl/env.py:91: np.clip only when cfg.clip_actions
+        pd = _native.pd_map(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale, self._pd_frozen,
+                            clip)
         if self.fused_env_step and hasattr(self.physics, "step_fused"):
             # R13 + the physics stand-in + the env step: one launch
             self.physics.step_fused(self, params, pd, timer=self.kernel_timer)
@@ -300,7 +306,7 @@ class HumanoidPHC:
                 self.physics.step_actions(self, pd)
             else:
                 _native.actions_to_pd(actions, self.pd_target, self._pd_action_offset, self._pd_action_scale,
-                                      self._pd_frozen)
+                                      self._pd_frozen, clip)
                 self.physics.step(self)
             _native.env_step(self._env_c, self._motion_lib.packed.c, params, timer=self.kernel_timer)
         if fused_reset and "terminals" in self._puffer:

@@ -22,6 +22,11 @@ from .policies import weight_cache
 _STATE_BYTES = ctypes.sizeof(N.OptStateC)
 
 
+# the index space of FlatAdam.state_dict()'s "state" keys: the module's parameter order, as a
+# torch.optim.Adam(policy.parameters()) checkpoint (marker written into "flat_adam")
+INDEX_SPACE = "module"
+
+
 class FlatAdam(torch.optim.Adam):
     """torch.optim.Adam over the FlatGrads parameter set with the fused clip / loss-scale /
     Adam step.  use_loss_scale follows torch.amp.GradScaler's defaults (init 2^16, growth 2 every
@@ -95,12 +100,17 @@ class FlatAdam(torch.optim.Adam):
         group["params"] = list(range(len(order)))
         return {"state": state, "param_groups": [group],
                 "flat_adam": {"loss_scale": float(self._f[0]), "growth_tracker": int(self._i[1]),
-                              "skipped": int(self._i[3])}}
+                              "skipped": int(self._i[3]), "index_space": INDEX_SPACE}}
 
     def load_state_dict(self, state_dict):
         """Loads a state dict in the module-parameter index space (what state_dict writes and what
         a torch.optim.Adam(policy.parameters()) checkpoint holds)."""
         extra = state_dict.get("flat_adam")
+        if extra is not None and extra.get("index_space") != INDEX_SPACE:
+            # FlatAdam before round 4 wrote its state in the flat, grad-ready order; the twin layers
+            # share shapes, so such moments could load into the wrong parameters without any error
+            raise ValueError("optimizer state dict written by an older FlatAdam (flat grad-ready index order, "
+                             f"no flat_adam['index_space'] == {INDEX_SPACE!r}); it cannot be mapped to parameters")
         order = self.flat_grads.module_params
         groups = state_dict["param_groups"]
         if len(groups) != 1 or len(groups[0]["params"]) != len(order):
@@ -114,6 +124,9 @@ class FlatAdam(torch.optim.Adam):
                 if st is None or id(p) not in views:
                     continue
                 off, k = views[id(p)]
+                if tuple(st["exp_avg"].shape) != tuple(p.shape) or tuple(st["exp_avg_sq"].shape) != tuple(p.shape):
+                    raise ValueError(f"optimizer state {i}: moments of shape {tuple(st['exp_avg'].shape)} for a "
+                                     f"parameter of shape {tuple(p.shape)}")
                 self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
                 self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
                 step = int(float(st["step"]))

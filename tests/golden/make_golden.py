@@ -472,7 +472,69 @@ def gen_state_dict():
         f.write("\n".join(rows) + "\n")
 
 
-if __name__ == "__main__":
+def lstm_fill(module):
+    """Deterministic weights for the LSTM-policy fixture (the test applies the same rule to the
+    port): parameter / buffer i of state_dict() order from torch.Generator seed 1000 + i."""
+    with torch.no_grad():
+        for i, (k, v) in enumerate(module.state_dict().items()):
+            g = torch.Generator().manual_seed(1000 + i)
+            x = torch.randn(v.shape, generator=g, dtype=torch.float64)
+            if k.endswith("running_var"):
+                x = x.abs() + 0.5
+            elif k.endswith("count"):
+                x = torch.full(v.shape, 10.0, dtype=torch.float64)
+            elif k.endswith("sigma"):
+                x = x * 0.1 - 1.0
+            else:
+                x = x * (0.5 / max(1, v.shape[-1]) ** 0.5)
+            v.copy_(x.to(v.dtype))
+
+
+def gen_lstm(seed=7, rows=8):
+    """N4: LSTMCriticPolicy / LSTMActorPolicy (puffer_phc/policies/lstm_policy.py:25-148) on fixed
+    weights (lstm_fill) and inputs: state-dict keys / shapes, encode_observations, decode_actions
+    (Normal mean / std, value, mean bound loss in training mode).  pufferlib.models.LSTMWrapper is
+    stubbed (the Recurrent wrapper itself stays unpinned)."""
+    from puffer_phc.policies.lstm_policy import LSTMActorPolicy, LSTMCriticPolicy
+
+    class Box:
+        def __init__(self, n, high=1.0):
+            self.shape = (n,)
+            self.high = np.full(n, high, np.float32)
+
+    rng = np.random.default_rng(seed)
+    obs = (rng.normal(size=(rows, 934)) * 2).astype(np.float32)
+    hid = rng.normal(size=(rows, 512)).astype(np.float32)
+    out, keys = {"obs": obs, "hidden_in": hid}, []
+    env = SimpleNamespace(single_observation_space=Box(934, np.inf), single_action_space=Box(69),
+                          amp_observation_space=None)
+    for name, cls in (("critic", LSTMCriticPolicy), ("actor", LSTMActorPolicy)):
+        pol = cls(env, hidden_size=512)
+        for k, v in pol.state_dict().items():
+            keys.append(f"{name}\t{k}\t{'x'.join(map(str, v.shape))}\t{str(v.dtype)}")
+        keys.append(f"{name}\t#trainable\t{sum(p.numel() for p in pol.parameters() if p.requires_grad)}\t-")
+        lstm_fill(pol)
+        with torch.no_grad():
+            for training in (False, True):
+                pol.train(training)
+                h, _ = pol.encode_observations(torch.from_numpy(obs))
+                probs, value = pol.decode_actions(torch.from_numpy(hid))
+                tag = f"{name}_{'train' if training else 'eval'}"
+                out[f"{tag}_encoded"] = h.numpy()
+                out[f"{tag}_mu"] = probs.mean.numpy()
+                out[f"{tag}_std"] = probs.stddev.numpy()
+                out[f"{tag}_value"] = value.numpy()
+                if training:
+                    out[f"{tag}_bound"] = np.float32(pol.mean_bound_loss)
+    np.savez_compressed(os.path.join(OUT, "lstm_policy.npz"), **out)
+    with open(os.path.join(OUT, "lstm_state_dict_keys.tsv"), "w") as f:
+        f.write("\n".join(keys) + "\n")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1:  # only the named generators, e.g. `make_golden.py lstm`
+    for name in sys.argv[1:]:
+        globals()[f"gen_{name}"]()
+elif __name__ == "__main__":
     sk = gen_skeleton()
     lib = gen_motion_lib(sk)
     gen_motion_state(lib)
@@ -482,5 +544,6 @@ if __name__ == "__main__":
     gen_gae()
     gen_rms()
     gen_state_dict()
+    gen_lstm()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -85,3 +85,67 @@ def test_env_step_parity_at_baseline_sizes(num_envs, num_clips):
             ms = O.motion_state(lib, ids[reset], st, pre["goff"][reset])
             np.testing.assert_array_equal(e._rigid_body_state.cpu().numpy()[reset][..., 0:3], ms["rg_pos"])
     assert resets > 0
+
+
+_FUSED_BUFS = ("_rigid_body_state", "_dof_state", "dof_force_tensor", "pd_target", "obs_buf", "rew_buf", "reward_raw",
+               "progress_buf", "reset_buf", "_terminate_buf", "_motion_start_times", "_motion_start_times_offset",
+               "_global_offset", "_sampled_motion_ids")
+
+
+@pytest.mark.parametrize("num_envs,num_clips,amp", [(1024, 1, False), (4096, 4096, False), (4096, 4096, True)],
+                         ids=["c2_1024_shared_clip", "c3_4096", "c3_4096_amp"])
+def test_fused_replay_step_at_baseline_sizes(num_envs, num_clips, amp):
+    """The kernel bench.py times (phc_env_step_replay = k_env_step<true, true>: R13 action -> PD map,
+    the replay stand-in and the post-physics step in ONE launch) against the three-launch path
+    (phc_actions_to_pd -> phc_physics_replay -> phc_env_step, oracle-pinned by the test above) at the
+    sizes it is timed at: every buffer bit for bit over 16 PufferEnv steps with auto-resets and
+    actions beyond [-1, 1].  The fused run's non-resetting rows are also checked against the oracle
+    directly (obs / reward 1e-5, termination exact) from the state the fused launch wrote.
+    Reference: /root/reference/puffer_phc/envs/humanoid_phc.py:105-172, clean_pufferl/env.py:90-164."""
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    envs = []
+    for fused in (False, True):
+        q, t, c, fps = synthetic_clips(num_clips, 20, 60, seed=num_envs + 1, device=DEV)
+        packed = PackedMotions.from_global_rotations(q, t, c, fps)
+        env = PHCPufferEnv(EnvConfig(num_envs=num_envs, seed=num_envs, use_amp_obs=amp, fused_env_step=fused),
+                           motion_data=packed)
+        env.reset()
+        envs.append(env)
+    a, b = envs
+    assert a.env.fused_env_step is False and b.env.fused_env_step is True
+    lib = _oracle_lib(packed)
+    g = torch.Generator(device=DEV).manual_seed(num_envs)
+    resets = 0
+    for step in range(STEPS):
+        eb = b.env
+        pre = dict(progress=eb.progress_buf.cpu().numpy().astype(np.int32), start=eb._motion_start_times.cpu().numpy(),
+                   off=eb._motion_start_times_offset.cpu().numpy(), goff=eb._global_offset.cpu().numpy(),
+                   ids=eb._sampled_motion_ids.cpu().numpy())
+        act = torch.randn((num_envs, 69), device=DEV, generator=g) * 1.5
+        outs = [env.step(act) for env in envs]
+        torch.cuda.synchronize()
+        for name in _FUSED_BUFS:
+            assert torch.equal(getattr(a.env, name), getattr(eb, name)), (step, name)
+        for name in ("terminals", "truncations", "masks", "rewards", "observations"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), (step, name)
+        if amp:
+            assert torch.equal(a.env._amp_obs_buf, eb._amp_obs_buf), step
+        assert torch.equal(outs[0][1], outs[1][1])
+        # the fused launch against the oracle on the rows it did not re-initialise
+        reset = (b.terminals | b.truncations).cpu().numpy()
+        resets += int(reset.sum())
+        keep = ~reset
+        ref = O.env_step(lib, pre["ids"], (pre["progress"] + 1).astype(np.int16), pre["start"], pre["off"], pre["goff"],
+                         eb._rigid_body_state.cpu().numpy(), eb._dof_vel.cpu().numpy(),
+                         eb.dof_force_tensor.cpu().numpy())
+        np.testing.assert_allclose(b.rewards.cpu().numpy()[keep], ref["rew"][keep], atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(b.observations.cpu().numpy()[keep], ref["obs"][keep], atol=1e-5, rtol=1e-5)
+        ties = np.any(np.abs(ref["reset_dist"] - 0.25) < 1e-6, -1)
+        np.testing.assert_array_equal(ref["terminate"][keep & ~ties], False)
+        np.testing.assert_array_equal(ref["reset"][keep & ~ties], False)
+    assert resets > 0
+    np.testing.assert_array_equal(b.env.pd_target.cpu().numpy(), O.actions_to_pd(act.cpu().numpy()))

@@ -308,6 +308,30 @@ def test_actions_to_pd_vs_oracle(N):
     pd = torch.empty((1000, 69), device=DEV)
     N.actions_to_pd(_t(a), pd, _t(off), _t(scale), _t(frozen))
     np.testing.assert_array_equal(pd.cpu().numpy(), O.actions_to_pd(a))
+    # EnvConfig.clip_actions = False: no clip (clean_pufferl/env.py:91)
+    N.actions_to_pd(_t(a), pd, _t(off), _t(scale), _t(frozen), clip=False)
+    np.testing.assert_array_equal(pd.cpu().numpy(), O.actions_to_pd(a, clip=False))
+    assert np.abs(pd.cpu().numpy()).max() > np.pi * 1.5
+
+
+@pytest.mark.parametrize("physics", ["replay", "articulated"])
+def test_env_honours_clip_actions(physics):
+    """cfg.clip_actions reaches every folded action -> PD map (the fused replay launch and the
+    articulated physics launch): with it off the PD targets are offset + scale * a unclipped."""
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    for clip in (True, False):
+        q, t, c, fps = synthetic_clips(4, 20, 60, seed=1, device=DEV)
+        env = PHCPufferEnv(EnvConfig(num_envs=8, seed=1, clip_actions=clip, physics=physics),
+                           motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
+        env.reset()
+        act = torch.randn((8, 69), device=DEV, generator=torch.Generator(device=DEV).manual_seed(2)) * 3
+        env.step(act)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(env.env.pd_target.cpu().numpy(), O.actions_to_pd(act.cpu().numpy(), clip=clip))
 
 
 def test_bad_arguments_raise(N, golden_lib):

@@ -9,6 +9,8 @@ rounding order; the clip coefficient here comes from a double-precision norm).  
 (double accumulation here, fp32 per-parameter means in torch).  Skip / scale decisions are exact.
 """
 
+import copy
+
 import pytest
 import torch
 
@@ -118,6 +120,18 @@ def test_state_dict_round_trip():
     opt2.load_state_dict(sd)
     assert torch.equal(opt2.exp_avg, opt.exp_avg) and torch.equal(opt2.exp_avg_sq, opt.exp_avg_sq)
     assert float(opt2.loss_scale) == float(opt.loss_scale)
+    assert sd["flat_adam"]["index_space"] == "module"
+    # a FlatAdam state dict of the earlier, flat grad-ready index order (no marker) is refused, not
+    # loaded into whichever parameters happen to share the count
+    old = copy.deepcopy(sd)
+    del old["flat_adam"]["index_space"]
+    with pytest.raises(ValueError, match="older FlatAdam"):
+        opt2.load_state_dict(old)
+    bad = copy.deepcopy(sd)
+    k0 = next(iter(bad["state"]))
+    bad["state"][k0]["exp_avg"] = bad["state"][k0]["exp_avg"].reshape(-1)[:1].clone()
+    with pytest.raises(ValueError, match="moments of shape"):
+        opt2.load_state_dict(bad)
     for o, f, P in ((opt, fg, a), (opt2, fg2, b)):
         f.zero()
         for p, g in zip(P, _grads(7, float(o.loss_scale))):

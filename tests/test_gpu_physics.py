@@ -210,6 +210,37 @@ def test_env_steps_with_articulated_physics():
     assert torch.isfinite(env.env.dof_force_tensor).all()
 
 
+@pytest.mark.parametrize("self_collision", [False, True])
+def test_env_honours_has_self_collision(self_collision):
+    """RobotConfig.has_self_collision reaches the physics step (the reference's
+    --disable_self_collision, humanoid_phc.py:338 / 370-381): an env built from the config runs bit for
+    bit like one handed ArticulatedPhysics(PhysicsConfig(self_collision=...)) explicitly."""
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig, RobotConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.physics import ArticulatedPhysics, PhysicsConfig
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    envs = []
+    for explicit in (False, True):
+        q, t, c, fps = synthetic_clips(8, 20, 60, seed=3, device=DEV)
+        packed = PackedMotions.from_global_rotations(q, t, c, fps)
+        cfg = EnvConfig(num_envs=16, seed=2, physics="articulated",
+                        robot=RobotConfig(has_self_collision=self_collision))
+        phys = ArticulatedPhysics(PhysicsConfig(self_collision=self_collision)) if explicit else None
+        env = PHCPufferEnv(cfg, motion_data=packed, physics=phys)
+        env.reset()
+        envs.append(env)
+    assert envs[0].env.physics.config.self_collision is self_collision
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    for _ in range(4):
+        act = torch.randn((16, 69), device=DEV, generator=gen) * 2.0
+        for env in envs:
+            env.step(act)
+        assert torch.equal(envs[0].env._rigid_body_state, envs[1].env._rigid_body_state)
+        assert torch.equal(envs[0].env.dof_force_tensor, envs[1].env.dof_force_tensor)
+
+
 def test_ppo_iteration_with_articulated_physics():
     """One clean_pufferl iteration (graph rollout + PPO update) with the physics step in the env:
     the rollout's physics launches run inside evaluate(), the update trains on their outcome."""

@@ -161,3 +161,43 @@ def test_adversarial_reward_propagates_nan():
     reward = torch.empty(64, device=DEV)
     N.disc_head_fwd(h, w, b, reward=reward)
     assert torch.isnan(reward).all()
+
+
+def test_deferred_loss_readback_matches_synchronous(monkeypatch):
+    """train() returns PendingLossComponents (a non-blocking copy of the loss row into pinned memory
+    plus its event).  The first read waits on that event only; its values must equal the row read
+    after a full device synchronisation, field by field, and dataclasses.asdict must see them."""
+    import dataclasses
+
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.clean_pufferl import structs
+    from puffer_phc_amd.clean_pufferl.core import _fill_losses
+    from puffer_phc_amd.config import TrainConfig
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+
+    hosts = []
+    orig = structs.PendingLossComponents.__init__
+
+    def spy(self, host, event, fill):
+        hosts.append(host)
+        orig(self, host, event, fill)
+
+    monkeypatch.setattr(structs.PendingLossComponents, "__init__", spy)
+    env = _env(256, False)
+    torch.manual_seed(0)
+    policy = Policy(PHCPolicy(env)).to(DEV)  # full widths: the fused f16 minibatch path
+    cfg = TrainConfig(batch_size=256 * 32, minibatch_size=2048, bptt_horizon=8, checkpoint_interval=10 ** 9,
+                      update_epochs=1)
+    comps, info, util = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+    clean_pufferl.evaluate(comps, info)
+    losses = clean_pufferl.train(comps, info, util)
+    assert isinstance(losses, structs.PendingLossComponents) and len(hosts) == 1
+    got = dataclasses.asdict(losses)  # first read: waits on the event alone
+    torch.cuda.synchronize()
+    ref = structs.LossComponents()
+    _fill_losses(ref, hosts[0].numpy())
+    exp = dataclasses.asdict(ref)
+    for k, v in exp.items():
+        np.testing.assert_equal(got[k], v, err_msg=k)
+    assert np.isfinite([got["policy_loss"], got["value_loss"], got["entropy"]]).all()
+    assert vars(losses)["approx_kl"] == exp["approx_kl"]
