@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--traffic-file", default=None)
+    ap.add_argument("--dp-mode", choices=["grouped", "per_layer", "split"], default="grouped",
+                    help="data-parallel weight-gradient / all-reduce schedule at N > 1 (twin_mlp.set_dp_mode)")
     a = ap.parse_args()
     k, w = DEFAULTS[a.mode]
     a.steps = k if a.steps is None else a.steps
@@ -270,7 +272,19 @@ def cpu_baseline(env, packed, seconds):
         c_oracle.compute_gae(d, v, r, 0.98, 0.2)
         reps += 1
     gae_ms = (time.perf_counter() - t0) / reps * 1e3
+    # the port's speed relative to the reference's own torch-CPU composition, measured side by side on
+    # one host (tools/ref_vs_port_cpu.py: the reference cannot travel to this box)
+    calib = None
+    cf = os.path.join(ROOT, "profiles", "r04_ref_vs_port_cpu.json")
+    if os.path.exists(cf):
+        with open(cf) as f:
+            c = json.load(f)
+        calib = {"port_over_reference_1_thread": c["port_over_reference"], "calibration_host": c["host_cpu_model"],
+                 "reference_equivalent_value_1_thread": one / c["port_over_reference"],
+                 "reference_equivalent_value_all_cores": allc / c["port_over_reference"],
+                 "file": os.path.relpath(cf, ROOT)}
     return {"value": allc, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "reference_calibration": calib,
             "comparison": "env step only (motion state x2 + reward + reset + obs); no policy inference or PPO "
                           "update, which the headline value includes",
             "value_1_thread": one, "value_all_cores": allc, "cores_all": workers,
@@ -423,6 +437,9 @@ def main():
 
         faulthandler.dump_traceback_later(float(os.environ["PHC_WATCHDOG_S"]), repeat=True)
     world, rank = setup_dist()
+    from puffer_phc_amd.policies import twin_mlp
+
+    twin_mlp.set_dp_mode(args.dp_mode)
     device = f"cuda:{torch.cuda.current_device()}"
     torch.manual_seed(1234 + rank)
     env, packed, env_cfg = build_env(args, rank)
@@ -441,6 +458,9 @@ def main():
     ptimer = None
     if args.physics == "articulated":  # every phc_physics_step launch, timed by its dispatch events
         ptimer = env.env.physics.timer = KernelTimer(capacity=max(4096, 64 * args.steps), period=ENV_TIMER_PERIOD)
+    flat = getattr(getattr(runner, "components", None), "flat_grads", None)
+    if flat is not None and world > 1:
+        flat.timing, flat.exposed = True, []
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -477,6 +497,19 @@ def main():
         counts = [float(c) for c in every]
     elapsed, kern_s = float(t[0]), float(t[1])
     processed_all = whole_job_steps(counts, args.mode == "ppo", world)
+    dp = None
+    if flat is not None and world > 1:
+        # the exposed all-reduce wait per minibatch backward: rank 0's and the slowest rank's
+        exp_ms, n_bw = flat.exposed_ms()
+        flat.timing = False
+        e = torch.tensor([exp_ms or 0.0], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
+        dp = {"mode": args.dp_mode, "backend": torch.distributed.get_backend(),
+              "allreduce_exposed_ms_per_minibatch_rank0": exp_ms,
+              "allreduce_exposed_ms_per_minibatch_max_rank": float(e[0]), "minibatches_timed": n_bw,
+              "grad_bytes_per_minibatch": flat.flat.numel() * 4,
+              "note": "CUDA events on rank's compute stream around the wait for the backward's all-reduces "
+                      "(FlatGrads.overlap_finish): the stall after the last backward kernel"}
 
     if rank == 0:
         fused = bool(getattr(env.env, "fused_env_step", False)) and args.physics == "replay"
@@ -536,6 +569,8 @@ def main():
             "cpu_baseline": cpu,
         }
         out["config"]["env_steps_timed"] = processed_all  # value = env_steps_timed / wall seconds
+        if dp is not None:
+            out["config"]["dp"] = dp
         if args.physics == "articulated":
             out["roofline_physics"] = physics_roofline(args, phys_s, phys_launches)
             if not args.no_cpu_baseline:

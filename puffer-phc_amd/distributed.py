@@ -83,6 +83,10 @@ class FlatGrads:
         self.bucket = max(1, bucket_bytes // 4)
         self._works = None
         self._done = None
+        # measurement aid (bench.py at N > 1): events on the compute stream around the wait for the
+        # backward's all-reduces — the time the stream stalls on RCCL after its last backward kernel
+        self.timing = False
+        self.exposed = []
 
     def overlap_begin(self):
         """Install the gradient-ready hook for one backward (a no-op without data parallelism)."""
@@ -115,10 +119,24 @@ class FlatGrads:
         rest = [p for p in self.params if id(p) not in self._done]
         if rest:
             self._on_ready(rest)
+        ev = None
+        if self.timing and self.flat.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for w in self._works:
             w.wait()
+        if ev is not None:
+            ev[1].record()
+            self.exposed.append(ev)
         self._works, self._done = None, None
         self.flat.div_(world_size())
+
+    def exposed_ms(self):
+        """Mean exposed all-reduce wait per backward (ms) over the timed backwards, and their count."""
+        if not self.exposed:
+            return None, 0
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.exposed) / len(self.exposed), len(self.exposed)
 
     def zero(self):
         self.flat.zero_()

@@ -449,8 +449,22 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None, store=Fal
                     jobs.extend(pairs)  # summed with the bias jobs below
                 else:
                     N.reduce_into(pairs, accumulate=False)
-            N.weight_grad_group([problems[l][3] for l in _grouped_subset(problems, xc.device)],
-                                accumulate=direct and not store)
+            sel = _grouped_subset(problems, xc.device)
+            if direct and GRAD_READY is not None and DP_SPLIT_GROUP:
+                # data parallel, split mode: the bias sums and left-out layers first, then the last
+                # three trunk layers' tiles in one launch and their span's all-reduce, which overlaps
+                # the launch of the remaining layers (the same tiles: bit-equal to one launch)
+                if jobs:
+                    N.reduce_into(jobs, accumulate=not store)
+                    jobs.clear()
+                for lo in (max(L - 3, 0), 0):
+                    part = [l for l in sel if l >= lo]
+                    sel = [l for l in sel if l < lo]
+                    if part:
+                        N.weight_grad_group([problems[l][3] for l in part], accumulate=not store)
+                    GRAD_READY([p for l in range(L - 1, lo - 1, -1) for p in params[4 * l:4 * l + 4]])
+                return None
+            N.weight_grad_group([problems[l][3] for l in sel], accumulate=direct and not store)
         if direct:
             if jobs:
                 N.reduce_into(jobs, accumulate=not store)
@@ -602,6 +616,25 @@ GROUPED_WGRAD = True
 # started after it (0, default: the grouped launch fills the 256 CUs exactly once and RCCL's
 # kernels do not take CUs from the backward's GEMMs)
 DP_PER_LAYER = os.environ.get("PHC_DP_PER_LAYER", "0") == "1"
+# data parallel on the grouped path: two grouped weight-gradient launches, the last three trunk
+# layers first, so that span's all-reduce overlaps the second launch (PHC_DP_SPLIT_GROUP=1)
+DP_SPLIT_GROUP = os.environ.get("PHC_DP_SPLIT_GROUP", "0") == "1"
+DP_MODES = ("grouped", "per_layer", "split")
+
+
+def set_dp_mode(mode):
+    """grouped (default): one grouped weight-gradient launch, then the trunk span's all-reduce;
+    per_layer: per-layer split-K weight gradients, each layer's all-reduce started as it lands;
+    split: two grouped launches (last three layers first), the first span's all-reduce overlapping
+    the second launch.  Only the data-parallel backward reads this (GRAD_READY set)."""
+    global DP_PER_LAYER, DP_SPLIT_GROUP
+    if mode not in DP_MODES:
+        raise ValueError(f"dp mode {mode!r} not in {DP_MODES}")
+    DP_PER_LAYER, DP_SPLIT_GROUP = mode == "per_layer", mode == "split"
+
+
+def dp_mode():
+    return "per_layer" if DP_PER_LAYER else ("split" if DP_SPLIT_GROUP else "grouped")
 
 
 def _use_mfma(weights, dtype):

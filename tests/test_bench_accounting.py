@@ -69,13 +69,16 @@ def test_two_rank_gloo_bench_reports_rows_over_wall():
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mode", "ppo", "--steps", "1",
            "--warmup", "1", "--envs", "512", "--batch-size", "8192", "--minibatch-size", "2048",
-           "--no-cpu-baseline"]
+           "--no-cpu-baseline", "--dp-mode", "split"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_envs"] == 1024
+    dp = out["config"]["dp"]  # the exposed all-reduce wait per minibatch backward
+    assert dp["mode"] == "split" and dp["minibatches_timed"] >= 4 and dp["backend"] == "gloo"
+    assert dp["allreduce_exposed_ms_per_minibatch_max_rank"] >= dp["allreduce_exposed_ms_per_minibatch_rank0"] >= 0
     rows = out["config"]["env_steps_timed"]
     # each rank collects >= its batch of mask-true rows per iteration (plus the last step's
     # overflow), so the whole job is ~2 x 8192, not 4 x

@@ -41,7 +41,7 @@ class _Env:
         self.amp_observation_space = None
 
 
-def _worker(rank, world, port, out_dir, per_layer):
+def _worker(rank, world, port, out_dir, mode):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -54,7 +54,7 @@ def _worker(rank, world, port, out_dir, per_layer):
     from puffer_phc_amd.policies import PHCPolicy, Policy, twin_mlp
     from puffer_phc_amd.policies.fused_ppo import fused_ppo_loss
 
-    twin_mlp.DP_PER_LAYER = per_layer
+    twin_mlp.set_dp_mode(mode)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -109,10 +109,10 @@ def _worker(rank, world, port, out_dir, per_layer):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("per_layer", [False, True], ids=["grouped", "per_layer"])
-def test_dp_gradient_matches_mean_and_union(tmp_path, per_layer):
+@pytest.mark.parametrize("mode", ["grouped", "per_layer", "split"])
+def test_dp_gradient_matches_mean_and_union(tmp_path, mode):
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path), per_layer), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
     for r in range(2):
         res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
         assert res["nonzero"] > 1000

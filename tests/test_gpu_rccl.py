@@ -80,8 +80,8 @@ def test_rccl_collectives(rccl):
     assert torch.equal(t, ref)
 
 
-@pytest.mark.parametrize("per_layer", [False, True], ids=["grouped", "per_layer"])
-def test_rccl_overlapped_backward_bit_equal(rccl, per_layer):
+@pytest.mark.parametrize("mode", ["grouped", "per_layer", "split"])
+def test_rccl_overlapped_backward_bit_equal(rccl, mode):
     """The trainer's DP minibatch backward (full widths, 32768 rows, gradients stored into a
     NaN-filled flat buffer, all-reduces started during the backward) vs the single-GPU backward."""
     D = rccl
@@ -117,16 +117,23 @@ def test_rccl_overlapped_backward_bit_equal(rccl, per_layer):
         torch.cuda.synchronize()
         return fg.flat.detach().clone()
 
-    prev = (twin_mlp.DP_PER_LAYER, twin_mlp.GROUPED_WGRAD)
+    prev = (twin_mlp.dp_mode(), twin_mlp.GROUPED_WGRAD)
+    ready = []
     try:
-        twin_mlp.DP_PER_LAYER = per_layer
+        twin_mlp.set_dp_mode(mode)
+        orig = fg._on_ready
+        fg._on_ready = lambda ps: (ready.append(len(ps)), orig(ps))  # noqa: E731 (spy)
         dp = backward(True)
-        # the single-GPU path with the same weight-gradient kernels: grouped launch, or (per-layer
-        # mode) the split-K per-layer launches
-        twin_mlp.GROUPED_WGRAD = not per_layer
+        fg._on_ready = orig
+        # the single-GPU path with the same weight-gradient kernels: grouped launch (grouped and
+        # split modes: the same tiles), or (per-layer mode) the split-K per-layer launches
+        twin_mlp.GROUPED_WGRAD = mode != "per_layer"
         single = backward(False)
     finally:
-        twin_mlp.DP_PER_LAYER, twin_mlp.GROUPED_WGRAD = prev
+        twin_mlp.set_dp_mode(prev[0])
+        twin_mlp.GROUPED_WGRAD = prev[1]
+    if mode == "split":  # ... the last three trunk layers' span (12 params), then the whole trunk
+        assert ready[-2:] == [12, 24], ready
     assert torch.isfinite(dp).all()
     assert torch.equal(dp, single)
 
