@@ -85,6 +85,16 @@ typedef struct phc_env_buffers {
   int32_t *episode_length;    /* [N] */
   double *stats;              /* [phc_stats_blocks(N), PHC_STATS_SLOTS] per-block log sums */
   uint32_t *rng_counter;      /* [N] per-env counter of the counter-based RNG (nullable) */
+  /* optional (R17 fused into the step): the policy's first trunk-GEMM operand of every obs row the
+   * step writes — RunningNorm(obs) (policies/running_norm.py:15-20) rounded once to f16 / bf16,
+   * [N, obs_operand_ld] zero-padded past 934 — the values phc_obs_half writes, bit for bit.
+   * Written by phc_env_step / phc_env_step_replay when obs_operand is set (reset kernels do not). */
+  void *obs_operand;
+  const float *obs_norm_mean; /* [934] running_mean */
+  const float *obs_norm_var;  /* [934] running_var */
+  float obs_norm_eps, obs_norm_clip;
+  int32_t obs_operand_ld;     /* % 8 == 0, >= 934; obs_operand 16-byte aligned */
+  int32_t obs_operand_dtype;  /* PHC_DT_F16 or PHC_DT_BF16 */
 } phc_env_buffers;
 
 /* Step constants: RewardConfig (config.py:23-36), EnvConfig power coef / early termination
@@ -426,6 +436,10 @@ typedef struct phc_policy_act_args {
   int64_t rows;
   int32_t hidden, num_actions;
   float ln_eps, std_max;
+  /* optional: W_mu transposed, [hidden, ld_w_mu_t] fp32, 16-byte aligned, ld_w_mu_t % 4 == 0, >= num_actions:
+   * the mu head then reads W rows coalesced across the actions (nullable: w_mu is read) */
+  const float *w_mu_t;
+  int32_t ld_w_mu_t, reserved;
 } phc_policy_act_args;
 int phc_policy_act(const phc_policy_act_args *args, void *stream);
 

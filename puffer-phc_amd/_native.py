@@ -45,7 +45,30 @@ class EnvBuffersC(ctypes.Structure):
                 ("motion_start_offset", c_vp), ("global_offset", c_vp), ("obs", c_vp), ("rew", c_vp),
                 ("reward_raw", c_vp), ("reset", c_vp), ("terminate", c_vp), ("terminals", c_vp),
                 ("truncations", c_vp), ("masks", c_vp), ("episode_return", c_vp), ("episode_length", c_vp),
-                ("stats", c_vp), ("rng_counter", c_vp)]
+                ("stats", c_vp), ("rng_counter", c_vp), ("obs_operand", c_vp), ("obs_norm_mean", c_vp),
+                ("obs_norm_var", c_vp), ("obs_norm_eps", ctypes.c_float), ("obs_norm_clip", ctypes.c_float),
+                ("obs_operand_ld", ctypes.c_int32), ("obs_operand_dtype", ctypes.c_int32)]
+
+
+def set_obs_operand(env_c, out, mean, var, eps, clip):
+    """Have phc_env_step / phc_env_step_replay also write RunningNorm(obs) as the policy's padded
+    f16 / bf16 first-GEMM operand into out [N, ld] (phc_obs_half's values); out None clears it."""
+    if out is None:
+        env_c.obs_operand = None
+        env_c.obs_norm_mean = env_c.obs_norm_var = None
+        env_c.obs_operand_ld = env_c.obs_operand_dtype = 0
+        return
+    N = int(env_c.num_envs)
+    if out.dim() != 2 or out.shape[0] != N or out.shape[1] < OBS_DIM or out.shape[1] % 8 or not out.is_contiguous() \
+            or out.data_ptr() % 16 or out.dtype not in (torch.float16, torch.bfloat16) or not out.is_cuda:
+        raise ValueError("obs operand must be a contiguous 16-B aligned f16 / bf16 device [num_envs, ld] tensor, "
+                         "ld >= 934, ld % 8 == 0")
+    env_c.obs_operand = out.data_ptr()
+    env_c.obs_norm_mean = _ptr(mean.reshape(-1), torch.float32, (OBS_DIM,), "running_mean")
+    env_c.obs_norm_var = _ptr(var.reshape(-1), torch.float32, (OBS_DIM,), "running_var")
+    env_c.obs_norm_eps, env_c.obs_norm_clip = float(eps), float(clip)
+    env_c.obs_operand_ld = out.shape[1]
+    env_c.obs_operand_dtype = DTYPE_CODE[out.dtype]
 
 
 class StepParamsC(ctypes.Structure):
@@ -154,7 +177,8 @@ class PolicyActArgsC(ctypes.Structure):
     _fields_ = [("trunk_out", c_vp), ("ln_gamma", c_vp * 2), ("ln_beta", c_vp * 2), ("w_mu", c_vp), ("b_mu", c_vp),
                 ("w_value", c_vp), ("b_value", c_vp), ("log_sigma", c_vp), ("noise", c_vp), ("actions", c_vp),
                 ("logprob", c_vp), ("value", c_vp), ("mu", c_vp), ("rows", c_i64), ("hidden", ctypes.c_int32),
-                ("num_actions", ctypes.c_int32), ("ln_eps", ctypes.c_float), ("std_max", ctypes.c_float)]
+                ("num_actions", ctypes.c_int32), ("ln_eps", ctypes.c_float), ("std_max", ctypes.c_float),
+                ("w_mu_t", c_vp), ("ld_w_mu_t", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class AdamParamsC(ctypes.Structure):
@@ -754,11 +778,19 @@ def obs_half(obs, mean, var, eps, clip, out, rows=None):
 
 
 def policy_act(trunk_out, ln_actor, ln_critic, eps, w_mu, b_mu, w_value, b_value, log_sigma, noise, actions, logprob, value,
-               mu=None, std_max=float("inf")):
+               mu=None, std_max=float("inf"), w_mu_t=None):
     """Rollout tail after the trunks: LayerNorm+SiLU of both trunks (ln_* = (weight, bias)),
-    mu / value heads, Normal sample and log-prob (phc_policy_act)."""
+    mu / value heads, Normal sample and log-prob (phc_policy_act).  w_mu_t: optional [hidden, ld]
+    transposed copy of w_mu (ld % 4 == 0, 16-B aligned): the mu head's weight reads coalesce."""
     G, M, H = trunk_out.shape
     A = w_mu.shape[0]
+    wt_ptr, wt_ld = None, 0
+    if w_mu_t is not None:
+        if w_mu_t.dtype != torch.float32 or w_mu_t.dim() != 2 or w_mu_t.shape[0] != H or w_mu_t.stride(1) != 1 \
+                or w_mu_t.stride(0) < A or w_mu_t.stride(0) % 4 or w_mu_t.data_ptr() % 16 or not w_mu_t.is_cuda:
+            raise ValueError("policy_act: w_mu_t must be a 16-B aligned fp32 [hidden, ld >= actions, ld % 4 == 0] "
+                             "device tensor")
+        wt_ptr, wt_ld = w_mu_t.data_ptr(), w_mu_t.stride(0)
     if G != 2:
         raise ValueError("policy_act: trunk_out must be [2, rows, hidden]")
     args = PolicyActArgsC(_ptr(trunk_out, torch.float32, (2, M, H), "trunk_out"),
@@ -773,7 +805,7 @@ def policy_act(trunk_out, ln_actor, ln_critic, eps, w_mu, b_mu, w_value, b_value
                           _ptr(noise, torch.float32, (M, A), "noise"), _ptr(actions, torch.float32, (M, A), "actions"),
                           _ptr(logprob, torch.float32, (M,), "logprob"), _ptr(value, torch.float32, (M,), "value"),
                           _ptr(mu, torch.float32, (M, A), "mu", nullable=True), M, H, A, float(eps),
-                          min(float(std_max), 3.0e38))
+                          min(float(std_max), 3.0e38), wt_ptr, wt_ld, 0)
     _check(lib().phc_policy_act(ctypes.byref(args), _stream()), "phc_policy_act")
 
 

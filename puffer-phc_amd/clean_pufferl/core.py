@@ -23,7 +23,7 @@ from .. import _native
 from .. import distributed as D
 from ..optim import FlatAdam
 from ..policies.fused_ppo import fused_ppo_loss, fused_ppo_supported
-from ..policies.twin_mlp import refresh_twin
+from ..policies.twin_mlp import half_input_width, refresh_twin
 from .ppo_loss import ppo_coefs, ppo_objective
 from .structs import Experience, LossComponents, PendingLossComponents, Profile, StatsData, TrainComponents, TrainInfo, Utilization
 from .utils import count_params, save_checkpoint, seed_everything
@@ -160,6 +160,34 @@ class RolloutStep:
         self.eager_steps = 0
         pol = self.policy.policy if hasattr(self.policy, "policy") else self.policy
         self.twin = getattr(pol, "_twin", None)
+        # R17 fused into the env step: the step kernel writes RunningNorm(obs) as the policy's first
+        # GEMM operand (HumanoidPHC.set_obs_operand), so the captured graph starts at the trunks; the
+        # operand is rebuilt eagerly (phc_obs_half) at the first step of every evaluate() — the
+        # statistics change between iterations — and whenever a reset kernel wrote obs rows
+        self.opnd, self.opnd_first = None, True
+        henv = getattr(env, "env", None)
+        width = half_input_width(self.twin, _compute_dtype(self.cfg)) if self.twin is not None else None
+        if (self.fused_act and width is not None and hasattr(pol, "act_rollout") and hasattr(pol, "obs_norm")
+                and henv is not None and hasattr(henv, "set_obs_operand") and
+                getattr(info.config, "fused_obs_operand", True)):
+            self.opnd = torch.zeros((n, width), dtype=_compute_dtype(self.cfg), device=dev)
+            self._opnd_norm = None
+
+    def begin(self):
+        """Start of an evaluate() call: the RunningNorm statistics may have changed since the last."""
+        self.opnd_first = True
+
+    def _refresh_operand(self):
+        pol = self.policy.policy if hasattr(self.policy, "policy") else self.policy
+        nm = pol.obs_norm
+        henv = self.env.env
+        key = (nm.running_mean.data_ptr(), nm.running_var.data_ptr(), float(nm.epsilon), float(nm.clip))
+        if key != self._opnd_norm:  # (re)point the step kernel at the statistics' buffers
+            henv.set_obs_operand(self.opnd, nm.running_mean, nm.running_var, nm.epsilon, nm.clip)
+            self._opnd_norm = key
+        if self.opnd_first or not henv.obs_operand_fresh:
+            _native.obs_half(self.env.observations, nm.running_mean, nm.running_var, nm.epsilon, nm.clip, self.opnd)
+            self.opnd_first = False
 
     def _body(self):
         pol = self.policy.policy if hasattr(self.policy, "policy") else self.policy
@@ -170,7 +198,7 @@ class RolloutStep:
                 # an RNG op inside the captured graph would add the generator's seed / offset
                 # updates to every replay), then the fused policy tail writes the staging buffers
                 fused = pol.act_rollout(self.env.observations, self.noise, self.actions, self.logprob, self.value,
-                                        mu=self.mu)
+                                        mu=self.mu, obs_half=self.opnd)
             if not fused:
                 actions, logprob, _, value = self.policy(self.env.observations)
                 self.value.copy_(value.flatten())
@@ -182,6 +210,8 @@ class RolloutStep:
     def run(self, use_graph=True):
         if self.twin is not None:
             refresh_twin(self.twin, _compute_dtype(self.cfg))  # in-place refresh after optimizer steps
+        if self.opnd is not None:
+            self._refresh_operand()
         if self.fused_act:
             self.noise.normal_()
         if self.graph is not None:
@@ -241,6 +271,7 @@ def _evaluate_graph(components, info):
     with profile.evaluate:
         start = experience.ptr
         rs.store.reset(start)
+        rs.begin()
         # a step stores at most num_agents rows, so the buffer cannot fill before `min_steps`:
         # those steps run without a host read; after them the device cursor is read once per
         # step (the reference's per-step mask.sum().item(), core.py:136, becomes the running

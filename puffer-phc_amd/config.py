@@ -5,6 +5,7 @@ tyro is not available offline; `scripts/train.py` parses the same dotted flags
 non-CLI (the reference marks them `Suppress`).
 """
 
+import os
 from dataclasses import dataclass, field
 from typing import Literal, Optional, Tuple
 
@@ -205,3 +206,6 @@ class TrainConfig(DeviceConfig):
     # train(): normalise + round the whole batch's observations into the first GEMM's half
     # operand once per call, in minibatch order (phc_obs_half); False = per minibatch, fp32
     fused_obs: bool = True
+    # rollout: the env step kernel also writes RunningNorm(obs) as the first GEMM's half operand
+    # (HumanoidPHC.set_obs_operand); False = a phc_obs_half launch per rollout step
+    fused_obs_operand: bool = os.environ.get("PHC_FUSED_OBS_OPERAND", "1") == "1"

@@ -332,6 +332,146 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
   }
 }
 
+// ---- 256 x 256 main loop as a ping-pong of two wave groups (PHC_GEMM_8PH) -------------------
+// The 8 waves form two groups (wave rows wm = 0 / 1, one wave of each on every SIMD) that run one
+// workgroup barrier apart: while one group issues its LDS fragment reads and its share of the next
+// K-tile's LDS-DMA, the other runs 16 MFMAs, then they swap — the SIMD's matrix pipe always has a
+// wave with MFMA work.  A K-tile is four phases, one per quadrant of a wave's 128 x 64 output
+// (64 rows x 32 columns x K 64 = 16 MFMAs): (A lo, B lo), (A lo, B hi), (A hi, B hi), (A hi, B lo),
+// so a phase reads 12, 4, 8 or 0 fragments.  The operand tile moves in four half-tiles named by
+// the phase that first reads them — B lo (the first 32 of every wave's 64 B rows), A lo (the first
+// 64 of every wave's 128 A rows), B hi, A hi — each phase issuing one half-tile (2 glds per
+// thread) of the NEXT K-tile, three phases before it is read; a counted vmcnt before the first
+// barrier of the phase ahead of the read retires it, so two half-tiles stay in flight across
+// every barrier and no wait drains the DMA.  Restaging a slot is >= 2 phases after its last read.
+#ifndef PHC_GEMM_8PH
+#define PHC_GEMM_8PH 0
+#endif
+#ifndef PHC_8PH_RELOAD_B  // 1: phase 4 re-reads the B lo fragments (one B register set instead of two)
+#define PHC_8PH_RELOAD_B 0
+#endif
+
+// local row lr (0..127) of half-tile `hi` -> tile row: groups of SPAN rows, every other group
+template <int SPAN> __device__ __forceinline__ int half_row(int lr, int hi) {
+  return (lr / SPAN) * 2 * SPAN + hi * SPAN + lr % SPAN;
+}
+
+// glds of one half-tile: 128 rows x 64 k (16 KB), 2 wave-instructions per wave of 8; LDS rows keep
+// the tile's [row][8 chunks] image (chunk c of row r at slot c ^ (r & 7))
+template <int SPAN>
+__device__ __forceinline__ void stage_half(const char *base, int64_t ld, int64_t row0, int64_t rows, int k0,
+                                           char *lds_tile, int hi, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = i * 8 + wave;  // local rows 8j .. 8j + 7
+    const int r0 = half_row<SPAN>(8 * j, hi);
+    const int r = r0 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    int64_t gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    const char *src = base + (gr * ld + k0 + (c << 3)) * 2;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (lds_void *)(lds_tile + r0 * 128), 16, 0, 0);
+  }
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// one phase's MFMAs: quadrant (QM, QN) of the wave's accumulators over the K-tile's two 32-deep steps
+template <typename T, int QM, int QN, typename V8, int MI, int NI>
+__device__ __forceinline__ void phase_mfma(f4 (&acc)[MI][NI], const V8 (&fa)[4][2], const V8 (&fb)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        f4 &c = acc[4 * QM + ii][2 * QN + jj];
+        if constexpr (std::is_same<T, _Float16>::value)
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][s], fb[jj][s], c, 0, 0, 0);
+        else
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ii][s], fb[jj][s], c, 0, 0, 0);
+      }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+__device__ __forceinline__ void phase_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// One K-tile (four phases) from `rd`, issuing the next K-tile's half-tiles into `wr` (issue), or on
+// the last K-tile `aux` (the grad epilogue's LDS-DMA of its first three aux passes, 12 glds per
+// wave, issued in phase 1; then the counted waits leave them in flight).  rd / wr restrict: the
+// compiler's own wait insertion does not drain the DMA before the fragment reads.
+template <typename T, typename TL, typename AuxFn>
+__device__ __forceinline__ void ktile_8ph(const char *__restrict__ rd, char *__restrict__ wr, bool issue, bool aux,
+                                          const AuxFn &aux_fn, const char *A, int64_t lda, int64_t m0, int64_t m,
+                                          const char *B, int64_t ldb, int64_t n0, int64_t n, int k0n, int wave,
+                                          int lane, f4 (&acc)[TL::MI][TL::NI]) {
+  using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
+  const int wm = wave / TL::WGN, wn = wave % TL::WGN;
+  const char *ta = rd;
+  const char *tb = rd + TL::BM * 128;
+  char *wa = wr;
+  char *wb = wr + TL::BM * 128;
+#if PHC_8PH_RELOAD_B
+  V8 fa[4][2], fb0[2][2];
+  V8(&fb1)[2][2] = fb0;
+#else
+  V8 fa[4][2], fb0[2][2], fb1[2][2];
+#endif
+  auto load_a = [&](int qm) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+        read_frag<64>(ta, wm * TL::TM + (4 * qm + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), fa[ii][s]);
+  };
+  auto load_b = [&](V8(&f)[2][2], int qn) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+        read_frag<64>(tb, wn * TL::TN + (2 * qn + jj) * 16 + (lane & 15), s * 4 + (lane >> 4), f[jj][s]);
+  };
+  // phase 1: issue B lo of the next K-tile (or the aux rows), read A lo + B lo, retire B hi
+  if (issue) stage_half<32>(B, ldb, n0, n, k0n, wb, 0, wave, lane);
+  if (aux) aux_fn();
+  load_b(fb0, 0);
+  load_a(0);
+  if (issue) wait_vm<4>();
+  else if (aux) wait_vm<14>();
+  else wait_vm<2>();
+  phase_barrier();
+  phase_mfma<T, 0, 0>(acc, fa, fb0);
+  phase_barrier();
+  // phase 2: issue A lo, read B hi, retire A hi
+  if (issue) stage_half<64>(A, lda, m0, m, k0n, wa, 0, wave, lane);
+  load_b(fb1, 1);
+  if (issue) wait_vm<4>();
+  else if (aux) wait_vm<12>();
+  else wait_vm<0>();
+  phase_barrier();
+  phase_mfma<T, 0, 1>(acc, fa, fb1);
+  phase_barrier();
+  // phase 3: issue B hi, read A hi
+  if (issue) stage_half<32>(B, ldb, n0, n, k0n, wb, 1, wave, lane);
+  load_a(1);
+  phase_barrier();
+  phase_mfma<T, 1, 1>(acc, fa, fb1);
+  phase_barrier();
+  // phase 4: issue A hi, (re-read B lo,) retire the next K-tile's A lo + B lo
+  if (issue) stage_half<64>(A, lda, m0, m, k0n, wa, 1, wave, lane);
+  if (PHC_8PH_RELOAD_B) load_b(fb0, 0);
+  if (issue) wait_vm<4>();
+  phase_barrier();
+  phase_mfma<T, 1, 0>(acc, fa, fb0);
+  phase_barrier();
+}
+
 // Grad epilogues (SiLU' / ReLU' with a half-precision aux) of 256 x 256 tiles stage the aux
 // (pre-activation) rows through LDS: the rows of epilogue passes 0-2 move by LDS-DMA during the
 // last K-step (into the operand buffer that step does not read and the 32 KB above the operand
@@ -406,7 +546,32 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
       stage_tile<BM / 2, TL::kWaves, TL::BK>(A, g.lda, m0 + BM / 2, g.m, kt * TL::BK, st + BM / 2 * TL::BK * 2, wave, lane);
     if (parts & 2) stage_tile<BN, TL::kWaves, TL::BK>(B, g.ldb, n0, g.n, kt * TL::BK, st + BM * TL::BK * 2, wave, lane);
   };
-  if constexpr (TL::STAGES == 2) {
+  if constexpr (PHC_GEMM_8PH && BM == 256 && BN == 256 && TL::kWaves == 8 && TL::STAGES == 2 && TL::BK == 64 &&
+                TL::WGM == 2 && TL::WGN == 4) {
+    // the ping-pong main loop: K-tile 0's half-tiles in read order, A lo + B lo retired, then the
+    // second wave group (waves 4-7) falls one barrier behind the first and catches up at the end
+    const bool second = (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) >= 4;
+    char *b0 = smem + BM * 128;
+    stage_half<32>(B, g.ldb, n0, g.n, 0, b0, 0, wave, lane);
+    stage_half<64>(A, g.lda, m0, g.m, 0, smem, 0, wave, lane);
+    stage_half<32>(B, g.ldb, n0, g.n, 0, b0, 1, wave, lane);
+    stage_half<64>(A, g.lda, m0, g.m, 0, smem, 1, wave, lane);
+    wait_vm<4>();
+    phase_barrier();
+    if (second) phase_barrier();
+    auto aux3 = [&]() {
+      stage_aux_pass(0, aux_slot(0));
+      stage_aux_pass(1, aux_slot(1));
+      stage_aux_pass(2, aux_slot(2));
+    };
+    for (int kt = 0; kt < kt_n; ++kt) {
+      const bool last = kt + 1 == kt_n;
+      ktile_8ph<T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, !last,
+                       last && stage_aux, aux3, A, g.lda, m0, g.m, B, g.ldb, n0, g.n, (kt + 1) * TL::BK, wave, lane,
+                       acc);
+    }
+    if (!second) phase_barrier();
+  } else if constexpr (TL::STAGES == 2) {
     stage(0, smem);
     for (int kt = 0; kt < kt_n; ++kt) {
       dma_barrier();  // tile kt landed; buffer (kt+1)&1 is no longer read

@@ -147,6 +147,7 @@ constexpr int kActMaxA = 72;     // actions supported (PHC_NUM_DOF + 3)
 constexpr int kActThreads = 320; // 2 k halves x 2 row groups x up to 72 actions (288), 5 waves
 constexpr int kActTasks = (2 * kActRows + kActThreads / 64 - 1) / (kActThreads / 64);  // LN rows per wave
 static_assert(2 * (kActRows / 4) * kActMaxA <= kActThreads, "one (k half, row group, action) per thread");
+static_assert(4 * kActMaxA <= kActThreads && (kActRows / 2) * kActMaxA <= kActThreads, "transposed-W mu head threads");
 
 __device__ __forceinline__ float wave_sum(float s) {
 #pragma unroll
@@ -184,6 +185,70 @@ __device__ __forceinline__ void ln_silu_row(float x[C][4], const float *__restri
       const float ln = (x[k][e] - mean) * rstd * g4[e] + b4[e];
       x[k][e] = ln / (1.0f + expf(-ln));
     }
+  }
+}
+
+// The mu head, sample and log_prob from the transposed W_mu: thread (kq, j) accumulates all kActRows
+// rows of action j over the k quarter kq — per k step one dword of W^T row k (the 4 x A threads of a
+// step read one contiguous run of every W^T row: coalesced, where w_mu's rows put 64 lanes on 64
+// lines) and one broadcast float4 of each h row from LDS; the quarters are summed in a fixed order.
+template <int H>
+__device__ __forceinline__ void act_tail_wt(const phc_policy_act_args &a, float (*hs)[H], float (*part)[kActMaxA],
+                                            int64_t r0, int tid) {
+  __shared__ float quarter[4][kActRows][kActMaxA];
+  const int A = a.num_actions;
+  constexpr int KQ = H / 4;
+  if (tid < 4 * A) {
+    const int kq = tid / A, j = tid % A;
+    float acc[kActRows];
+#pragma unroll
+    for (int r = 0; r < kActRows; ++r) acc[r] = 0.0f;
+    const int64_t ld = a.ld_w_mu_t;
+    const float *wt = a.w_mu_t + (int64_t)(kq * KQ) * ld + j;
+#pragma unroll 2
+    for (int kk = 0; kk < KQ; kk += 4) {
+      const float w0 = wt[(kk + 0) * ld], w1 = wt[(kk + 1) * ld], w2 = wt[(kk + 2) * ld], w3 = wt[(kk + 3) * ld];
+#pragma unroll
+      for (int r = 0; r < kActRows; ++r) {
+        const float4 h = *reinterpret_cast<const float4 *>(&hs[r][kq * KQ + kk]);
+        acc[r] += h.x * w0;
+        acc[r] += h.y * w1;
+        acc[r] += h.z * w2;
+        acc[r] += h.w * w3;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kActRows; ++r) quarter[kq][r][j] = acc[r];
+  }
+  __syncthreads();
+  // thread (g, j): rows 2g, 2g + 1 of action j
+  const float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+  if (tid < (kActRows / 2) * A) {
+    const int g = tid / A, j = tid % A;
+    float sd = expf(a.log_sigma[j]);
+    sd = sd > a.std_max ? a.std_max : sd;
+    const float bj = a.b_mu[j];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int rr = 2 * g + u;
+      const int64_t row = r0 + rr;
+      float lp = 0.0f;
+      if (row < a.rows) {
+        const float mu = ((quarter[0][rr][j] + quarter[1][rr][j]) + (quarter[2][rr][j] + quarter[3][rr][j])) + bj;
+        const float act = mu + sd * a.noise[row * A + j];
+        const float d = act - mu;
+        lp = -(d * d) / (2.0f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
+        a.actions[row * A + j] = act;
+        if (a.mu) a.mu[row * A + j] = mu;
+      }
+      part[rr][j] = lp;
+    }
+  }
+  __syncthreads();
+  if (tid < kActRows && r0 + tid < a.rows) {
+    float s = 0.0f;
+    for (int jj = 0; jj < A; ++jj) s += part[tid][jj];
+    a.logprob[r0 + tid] = s;
   }
 }
 
@@ -240,6 +305,10 @@ __global__ __launch_bounds__(kActThreads) void k_policy_act(phc_policy_act_args 
   }
   __syncthreads();
   if (tid < kActRows && r0 + tid < a.rows) a.value[r0 + tid] = red[tid];
+  if (a.w_mu_t) {
+    act_tail_wt<H>(a, hs, part, r0, tid);
+    return;
+  }
 
   // mu head: thread (kh, g, j) owns rows 4g..4g+3 of action j over k in [kh H/2, (kh+1) H/2);
   // per 4-deep k step one float4 of its W_mu row (L2) and one broadcast float4 of each h row
@@ -371,6 +440,9 @@ extern "C" int phc_policy_act(const phc_policy_act_args *args, void *stream) {
               "policy_act: hidden must be 256, 512, 768 or 1024");
   PHC_REQUIRE(a.num_actions >= 1 && a.num_actions <= kActMaxA, "policy_act: 1..%d actions", kActMaxA);
   PHC_REQUIRE((reinterpret_cast<uintptr_t>(a.trunk_out) & 15) == 0, "policy_act: trunk_out must be 16-byte aligned");
+  PHC_REQUIRE(!a.w_mu_t || (a.ld_w_mu_t >= a.num_actions && a.ld_w_mu_t % 4 == 0 &&
+                            (reinterpret_cast<uintptr_t>(a.w_mu_t) & 15) == 0),
+              "policy_act: w_mu_t must be 16-byte aligned with ld_w_mu_t >= num_actions, ld_w_mu_t %% 4 == 0");
   if (a.rows == 0) return PHC_OK;
   const dim3 grid((unsigned)((a.rows + kActRows - 1) / kActRows));
   hipStream_t st = as_stream(stream);

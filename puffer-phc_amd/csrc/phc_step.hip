@@ -84,13 +84,18 @@ struct EnvView {
   int32_t *ep_len;
   double *stats;
   uint32_t *rng;
+  void *opnd;  // the fused obs operand (phc_env_buffers.obs_operand), nullable
+  const float *opnd_mean, *opnd_var;
+  float opnd_eps, opnd_clip;
+  int opnd_ld, opnd_bf16;
 };
 
 static EnvView env_view(const phc_env_buffers *e) {
   return {e->num_envs, e->rigid_body_state, e->root_state, e->dof_state, e->dof_force, e->progress,
           e->motion_ids, e->motion_start_times, e->motion_start_offset, e->global_offset, e->obs, e->rew,
           e->reward_raw, e->reset, e->terminate, e->terminals, e->truncations, e->masks, e->episode_return,
-          e->episode_length, e->stats, e->rng_counter};
+          e->episode_length, e->stats, e->rng_counter, e->obs_operand, e->obs_norm_mean, e->obs_norm_var,
+          e->obs_norm_eps, e->obs_norm_clip, e->obs_operand_ld, e->obs_operand_dtype == PHC_DT_BF16 ? 1 : 0};
 }
 
 // ------------------------------------------------------------ motion state --
@@ -168,15 +173,21 @@ __device__ __forceinline__ float reset_draw(const EnvView &e, int64_t env, unsig
 }
 
 // Observation of one env from its sim state (this lane's body) and the reference state ref1.
-__device__ __forceinline__ void env_obs_ref(const EnvView &e, int64_t env, int lane, const BodyRec &s,
-                                            const BodyRec &ref1, bool write) {
+// the observation row of one env from its half-wave into `row` (global memory, or the workgroup's
+// LDS staging rows: k_env_step)
+__device__ __forceinline__ void env_obs_row(float *row, int lane, const BodyRec &s, const BodyRec &ref1, bool write) {
   const bool active = lane < kBodies;
   const int b = active ? lane : 0;
   const v3 root_p = {group_bcast(s.p.x), group_bcast(s.p.y), group_bcast(s.p.z)};
   const q4 root_r = {group_bcast(s.r.x), group_bcast(s.r.y), group_bcast(s.r.z), group_bcast(s.r.w)};
   Heading hinv, hrot;
   heading_quats(root_r, &hrot, &hinv);
-  if (write && active) write_obs_body(e.obs + env * kObs, b, s, root_p, hinv, hrot, ref1);
+  if (write && active) write_obs_body(row, b, s, root_p, hinv, hrot, ref1);
+}
+
+__device__ __forceinline__ void env_obs_ref(const EnvView &e, int64_t env, int lane, const BodyRec &s,
+                                            const BodyRec &ref1, bool write) {
+  env_obs_row(e.obs + env * kObs, lane, s, ref1, write);
 }
 
 // Observation of one env from its sim state and the reference at `t1` (+ offset `off`).
@@ -414,9 +425,9 @@ __device__ __forceinline__ double stats_prefetch(const EnvView &e) {
   return (e.stats && threadIdx.x < 10) ? e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] : 0.0;
 }
 
-template <int kEnvs>
+template <int kEnvs, bool kSync = true>
 __device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10], double prev) {
-  __syncthreads();
+  if (kSync) __syncthreads();
   if (threadIdx.x < 10) {
     double acc = 0.0;
 #pragma unroll
@@ -430,9 +441,58 @@ __device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10], 
 // the replayed sim state (k_physics_replay: the reference at t plus noise, which is exactly ref0
 // below plus noise, so its frame rows are gathered once) and the post-physics step; the same
 // values as k_actions_to_pd -> k_physics_replay -> k_env_step bit for bit.
+// The observation rows (the kernel's largest output: 3,736 B per env) are staged in LDS and written
+// out by the whole workgroup as 16-B stores: the workgroup's 8 rows are one contiguous 29,888-B
+// span of obs [N, 934], so ~8 fully coalesced dwordx4 stores per thread replace 39 scattered dword
+// stores per body lane (PHC_ENV_OBS_LDS=0: written in place).
+#ifndef PHC_ENV_OBS_LDS
+#define PHC_ENV_OBS_LDS 1
+#endif
+
+// copy `nf` floats of LDS staging rows to global `dst` with 16-B stores (dst 16-B aligned), else 4-B
+__device__ __forceinline__ void copy_rows_out(float *__restrict__ dst, const float *__restrict__ src, int nf) {
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int n4 = nf >> 2;
+    for (int i = threadIdx.x; i < n4; i += kBlock)
+      reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(src)[i];
+    for (int i = (n4 << 2) + threadIdx.x; i < nf; i += kBlock) dst[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < nf; i += kBlock) dst[i] = src[i];
+  }
+}
+
+// RunningNorm + rounding of the workgroup's staged obs rows into the policy's first-GEMM operand
+// (phc_obs_half's expression: (x - mean) / sqrtf(var + eps), clamped, one rounding; columns past
+// the 934 observations zero): 16 B per output chunk, rows of the workgroup's contiguous span
+template <typename T>
+__device__ __forceinline__ void operand_rows_out(const EnvView &e, const float *__restrict__ rows, int64_t env0,
+                                                 int nv) {
+  const int chunks = e.opnd_ld / 8;
+  for (int i = threadIdx.x; i < nv * chunks; i += kBlock) {
+    const int rr = i / chunks, c0 = (i - rr * chunks) * 8;
+    const float *x = rows + rr * kObs;
+    T o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float v = 0.0f;
+      if (c0 + q < kObs) {
+        v = (x[c0 + q] - e.opnd_mean[c0 + q]) / sqrtf(e.opnd_var[c0 + q] + e.opnd_eps);
+        v = v < -e.opnd_clip ? -e.opnd_clip : (v > e.opnd_clip ? e.opnd_clip : v);
+      }
+      o[q] = (T)v;
+    }
+    uint4 raw;
+    __builtin_memcpy(&raw, o, sizeof(raw));
+    *reinterpret_cast<uint4 *>(static_cast<T *>(e.opnd) + (env0 + rr) * e.opnd_ld + c0) = raw;
+  }
+}
+
 template <bool AUTO, bool REPLAY>
 __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
+#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
+  __shared__ __attribute__((aligned(16))) float sh_obs[kEnvsPerBlock * kObs];
+#endif
   const int g = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + g;
   const int lane = threadIdx.x % kGroup;
@@ -508,17 +568,32 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
     const BodyRec r1 = blend_body(rows1.a, rows1.c, bl1.b, &off1);
     e.obs[ei * kObs + lane] = r1.p.x + r1.r.w + r1.v.y + r1.av.z + s.p.x;
   }
+#elif PHC_ENV_OBS_LDS
+  env_obs_row(sh_obs + g * kObs, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
 #else
   env_obs_ref(e, ei, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
 #endif
 
-  if (e.stats) {
-    if (lane == 0) {
+  if (e.stats && lane == 0) {
 #pragma unroll
-      for (int k = 0; k < 10; ++k) sh_stats[g][k] = st_row[k];
-    }
-    flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
+    for (int k = 0; k < 10; ++k) sh_stats[g][k] = st_row[k];
   }
+#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
+  __syncthreads();  // the staged rows and the stats rows are complete
+  {
+    const int64_t env0 = (int64_t)blockIdx.x * kEnvsPerBlock;
+    const int64_t left = e.n - env0;
+    const int nv = left < kEnvsPerBlock ? (int)left : kEnvsPerBlock;
+    copy_rows_out(e.obs + env0 * kObs, sh_obs, nv * kObs);
+    if (e.opnd) {
+      if (e.opnd_bf16) operand_rows_out<__bf16>(e, sh_obs, env0, nv);
+      else operand_rows_out<_Float16>(e, sh_obs, env0, nv);
+    }
+  }
+  if (e.stats) flush_stats<kEnvsPerBlock, false>(e, sh_stats, st_prev);
+#else
+  if (e.stats) flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
@@ -565,6 +640,15 @@ static int check_env(const phc_env_buffers *e) {
               "env: null buffer");
   PHC_REQUIRE((e->episode_return == nullptr) == (e->episode_length == nullptr),
               "env: episode_return and episode_length must both be set or both null");
+  if (e->obs_operand) {
+    PHC_REQUIRE(PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0, "env: obs_operand needs the LDS-staged obs rows (PHC_ENV_OBS_LDS)");
+    PHC_REQUIRE(e->obs_norm_mean && e->obs_norm_var, "env: obs_operand needs the RunningNorm mean and var");
+    PHC_REQUIRE(e->obs_operand_ld >= PHC_OBS_DIM && e->obs_operand_ld % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(e->obs_operand) & 15) == 0,
+                "env: obs_operand must be 16-byte aligned with ld %% 8 == 0 and ld >= %d", PHC_OBS_DIM);
+    PHC_REQUIRE(e->obs_operand_dtype == PHC_DT_F16 || e->obs_operand_dtype == PHC_DT_BF16,
+                "env: obs_operand dtype must be f16 or bf16");
+  }
   return PHC_OK;
 }
 

@@ -103,19 +103,9 @@ __global__ __launch_bounds__(kGaeBlock) void k_gae_apply(const float *dn, const 
 constexpr int kRmsCols = 256;
 constexpr int64_t kRmsRows = 512;
 
-__global__ __launch_bounds__(kRmsCols) void k_rms_partial(const float *__restrict__ x, int64_t rows, int64_t cols,
-                                                          double *__restrict__ part) {
-  const int64_t col = (int64_t)blockIdx.x * kRmsCols + threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.y * kRmsRows;
-  const int64_t r1 = r0 + kRmsRows < rows ? r0 + kRmsRows : rows;
-  if (col >= cols) return;
-  double s = 0.0, s2 = 0.0;
-  for (int64_t r = r0; r < r1; ++r) {
-    const double xv = (double)x[r * cols + col];
-    s += xv;
-    s2 += xv * xv;
-  }
-  const int64_t nrc = r1 - r0;
+// (mean, M2) of one column chunk from its float64 sums
+__device__ __forceinline__ void rms_store_part(double *__restrict__ part, int64_t cols, int64_t col, double s, double s2,
+                                               int64_t nrc) {
   const double mean = s / (double)nrc;
   double m2 = s2 - s * mean;
   if (m2 < 0.0) m2 = 0.0;
@@ -124,21 +114,77 @@ __global__ __launch_bounds__(kRmsCols) void k_rms_partial(const float *__restric
   p[1] = m2;
 }
 
+// Each thread sums TWO adjacent columns (one 8-B load per row when the row starts allow it) over
+// the chunk's rows in row order — the same float64 sums as one column per thread — with the next
+// kPf rows' loads in flight ahead of the adds (the serial chain otherwise waits a memory round
+// trip per row).
+constexpr int kRmsPf = 8;
+__global__ __launch_bounds__(kRmsCols) void k_rms_partial(const float *__restrict__ x, int64_t rows, int64_t cols,
+                                                          double *__restrict__ part) {
+  const int64_t col = ((int64_t)blockIdx.x * kRmsCols + threadIdx.x) * 2;
+  const int64_t r0 = (int64_t)blockIdx.y * kRmsRows;
+  const int64_t r1 = r0 + kRmsRows < rows ? r0 + kRmsRows : rows;
+  if (col >= cols) return;
+  const bool two = col + 1 < cols;
+  const bool vec = two && (cols % 2 == 0) && ((reinterpret_cast<uintptr_t>(x) & 7) == 0);
+  double s0 = 0.0, q0 = 0.0, s1 = 0.0, q1 = 0.0;
+  float2 buf[kRmsPf];
+  auto load = [&](int64_t r) -> float2 {
+    const float *p = x + r * cols + col;
+    if (vec) return *reinterpret_cast<const float2 *>(p);
+    return float2{p[0], two ? p[1] : 0.0f};
+  };
+  int64_t r = r0;
+  for (; r + kRmsPf <= r1; r += kRmsPf) {
+#pragma unroll
+    for (int u = 0; u < kRmsPf; ++u) buf[u] = load(r + u);
+#pragma unroll
+    for (int u = 0; u < kRmsPf; ++u) {
+      const double a = (double)buf[u].x, b = (double)buf[u].y;
+      s0 += a;
+      q0 += a * a;
+      s1 += b;
+      q1 += b * b;
+    }
+  }
+  for (; r < r1; ++r) {
+    const float2 v = load(r);
+    const double a = (double)v.x, b = (double)v.y;
+    s0 += a;
+    q0 += a * a;
+    s1 += b;
+    q1 += b * b;
+  }
+  rms_store_part(part, cols, col, s0, q0, r1 - r0);
+  if (two) rms_store_part(part, cols, col + 1, s1, q1, r1 - r0);
+}
+
 // Chan merge of a column's row-chunk partials (mean, M2) in chunk order
 __device__ __forceinline__ void rms_chunk_merge(const double *__restrict__ part, int64_t rows, int64_t cols,
                                                 int64_t nchunks, int64_t col, double &n, double &mean, double &m2) {
   n = 0.0;
   mean = 0.0;
   m2 = 0.0;
-  for (int64_t k = 0; k < nchunks; ++k) {
-    const double nb = (double)((k + 1) * kRmsRows < rows ? kRmsRows : rows - k * kRmsRows);
-    const double mb = part[(k * cols + col) * 2];
-    const double m2b = part[(k * cols + col) * 2 + 1];
-    const double tot = n + nb;
-    const double delta = mb - mean;
-    mean += delta * (nb / tot);
-    m2 += m2b + delta * delta * (n * nb / tot);
-    n = tot;
+  // the chunk partials of the next 8 chunks are loaded before they are merged (same order)
+  constexpr int PF = 8;
+  for (int64_t k0 = 0; k0 < nchunks; k0 += PF) {
+    double2 pb[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      if (k0 + u < nchunks) pb[u] = *reinterpret_cast<const double2 *>(part + ((k0 + u) * cols + col) * 2);
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int64_t k = k0 + u;
+      if (k >= nchunks) break;
+      const double nb = (double)((k + 1) * kRmsRows < rows ? kRmsRows : rows - k * kRmsRows);
+      const double mb = pb[u].x;
+      const double m2b = pb[u].y;
+      const double tot = n + nb;
+      const double delta = mb - mean;
+      mean += delta * (nb / tot);
+      m2 += m2b + delta * delta * (n * nb / tot);
+      n = tot;
+    }
   }
 }
 
@@ -251,7 +297,8 @@ extern "C" int phc_rms_update(const float *x, int64_t rows, int64_t cols, float 
   const int64_t nchunks = (rows + kRmsRows - 1) / kRmsRows;
   double *part = reinterpret_cast<double *>(workspace);
   const unsigned gx = (unsigned)((cols + kRmsCols - 1) / kRmsCols);
-  hipLaunchKernelGGL(k_rms_partial, dim3(gx, (unsigned)nchunks), dim3(kRmsCols), 0, s, x, rows, cols, part);
+  const unsigned gp = (unsigned)((cols + 2 * kRmsCols - 1) / (2 * kRmsCols));  // two columns per thread
+  hipLaunchKernelGGL(k_rms_partial, dim3(gp, (unsigned)nchunks), dim3(kRmsCols), 0, s, x, rows, cols, part);
   if (int rc = check_launch("rms_partial")) return rc;
   hipLaunchKernelGGL(k_rms_merge, dim3(gx), dim3(kRmsCols), 0, s, part, rows, cols, nchunks, mean, var, count);
   if (int rc = check_launch("rms_merge")) return rc;
@@ -267,7 +314,8 @@ extern "C" int phc_rms_moments(const float *x, int64_t rows, int64_t cols, doubl
   const int64_t nchunks = (rows + kRmsRows - 1) / kRmsRows;
   double *part = reinterpret_cast<double *>(workspace);
   const unsigned gx = (unsigned)((cols + kRmsCols - 1) / kRmsCols);
-  hipLaunchKernelGGL(k_rms_partial, dim3(gx, (unsigned)nchunks), dim3(kRmsCols), 0, s, x, rows, cols, part);
+  const unsigned gp = (unsigned)((cols + 2 * kRmsCols - 1) / (2 * kRmsCols));  // two columns per thread
+  hipLaunchKernelGGL(k_rms_partial, dim3(gp, (unsigned)nchunks), dim3(kRmsCols), 0, s, x, rows, cols, part);
   if (int rc = check_launch("rms_partial")) return rc;
   hipLaunchKernelGGL(k_rms_moments, dim3(gx), dim3(kRmsCols), 0, s, part, rows, cols, nchunks, moments);
   return check_launch("rms_moments");

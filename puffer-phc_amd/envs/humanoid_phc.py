@@ -194,6 +194,10 @@ class HumanoidPHC:
             self._amp_c = _native.amp_struct(self._amp_obs_buf, self._amp_obs_demo_buf)
         self._puffer = {}
         self._env_c = None
+        # the policy's fused obs operand (set_obs_operand): (out, mean, var, eps, clip) or None, and
+        # whether the last obs write (a fused step) also wrote it
+        self._obs_operand = None
+        self.obs_operand_fresh = False
         self._build_structs()
 
     def attach_puffer_buffers(self, terminals, truncations, masks, episode_return, episode_length, stats):
@@ -208,7 +212,19 @@ class HumanoidPHC:
             self.dof_force_tensor, self.progress_buf, self._sampled_motion_ids, self._motion_start_times,
             self._motion_start_times_offset, self._global_offset, self.obs_buf, self.rew_buf, self.reward_raw,
             self.reset_buf, self._terminate_buf, rng_counter=self._rng_counter_buf, **self._puffer)
+        if self._obs_operand is not None:
+            _native.set_obs_operand(self._env_c, *self._obs_operand)
         self._build_step_params()
+
+    def set_obs_operand(self, out, mean, var, eps, clip):
+        """R17 fused into the step: every phc_env_step / phc_env_step_replay launch also writes
+        RunningNorm(obs) (running stats mean / var, eps, clip) as the policy's padded f16 / bf16
+        first-GEMM operand into out [N, ld] (phc_obs_half's values).  The reset kernels do not:
+        obs_operand_fresh says whether the operand matches obs_buf after the last launch.  out
+        None detaches it."""
+        self._obs_operand = None if out is None else (out, mean, var, float(eps), float(clip))
+        _native.set_obs_operand(self._env_c, out, mean, var, eps, clip)
+        self.obs_operand_fresh = False
 
     def _build_step_params(self):
         args = (self.dt, self.cfg.reward, self.cfg.rew_power_coef, self.cfg.reward.use_power_reward,
@@ -270,6 +286,7 @@ class HumanoidPHC:
             self._reset_mask[env_ids] = True
             _native.reset_envs(self._env_c, self._motion_lib.packed.c, self._step_params, mask=self._reset_mask,
                                seed=self._rng_seed, counter=self._next_counter())
+        self.obs_operand_fresh = False  # the reset kernel writes obs rows but not the fused operand
         self._init_amp_obs()
         return self.obs_buf
 
@@ -283,6 +300,7 @@ class HumanoidPHC:
         clean_pufferl/env.py:114-116, without leaving the device)."""
         _native.reset_envs(self._env_c, self._motion_lib.packed.c, self._step_params, mask=None,
                            seed=self._rng_seed, counter=self._next_counter())
+        self.obs_operand_fresh = False
         self._init_amp_obs()
 
     def step(self, actions, auto_reset=False):
@@ -325,6 +343,8 @@ class HumanoidPHC:
             self.extras["mpjpe"] = (self._rigid_body_pos - res["rg_pos"]).norm(dim=-1).mean(dim=-1)
             self.extras["body_pos"] = self._rigid_body_pos.cpu().numpy()
             self.extras["body_pos_gt"] = res["rg_pos"].cpu().numpy()
+        # every obs row of this step came from the step kernel, which also wrote the fused operand
+        self.obs_operand_fresh = self._obs_operand is not None
         if auto_reset and not fused_reset:
             self.reset_done()  # PHCPufferEnv.step's env.reset(reset_indices), clean_pufferl/env.py:114-116
         return self.obs_buf, self.rew_buf, self.reset_buf, self.extras

@@ -59,6 +59,7 @@ class FusedPPOLossFn(torch.autograd.Function):
         ctx.ppo = (mu, log_sigma, actions, row_coef, coefs)
         st = stats[1:]
         ctx.mark_non_differentiable(st)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         return stats[0], st
 
     @staticmethod

@@ -72,31 +72,33 @@ class PHCPolicy(DiscriminatorPolicy):
         n = self.obs_norm
         return N.obs_half(obs, n.running_mean, n.running_var, n.epsilon, n.clip, out, rows)
 
-    def act_rollout(self, obs, noise, actions, logprob, value, mu=None):
+    def act_rollout(self, obs, noise, actions, logprob, value, mu=None, obs_half=None):
         """Rollout inference (encode_observations + decode_actions + sample_logits) writing the
         sampled actions, their log-probability and the value into the given buffers: half input
         (phc_obs_half), MFMA trunks, then LayerNorm+SiLU, both heads, the Normal sample and
         log_prob in one kernel (phc_policy_act).  False when this precision / shape has no fused
-        path (the caller then runs the module)."""
+        path (the caller then runs the module).  obs_half: the operand already built from obs (the
+        env step's fused RunningNorm, HumanoidPHC.set_obs_operand)."""
         h = self._head
         if not (self.fused and self.fused_ln and twin_ln_silu_supported(self._twin.pairs[-1][0].weight.shape[0])):
             return False
-        xc = self.obs_half_input(obs)
+        xc = obs_half if obs_half is not None else self.obs_half_input(obs)
         if xc is None:
             return False
         w = self.mu[0].weight
         if self._w_mu_aligned is None or self._w_mu_aligned.device != w.device:
-            self._twin.extras = [(p, d) for p, d in self._twin.extras if p is not w]
-            self._w_mu_aligned = self._twin.add_extra(w)
+            self._twin.extras = [e for e in self._twin.extras if e[0] is not w]
+            # transposed [hidden, 72]: the tail's mu-head weight reads coalesce across the actions
+            self._w_mu_aligned = self._twin.add_extra(w, transpose_ld=-(-w.shape[0] // 4) * 4)
         y = twin_trunks(xc, self._twin)  # refreshes the MFMA operands and the aligned mu weight
         la, lc = self.actor_mlp[h], self.critic_mlp[h]
         vh, mh = self.critic_mlp[h + 2], self.mu[0]
         # the mu weight's aligned copy, refreshed with the trunk operands by twin_trunks above (or
         # refresh_twin before a graph replay); the plain parameter on other paths
-        w_mu = self._w_mu_aligned if _use_mfma(self._twin, xc.dtype) else mh.weight
-        N.policy_act(y, (la.weight, la.bias), (lc.weight, lc.bias), la.eps, w_mu, mh.bias, vh.weight, vh.bias,
+        w_mu_t = self._w_mu_aligned if _use_mfma(self._twin, xc.dtype) else None
+        N.policy_act(y, (la.weight, la.bias), (lc.weight, lc.bias), la.eps, mh.weight, mh.bias, vh.weight, vh.bias,
                      self.sigma, noise, actions, logprob, value, mu=mu,
-                     std_max=1e-6 if self._deterministic_action is True else float("inf"))
+                     std_max=1e-6 if self._deterministic_action is True else float("inf"), w_mu_t=w_mu_t)
         return True
 
     def encode_observations(self, obs):

@@ -101,23 +101,31 @@ class TwinWeights:
         self.pairs = list(zip(actor_linears, critic_linears))
         self._key = None
         self.w, self.b = [], []
-        # fp32 parameters copied alongside the MFMA operands into 16-B aligned buffers (the rollout
-        # tail reads the mu head's weight with float4 loads; a view into the flat optimizer buffer
-        # is only 4-B aligned): (parameter, destination)
+        # fp32 parameters copied alongside the MFMA operands into 16-B aligned buffers (a view into
+        # the flat optimizer buffer is only 4-B aligned): (parameter, destination, transposed
+        # destination) — the rollout tail reads the mu head's weight transposed, [hidden, ld]
         self.extras = []
 
-    def add_extra(self, param):
-        """Register an fp32 parameter for an aligned copy refreshed with the MFMA operands; returns
-        the destination (valid after the next mfma_operands / refresh_twin)."""
-        dst = torch.empty(param.shape, dtype=torch.float32, device=param.device)
-        self.extras.append((param, dst))
-        return dst
+    def add_extra(self, param, transpose_ld=None):
+        """Register a 2-D fp32 parameter [rows, cols] for an aligned copy refreshed with the MFMA
+        operands; returns the destination (valid after the next mfma_operands / refresh_twin):
+        [rows, cols], or with transpose_ld the transposed [cols, rows] view of a [cols,
+        transpose_ld] buffer."""
+        if transpose_ld is None:
+            dst = torch.empty(param.shape, dtype=torch.float32, device=param.device)
+            self.extras.append((param, dst, None))
+            return dst
+        rows, cols = param.shape
+        buf = torch.zeros((cols, transpose_ld), dtype=torch.float32, device=param.device)
+        dst_t = buf[:, :rows]
+        self.extras.append((param, None, dst_t))
+        return dst_t
 
     def params(self):
         out = []
         for a, c in self.pairs:
             out += [a.weight, a.bias, c.weight, c.bias]
-        return out + [p for p, _ in self.extras]
+        return out + [e[0] for e in self.extras]
 
     def get(self, dtype):
         """Stacked weights for `dtype`; refreshed IN PLACE when a parameter changed, so a captured
@@ -189,7 +197,7 @@ def _pack_jobs(weights, ops):
         jobs += [(a.bias.detach(), ops.b[i][:na], None), (c.bias.detach(), ops.b[i][na:], None)]
     for i, (a, c) in enumerate(weights.pairs[1:]):
         jobs += [(a.weight.detach(), ops.w[i][0], ops.wt[i][0]), (c.weight.detach(), ops.w[i][1], ops.wt[i][1])]
-    jobs += [(p.detach(), dst, None) for p, dst in weights.extras]
+    jobs += [(p.detach(), dst, dst_t) for p, dst, dst_t in weights.extras]
     return jobs
 
 

@@ -36,8 +36,9 @@ def test_host_only_queries():
 def test_struct_layouts_match_header_sizes():
     import ctypes
 
-    # 22 pointers/ints in phc_env_buffers, 9 fields in phc_motion_lib
-    assert ctypes.sizeof(_native.EnvBuffersC) == 8 * 22
+    # 22 pointers/ints in phc_env_buffers + the fused obs operand (3 pointers, 2 floats, 2 int32),
+    # 9 fields in phc_motion_lib
+    assert ctypes.sizeof(_native.EnvBuffersC) == 8 * 22 + 8 * 3 + 4 * 4
     assert ctypes.sizeof(_native.MotionLibC) == 8 * 9
     # 10 floats + 4 int32 + 24 floats + int32 + pad + uint64
     assert ctypes.sizeof(_native.StepParamsC) == 4 * (10 + 4 + 24 + 1) + 4 + 8

@@ -149,3 +149,42 @@ def test_fused_replay_step_at_baseline_sizes(num_envs, num_clips, amp):
         np.testing.assert_array_equal(ref["reset"][keep & ~ties], False)
     assert resets > 0
     np.testing.assert_array_equal(b.env.pd_target.cpu().numpy(), O.actions_to_pd(act.cpu().numpy()))
+
+
+@pytest.mark.parametrize("num_envs,dtype,fused,physics", [(4096, torch.float16, True, "replay"),
+                                                          (1001, torch.bfloat16, True, "replay"),
+                                                          (1001, torch.float16, False, "replay"),
+                                                          (64, torch.float16, True, "articulated")],
+                         ids=["c3_f16", "ragged_bf16", "three_launch", "articulated"])
+def test_step_writes_obs_operand(num_envs, dtype, fused, physics):
+    """R17 fused into the step (HumanoidPHC.set_obs_operand): after every step the [N, 960] operand
+    equals phc_obs_half(obs) bit for bit — in-launch auto-resets included — and a reset kernel
+    marks it stale (obs_operand_fresh False)."""
+    from puffer_phc_amd import _native as N
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    q, t, c, fps = synthetic_clips(min(num_envs, 512), 20, 60, seed=5, device=DEV)
+    env = PHCPufferEnv(EnvConfig(num_envs=num_envs, seed=3, fused_env_step=fused, physics=physics),
+                       motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
+    env.reset()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    mean = torch.randn((1, 934), device=DEV, generator=g) * 0.3
+    var = torch.rand((1, 934), device=DEV, generator=g) * 2 + 0.05
+    opnd = torch.full((num_envs, 960), float("nan"), dtype=dtype, device=DEV)
+    env.env.set_obs_operand(opnd, mean, var, 1e-5, 5.0)
+    assert not env.env.obs_operand_fresh
+    ref = torch.empty_like(opnd)
+    resets = 0
+    for _ in range(STEPS):
+        env.step(torch.randn((num_envs, 69), device=DEV, generator=g) * 0.5)
+        assert env.env.obs_operand_fresh
+        N.obs_half(env.observations, mean, var, 1e-5, 5.0, ref)
+        torch.cuda.synchronize()
+        assert torch.equal(opnd.view(torch.int16), ref.view(torch.int16))
+        resets += int((env.terminals | env.truncations).sum())
+    assert resets > 0
+    env.env.reset([0, 1])
+    assert not env.env.obs_operand_fresh

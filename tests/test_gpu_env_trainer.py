@@ -249,3 +249,36 @@ def test_fused_replay_step_equals_three_launches(amp):
     # the PD targets follow the reference's map (clip, scale, frozen hands / toes)
     ref = O.actions_to_pd(act.cpu().numpy())
     np.testing.assert_array_equal(envs[1].env.pd_target.cpu().numpy(), ref)
+
+
+def test_rollout_env_written_operand_matches_obs_half():
+    """The captured rollout reading the env step's fused RunningNorm operand (fused_obs_operand) vs a
+    phc_obs_half launch per step: identical experience buffers over two evaluate() calls with an obs
+    RunningNorm update between them (the operand is rebuilt at the start of each evaluate)."""
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig, TrainConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    runs = []
+    for fused_op in (False, True):
+        q, t, c, fps = synthetic_clips(64, 12, 40, seed=21, device=DEV)
+        env = PHCPufferEnv(EnvConfig(num_envs=128, seed=8), motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
+        torch.manual_seed(0)
+        policy = Policy(PHCPolicy(env, hidden_size=256, layer_sizes=(256, 256))).to(DEV)
+        cfg = TrainConfig(batch_size=128 * 16, minibatch_size=128 * 8, bptt_horizon=8, checkpoint_interval=10 ** 9,
+                          fused_obs_operand=fused_op)
+        comps, info, _ = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+        out = []
+        for _ in range(2):
+            clean_pufferl.evaluate(comps, info)
+            e = comps.experience
+            out.append((e.obs.clone(), e.actions.clone(), e.logprobs.clone(), e.values.clone()))
+            policy.policy.update_obs_rms(e.obs)
+        assert (comps.rollout.opnd is not None) == fused_op
+        runs.append(out)
+    for (a, b) in zip(*runs):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)

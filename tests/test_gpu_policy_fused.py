@@ -54,7 +54,8 @@ def _heads(H, A, g):
 
 @pytest.mark.parametrize("rows,H", [(4096, 512), (37, 512), (50, 256), (33, 1024)])
 @pytest.mark.parametrize("deterministic", [False, True])
-def test_policy_act_vs_torch(rows, H, deterministic):
+@pytest.mark.parametrize("transposed", [False, True], ids=["w_mu", "w_mu_t"])
+def test_policy_act_vs_torch(rows, H, deterministic, transposed):
     from puffer_phc_amd import _native as N
 
     A = 69
@@ -67,8 +68,12 @@ def test_policy_act_vs_torch(rows, H, deterministic):
     logprob = torch.empty(rows, device=DEV)
     value = torch.empty(rows, device=DEV)
     std_max = 1e-6 if deterministic else float("inf")
+    w_mu_t = None
+    if transposed:  # the rollout's layout: W_mu^T in a [H, 72] buffer (coalesced reads across actions)
+        w_mu_t = torch.zeros((H, 72), device=DEV)[:, :A]
+        w_mu_t.copy_(w_mu.t())
     N.policy_act(y, ln_a, ln_c, 1e-5, w_mu, b_mu, w_v, b_v, sigma, noise, actions, logprob, value, mu=mu,
-                 std_max=std_max)
+                 std_max=std_max, w_mu_t=w_mu_t)
     prev = torch.get_float32_matmul_precision()
     torch.set_float32_matmul_precision("highest")
     try:
@@ -100,13 +105,16 @@ def test_policy_act_is_deterministic():
     y = torch.randn((2, rows, H), device=DEV, generator=g)
     args = _heads(H, A, g)
     noise = torch.randn((rows, A), device=DEV, generator=g)
-    outs = []
-    for _ in range(2):
-        o = (torch.empty((rows, A), device=DEV), torch.empty(rows, device=DEV), torch.empty(rows, device=DEV))
-        N.policy_act(y, *args[:2], 1e-5, *args[2:], noise, *o)
-        outs.append(o)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    w_mu_t = torch.zeros((H, 72), device=DEV)[:, :A]
+    w_mu_t.copy_(args[2].t())
+    for wt in (None, w_mu_t):
+        outs = []
+        for _ in range(2):
+            o = (torch.empty((rows, A), device=DEV), torch.empty(rows, device=DEV), torch.empty(rows, device=DEV))
+            N.policy_act(y, *args[:2], 1e-5, *args[2:], noise, *o, w_mu_t=wt)
+            outs.append(o)
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
 
 
 class _Env:
