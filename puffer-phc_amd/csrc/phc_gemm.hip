@@ -55,6 +55,24 @@ constexpr int kGBK = 64;
 #ifndef PHC_GEMM_SPLIT_DMA
 #define PHC_GEMM_SPLIT_DMA 2
 #endif
+// measurement builds only (tools/build_variants.sh): 1 = every tile stages the operand panels of
+// tile (0, 0) (L2-hot operands, same instruction stream); 2 = only the first K-tile is staged (LDS
+// fragment reads + MFMA, no operand traffic)
+#ifndef PHC_GEMM_PROBE
+#define PHC_GEMM_PROBE 0
+#endif
+// 256 x 256 tiles: the second wave of every SIMD (waves 4-7) issues its share of the next K-tile's
+// DMA at MFMA groups PHC_GEMM_STG_A / _B instead of with waves 0-3, so one wave of each SIMD keeps
+// the matrix pipe fed while the other issues its LDS-DMA (0 = off)
+#ifndef PHC_GEMM_STG
+#define PHC_GEMM_STG 0
+#endif
+#ifndef PHC_GEMM_STG_A
+#define PHC_GEMM_STG_A 1
+#endif
+#ifndef PHC_GEMM_STG_B
+#define PHC_GEMM_STG_B 3
+#endif
 using f4 = __attribute__((ext_vector_type(4))) float;
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using b8 = __attribute__((ext_vector_type(8))) __bf16;
@@ -285,8 +303,10 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
   // the B operand's DMA a quarter K-step after A's on 256 x 256 tiles (measured: -4 % on the
   // minibatch GEMMs); on the short K-steps of 128 x 128 tiles the late B tile is exposed (+25 %)
   constexpr int SPLIT = TL::BM >= 256 ? PHC_GEMM_SPLIT_DMA : 0;
+  constexpr bool kStg = PHC_GEMM_STG && SPLIT && !PHC_GEMM_SPLIT_A && TL::kWaves == 8;
+  const bool late = kStg && __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (!SPLIT && issue) stage(next, wr, 3);
-  if (SPLIT && !PHC_GEMM_SPLIT_A && issue) stage(next, wr, 1);
+  if (SPLIT && !PHC_GEMM_SPLIT_A && issue && !late) stage(next, wr, 1);
   if (SPLIT && PHC_GEMM_SPLIT_A && issue) stage(next, wr, 4);
   const char *ta = rd;
   const char *tb = rd + TL::BM * BK * 2;
@@ -312,7 +332,12 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
       load_a(fa[(q + 1) & 1], s1, p1);
     }
     if (SPLIT && PHC_GEMM_SPLIT_A && issue && q == PHC_GEMM_SPLIT_A * NG / 8) stage(next, wr, 8);
-    if (SPLIT && issue && q == (SPLIT * NG / 8 < NG ? SPLIT * NG / 8 : NG - 1)) stage(next, wr, 2);
+    if (kStg) {
+      if (issue && late && q == PHC_GEMM_STG_A) stage(next, wr, 1);
+      if (issue && q == (late ? PHC_GEMM_STG_B : SPLIT * NG / 8)) stage(next, wr, 2);
+    } else if (SPLIT && issue && q == (SPLIT * NG / 8 < NG ? SPLIT * NG / 8 : NG - 1)) {
+      stage(next, wr, 2);
+    }
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
     if (PHC_GEMM_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -539,7 +564,12 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
 
   {
   const int kt_n = g.k / TL::BK;
+  const int64_t m0_ = m0;
+  const int n0_ = n0;
   auto stage = [&](int kt, char *st, int parts = 3) {  // parts: 1 = A tile, 2 = B tile, 4 / 8 = A halves
+    if (PHC_GEMM_PROBE == 2 && kt > 0) return;
+    const int64_t m0 = PHC_GEMM_PROBE == 1 ? 0 : m0_;
+    const int n0 = PHC_GEMM_PROBE == 1 ? 0 : n0_;
     if (parts & 1) stage_tile<BM, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
     if (parts & 4) stage_tile<BM / 2, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
     if (parts & 8)

@@ -133,8 +133,11 @@ __global__ __launch_bounds__(kBlock) void k_motion_state(LibView l, const int64_
 // into the sim buffers (_set_env_state, humanoid_phc.py:899-929), counters cleared
 // (_reset_env_tensors :745-778) and offsets cleared (_reset_ref_state_init :692-729).
 // Returns this lane's new rigid-body record; the caller then computes the obs at dt + mt.
+// rec_stage non-null: the rigid-body record goes to the caller's staging slot (k_env_step's per-wave
+// region, written out after) instead of rigid_body_state
 __device__ __forceinline__ BodyRec reset_env_state(const EnvView &e, const LibView &l, int64_t env, int lane,
-                                                   const MotionScalars &m, float u, float *mt_out) {
+                                                   const MotionScalars &m, float u, float *mt_out,
+                                                   float *rec_stage = nullptr) {
   const bool active = lane < kBodies;
   const int b = active ? lane : 0;
   const float fps_step = 1.0f / 30.0f;  // motion_lib.py:532 curr_fps
@@ -143,7 +146,7 @@ __device__ __forceinline__ BodyRec reset_env_state(const EnvView &e, const LibVi
   const Blend bl = frame_blend(mt, m);
   const BodyRec s = ref_body(l.frames, bl, b, &go_old);
   if (active) {
-    store_body(e.rb + (env * kBodies + b) * kRec, s);
+    store_body(rec_stage ? rec_stage : e.rb + (env * kBodies + b) * kRec, s);
     if (b == 0 && e.root) store_body(e.root + env * kRec, s);
     if (b >= 1) {
       const v3 dp = ref_dof_pos(l.local_rot, bl, b);
@@ -466,9 +469,9 @@ __device__ __forceinline__ void copy_rows_out(float *__restrict__ dst, const flo
 // the 934 observations zero): 16 B per output chunk, rows of the workgroup's contiguous span
 template <typename T>
 __device__ __forceinline__ void operand_rows_out(const EnvView &e, const float *__restrict__ rows, int64_t env0,
-                                                 int nv) {
+                                                 int nv, int tid, int nthreads) {
   const int chunks = e.opnd_ld / 8;
-  for (int i = threadIdx.x; i < nv * chunks; i += kBlock) {
+  for (int i = tid; i < nv * chunks; i += nthreads) {
     const int rr = i / chunks, c0 = (i - rr * chunks) * 8;
     const float *x = rows + rr * kObs;
     T o[8];
@@ -487,11 +490,69 @@ __device__ __forceinline__ void operand_rows_out(const EnvView &e, const float *
   }
 }
 
+// Per-wave staging of the fused replay step (REPLAY, PHC_ENV_STAGE): each wave (2 envs) moves its
+// envs' four frame rows (t and t+dt blends; 1,248 B each, 16-B aligned in the packed table) into its
+// own LDS region by LDS-DMA — 10 wave-instructions of 1 KiB, fully used 64-B lines — instead of 52
+// scattered 4-B lane loads per body; the lanes read their body's records from LDS.  The same region
+// then holds the envs' observation rows and replayed rigid-body records, written out by the wave as
+// contiguous 16-B stores (the records were 13 scattered 4-B stores per body lane).  Wave-local: no
+// workgroup barrier until the stats row.  9,984 B per wave keeps 4 workgroups per CU (the VGPR limit).
+#ifndef PHC_ENV_STAGE
+#define PHC_ENV_STAGE 1
+#endif
+constexpr int kWaveEnvs = 64 / kGroup;            // 2
+constexpr int kRowF = kBodies * kRec;             // 312 floats: one frame row = one env's records
+constexpr int kRowChunks = kRowF / 4;             // 78 x 16 B
+constexpr int kStWave = kWaveEnvs * 4 * kRowF;    // 2,496 floats per wave
+constexpr int kStRec = kWaveEnvs * kObs;          // records after the wave's obs rows
+constexpr int kStDma = (kWaveEnvs * 4 * kRowChunks + 63) / 64;  // 10 LDS-DMA wave-instructions
+static_assert(kStRec % 4 == 0 && kStRec + kWaveEnvs * kRowF <= kStWave, "obs rows + records fit the rows region");
+
+// the wave's 2 x 4 frame rows into `wreg` ([env][row][312]); fr = this lane's env's frame rows
+__device__ __forceinline__ void stage_frame_rows(const float *__restrict__ frames, float *wreg, const int64_t fr[4],
+                                                 int wl) {
+  int f0[4], f1[4];  // the rows of the wave's envs (lanes 0 and 32), wave-uniform
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f0[k] = __builtin_amdgcn_readlane((int)fr[k], 0);
+    f1[k] = __builtin_amdgcn_readlane((int)fr[k], 32);
+  }
+#pragma unroll
+  for (int i = 0; i < kStDma; ++i) {
+    const int j = i * 64 + wl;
+    if (j >= kWaveEnvs * 4 * kRowChunks) break;  // the last instruction's tail lanes (EXEC-masked) move nothing
+    const bool hi = j >= 4 * kRowChunks;
+    const int rem = hi ? j - 4 * kRowChunks : j;
+    const int rr = rem / kRowChunks, cc = rem - rr * kRowChunks;
+    const int fa = rr == 0 ? f0[0] : (rr == 1 ? f0[1] : (rr == 2 ? f0[2] : f0[3]));
+    const int fb = rr == 0 ? f1[0] : (rr == 1 ? f1[1] : (rr == 2 ? f1[2] : f1[3]));
+    const float *src = frames + (int64_t)(hi ? fb : fa) * kRowF + cc * 4;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)(wreg + i * 256), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's rows have landed (wave-local region)
+}
+
+// `nf` floats from the wave's LDS region to global `dst` by the wave's 64 lanes (16-B stores when
+// both sides are 16-B aligned)
+__device__ __forceinline__ void wave_copy_out(float *__restrict__ dst, const float *src, int nf, int wl) {
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int n4 = nf >> 2;
+    for (int i = wl; i < n4; i += 64) reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(src)[i];
+    for (int i = (n4 << 2) + wl; i < nf; i += 64) dst[i] = src[i];
+  } else {
+    for (int i = wl; i < nf; i += 64) dst[i] = src[i];
+  }
+}
+
 template <bool AUTO, bool REPLAY>
 __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
+  constexpr bool kStage = REPLAY && PHC_ENV_STAGE && PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0;
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
-  __shared__ __attribute__((aligned(16))) float sh_obs[kEnvsPerBlock * kObs];
+  // kStage: one 2,496-float region per wave (frame rows, then obs rows + records); else the
+  // workgroup's 8 obs rows
+  __shared__ __attribute__((aligned(16))) float sh_obs[kStage ? (kBlock / 64) * kStWave : kEnvsPerBlock * kObs];
 #endif
   const int g = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + g;
@@ -519,8 +580,21 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   // one memory round for the sim record and all four reference rows (t and t+dt)
   BodyRec s;
   if (!REPLAY) s = load_body(e.rb + (ei * kBodies + b) * kRec);
-  const RowPair rows0 = load_rows(l.frames, bl0, b);
-  RowPair rows1 = load_rows(l.frames, bl1, b);
+  RowPair rows0, rows1;
+#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
+  float *const wreg = sh_obs + (kStage ? (threadIdx.x >> 6) * kStWave : 0);
+  if constexpr (kStage) {
+    const int64_t fr[4] = {bl0.f0, bl0.f1, bl1.f0, bl1.f1};
+    stage_frame_rows(l.frames, wreg, fr, threadIdx.x & 63);
+    const float *rw = wreg + (g & 1) * (4 * kRowF) + b * kRec;
+    rows0 = {load_body(rw), load_body(rw + kRowF)};
+    rows1 = {load_body(rw + 2 * kRowF), load_body(rw + 3 * kRowF)};
+  } else
+#endif
+  {
+    rows0 = load_rows(l.frames, bl0, b);
+    rows1 = load_rows(l.frames, bl1, b);
+  }
   const BodyRec ref0 = blend_body(rows0.a, rows0.c, bl0.b, &go);
 
   float pw_reg = -1.0f;
@@ -528,7 +602,18 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
     v3 dv, f;
     s = ref0;
     replay_perturb(e, r, ei, b, prog, s, l, bl0, dv, f);
-    if (valid && lane < kBodies) {
+    if constexpr (kStage) {
+#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
+      // the record goes out with the wave's rows at the end; dof vel / force and the PD map here
+      if (lane < kBodies) store_body(wreg + kStRec + (g & 1) * kRowF + b * kRec, s);
+      if (valid && b >= 1) {
+        float *d = e.dof_state + (ei * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+        d[1] = dv.x; d[3] = dv.y; d[5] = dv.z;
+        float *fo = const_cast<float *>(e.dof_force) + ei * PHC_NUM_DOF + 3 * (b - 1);
+        fo[0] = f.x; fo[1] = f.y; fo[2] = f.z;
+      }
+#endif
+    } else if (valid && lane < kBodies) {
       store_replay(e, ei, b, s, dv, f);
       map_actions(r, ei, b);
     }
@@ -549,7 +634,11 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   v3 off1 = go;
   if (AUTO && valid && o.reset) {  // uniform per half-wave
     float mt;
-    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0), &mt);
+    float *rec_stage = nullptr;
+#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
+    if (kStage) rec_stage = wreg + kStRec + (g & 1) * kRowF + b * kRec;
+#endif
+    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0), &mt, rec_stage);
     if (lane == 0) {
       reset_env_counters(e, ei, mt);
       if (e.rng) e.rng[ei] += 1u;
@@ -569,7 +658,8 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
     e.obs[ei * kObs + lane] = r1.p.x + r1.r.w + r1.v.y + r1.av.z + s.p.x;
   }
 #elif PHC_ENV_OBS_LDS
-  env_obs_row(sh_obs + g * kObs, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
+  env_obs_row(kStage ? wreg + (g & 1) * kObs : sh_obs + g * kObs, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1),
+              valid);
 #else
   env_obs_ref(e, ei, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
 #endif
@@ -579,6 +669,32 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
     for (int k = 0; k < 10; ++k) sh_stats[g][k] = st_row[k];
   }
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
+  if constexpr (kStage) {
+    // the wave writes out its envs' rows (LDS operations of one wave complete in order: the lanes'
+    // row writes above are visible to the copy without a barrier)
+    const int wl = threadIdx.x & 63;
+    const int64_t env0 = (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6) * kWaveEnvs;
+    const int64_t left = e.n - env0;
+    const int nv = left <= 0 ? 0 : (left < kWaveEnvs ? (int)left : kWaveEnvs);
+    if (nv > 0) {
+      wave_copy_out(e.obs + env0 * kObs, wreg, nv * kObs, wl);
+      wave_copy_out(e.rb + env0 * kRowF, wreg + kStRec, nv * kRowF, wl);
+      if (r.actions) {  // R13 for the wave's envs, elementwise over their contiguous [nv, 69] span
+        const float *a = r.actions + env0 * PHC_NUM_DOF;
+        float *pd = r.pd + env0 * PHC_NUM_DOF;
+        for (int i = wl; i < nv * PHC_NUM_DOF; i += 64) {
+          const int d = i >= PHC_NUM_DOF ? i - PHC_NUM_DOF : i;
+          pd[i] = action_to_pd(a[i], d, r.off, r.scale, r.frozen, r.clip);
+        }
+      }
+      if (e.opnd) {
+        if (e.opnd_bf16) operand_rows_out<__bf16>(e, wreg, env0, nv, wl, 64);
+        else operand_rows_out<_Float16>(e, wreg, env0, nv, wl, 64);
+      }
+    }
+    if (e.stats) flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
+    return;
+  }
   __syncthreads();  // the staged rows and the stats rows are complete
   {
     const int64_t env0 = (int64_t)blockIdx.x * kEnvsPerBlock;
@@ -586,8 +702,8 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
     const int nv = left < kEnvsPerBlock ? (int)left : kEnvsPerBlock;
     copy_rows_out(e.obs + env0 * kObs, sh_obs, nv * kObs);
     if (e.opnd) {
-      if (e.opnd_bf16) operand_rows_out<__bf16>(e, sh_obs, env0, nv);
-      else operand_rows_out<_Float16>(e, sh_obs, env0, nv);
+      if (e.opnd_bf16) operand_rows_out<__bf16>(e, sh_obs, env0, nv, threadIdx.x, kBlock);
+      else operand_rows_out<_Float16>(e, sh_obs, env0, nv, threadIdx.x, kBlock);
     }
   }
   if (e.stats) flush_stats<kEnvsPerBlock, false>(e, sh_stats, st_prev);

@@ -174,5 +174,7 @@ def test_rollout_graph_sees_optimizer_updates():
     assert not torch.equal(v0, v1) and not torch.equal(a0, a1)
     assert torch.equal(v1, val) and torch.equal(a1, act)
     # the mu head reads its 16-B aligned copy (float4 loads), refreshed with the trunk operands
-    assert inner._w_mu_aligned.data_ptr() % 16 == 0
-    assert torch.equal(inner._w_mu_aligned, inner.mu[0].weight.detach())
+    # (the transposed [hidden, actions] copy with a 16-B aligned row stride: the rollout tail's
+    # weight loads coalesce across the actions)
+    assert inner._w_mu_aligned.data_ptr() % 16 == 0 and inner._w_mu_aligned.stride(0) % 4 == 0
+    assert torch.equal(inner._w_mu_aligned, inner.mu[0].weight.detach().t())
