@@ -514,6 +514,11 @@ def main():
     if rank == 0:
         fused = bool(getattr(env.env, "fused_env_step", False)) and args.physics == "replay"
         env_bytes = BYTES_PER_ENV_STEP_FUSED if fused else BYTES_PER_ENV_STEP
+        # the rollout's fused RunningNorm operand (HumanoidPHC.set_obs_operand): the step also writes
+        # the policy's [N, ld] half-precision first-GEMM operand row of every env
+        opnd = getattr(env.env, "_obs_operand", None)
+        opnd_bytes = int(opnd[0].shape[1] * opnd[0].element_size()) if opnd is not None else 0
+        env_bytes += opnd_bytes
         achieved = env_bytes * args.envs / kern_s / 1e9
         traffic = None
         tf = args.traffic_file or os.path.join(ROOT, "profiles", f"traffic_{'fused_' if fused else ''}{args.envs}.json")
@@ -581,7 +586,7 @@ def main():
                     "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     "kernel_us": kern_s * 1e6, "launches_timed": env_steps, "launches_in_region": env_offered,
-                    "algorithmic_bytes_per_env_step": env_bytes}
+                    "algorithmic_bytes_per_env_step": env_bytes, "obs_operand_bytes_per_env_step": opnd_bytes}
         if gemm_launches:
             # the dominant kernel of the PPO / rollout modes: the trunk GEMMs (MFMA-bound)
             tfs = gemm_flops / gemm_s / 1e12

@@ -196,7 +196,7 @@ class TrainConfig(DeviceConfig):
     precision: str = "fp16"
     # replay policy inference + experience store of each rollout step from a captured hipGraph
     # (the env step itself stays eager); False = the reference's eager loop
-    rollout_graph: bool = True
+    rollout_graph: bool = os.environ.get("PHC_ROLLOUT_GRAPH", "1") == "1"
     # PPO objective (ratio / clipping / value / bound losses and their gradients) in two HIP
     # kernels (clean_pufferl/ppo_loss.py); False = the reference's eager expression
     fused_loss: bool = True

@@ -50,10 +50,23 @@ __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x);
 #define PHC_PHYS_WAVES_PER_SIMD 2  // occupancy pinned (min = max): 3 waves per SIMD measured slower at 16384 envs
 #endif
 
+#ifndef PHC_PHYS_WAVESYNC
+#define PHC_PHYS_WAVESYNC 1  // single-wave workgroups: LDS hand-offs ordered without the workgroup barrier
+#endif
+
 constexpr int kModel = PHC_BODY_MODEL_STRIDE;
 constexpr int kPhysEnvs = PHC_PHYS_EPB;
 constexpr int kPhysBlock = kPhysEnvs * kGroup;
 constexpr int kSlot = 27;  // LDS floats per body: A(6, sym) B(9) M(6, sym) f(6)
+
+// The hand-offs between the tree levels (and the table / pair-list / self-contact exchanges) go
+// through LDS between the lanes of ONE wave (one workgroup = one wave of 2 envs): a wave's LDS
+// operations are performed in issue order, so a compiler barrier suffices to order them — the
+// workgroup barrier's s_waitcnt lgkmcnt(0) drain (~29 per substep) stalled the wave each time.
+__device__ __forceinline__ void phys_sync() {
+  if constexpr (PHC_PHYS_WAVESYNC && kPhysBlock == 64) asm volatile("" ::: "memory");
+  else __syncthreads();
+}
 constexpr int kMaxPoints = 8;
 
 struct PhysConsts {
@@ -313,7 +326,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     for (int k = 0; k < 7; ++k) t[T_SEG + k] = md[64 + k];
     t[T_MASK] = c.self_col ? md[71] : 0.0f;
   }
-  __syncthreads();
+  phys_sync();
   // the pair list (identical for every env): body t's partners j > t at offset = the pair counts
   // of the bodies before it
   if (threadIdx.x < kBodies) {
@@ -329,7 +342,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     }
     if (t == kBodies - 1) npairs_s = off;
   }
-  __syncthreads();
+  phys_sync();
   const int npairs = npairs_s;
   const float *T = tab + b * kTab;
   const int parent = (int)T[T_PARENT];
@@ -400,7 +413,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         s[7] = w.x; s[8] = w.y; s[9] = w.z;
         s[10] = v.x; s[11] = v.y; s[12] = v.z;
       }
-      __syncthreads();
+      phys_sync();
     }
   };
 
@@ -435,7 +448,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
 #pragma unroll
           for (int k = 0; k < 6; ++k) fsc[sub][b][k] = 0.0f;
         }
-        __syncthreads();
+        phys_sync();
         // each of the env's 32 lanes takes every 32nd pair: broad phase on the bounding spheres,
         // narrow phase (clamped segment-segment closest points) on the overlapping ones, the
         // equal and opposite contact forces added into both bodies' LDS wrench slots (world
@@ -493,13 +506,13 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
             atomicAdd(wj + 3, -Fi.x); atomicAdd(wj + 4, -Fi.y); atomicAdd(wj + 5, -Fi.z);
           }
         }
-        __syncthreads();
+        phys_sync();
         if (act) {  // this body's accumulated contact wrench, to body coordinates
           const float *ws = fsc[sub][b];
           fn_ = vadd(fn_, m3_tv(R, ld3(ws)));
           ff = vadd(ff, m3_tv(R, ld3(ws + 3)));
         }
-        __syncthreads();  // segw / fsc are rewritten next substep
+        phys_sync();  // segw / fsc are rewritten next substep
       }
       const v3 zb = {R.m[6], R.m[7], R.m[8]};  // R^T z
       const int npts = (int)T[T_NPTS];
@@ -604,7 +617,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         s[21] = Np.x; s[22] = Np.y; s[23] = Np.z;
         s[24] = Fp.x; s[25] = Fp.y; s[26] = Fp.z;
       }
-      __syncthreads();
+      phys_sync();
     }
     // ---- floating root: a0 = -IA^-1 pA (6x6 Cholesky on lane 0)
     v3 aw = {0.0f, 0.0f, 0.0f}, av = {0.0f, 0.0f, 0.0f};
@@ -656,7 +669,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       float *s = S[0];
       s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
     }
-    __syncthreads();
+    phys_sync();
     // ---- outward pass: a' = X a_parent + c, qdd = y - K a'_w - L a'_v, a = a' + [qdd; 0]
     v3 qdd = {0.0f, 0.0f, 0.0f};
     for (int L = 1; L <= depth; ++L) {
@@ -672,7 +685,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         float *s = S[b];
         s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
       }
-      __syncthreads();
+      phys_sync();
     }
     // ---- semi-implicit Euler
     if (act && b > 0) {

@@ -244,8 +244,9 @@ struct ReplayArgs {
 // has RNG counters, by the env's episode (rng_counter) and step (progress): no per-step host value,
 // so a captured graph replays fresh noise every step.  Body b >= 1 also gets its dof velocities
 // (reference + noise) and forces (noise), returned in dv / f.
+// dv_ref: body b's reference dof velocities at the blend (ref_dof_vel; the caller loads them early)
 __device__ __forceinline__ void replay_perturb(const EnvView &e, const ReplayArgs &r, int64_t env, int b, int prog,
-                                               BodyRec &s, const LibView &l, const Blend &bl, v3 &dv, v3 &f) {
+                                               BodyRec &s, v3 dv_ref, v3 &dv, v3 &f) {
   const float sigma = r.sigma;
   unsigned long long key = r.seed ^ mix64(r.counter);
   if (e.rng) key ^= mix64(((unsigned long long)e.rng[env] << 20) ^ (unsigned long long)(unsigned)prog ^ 0x5bd1e995ull);
@@ -272,7 +273,7 @@ __device__ __forceinline__ void replay_perturb(const EnvView &e, const ReplayArg
   dv = {0.0f, 0.0f, 0.0f};
   f = {0.0f, 0.0f, 0.0f};
   if (b >= 1) {
-    dv = ref_dof_vel(l.dof_vel, bl, b);
+    dv = dv_ref;
     h = mix64(base + 7);
     dv.x = dv.x + tri_noise(h, 0, 10.0f * sigma);
     dv.y = dv.y + tri_noise(h, 1, 10.0f * sigma);
@@ -545,6 +546,41 @@ __device__ __forceinline__ void wave_copy_out(float *__restrict__ dst, const flo
   }
 }
 
+// the same for one wave's nv <= 2 staged rows: lane l owns output chunks l, l + 64, ..., so each
+// column's mean and sqrt(var + eps) are loaded / computed once per lane for both rows (same
+// expression, bit-identical values)
+template <typename T>
+__device__ __forceinline__ void operand_rows_out_wave(const EnvView &e, const float *__restrict__ rows, int64_t env0,
+                                                      int nv, int wl) {
+  const int chunks = e.opnd_ld / 8;
+  for (int ch = wl; ch < chunks; ch += 64) {
+    const int c0 = ch * 8;
+    float mv[8], dv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool in = c0 + q < kObs;
+      mv[q] = in ? e.opnd_mean[c0 + q] : 0.0f;
+      dv[q] = in ? sqrtf(e.opnd_var[c0 + q] + e.opnd_eps) : 1.0f;
+    }
+    for (int rr = 0; rr < nv; ++rr) {
+      const float *x = rows + rr * kObs;
+      T o[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float v = 0.0f;
+        if (c0 + q < kObs) {
+          v = (x[c0 + q] - mv[q]) / dv[q];
+          v = v < -e.opnd_clip ? -e.opnd_clip : (v > e.opnd_clip ? e.opnd_clip : v);
+        }
+        o[q] = (T)v;
+      }
+      uint4 raw;
+      __builtin_memcpy(&raw, o, sizeof(raw));
+      *reinterpret_cast<uint4 *>(static_cast<T *>(e.opnd) + (env0 + rr) * e.opnd_ld + c0) = raw;
+    }
+  }
+}
+
 template <bool AUTO, bool REPLAY>
 __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
@@ -566,6 +602,24 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
 #endif
 
   const double st_prev = stats_prefetch(e);
+  // kStage: R13 for the wave's envs first (elementwise over their contiguous [nv, 69] action span,
+  // independent of everything else: its loads join the first memory round)
+#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
+  if constexpr (kStage) {
+    if (r.actions) {
+      const int wl = threadIdx.x & 63;
+      const int64_t env0 = (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6) * kWaveEnvs;
+      const int64_t left = e.n - env0;
+      const int nv = left <= 0 ? 0 : (left < kWaveEnvs ? (int)left : kWaveEnvs);
+      const float *a = r.actions + env0 * PHC_NUM_DOF;
+      float *pd = r.pd + env0 * PHC_NUM_DOF;
+      for (int i = wl; i < nv * PHC_NUM_DOF; i += 64) {
+        const int d = i >= PHC_NUM_DOF ? i - PHC_NUM_DOF : i;
+        pd[i] = action_to_pd(a[i], d, r.off, r.scale, r.frozen, r.clip);
+      }
+    }
+  }
+#endif
   // per-env scalars (broadcast loads: every lane of the half-wave reads the same word)
   const int prog = (int)e.progress[ei] + 1;
   const float st = e.start[ei];
@@ -581,6 +635,9 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   BodyRec s;
   if (!REPLAY) s = load_body(e.rb + (ei * kBodies + b) * kRec);
   RowPair rows0, rows1;
+  // the replay's reference dof velocities: loaded before the row DMA's wait, in the same memory round
+  v3 dv_ref = {0.0f, 0.0f, 0.0f};
+  if (REPLAY && b >= 1) dv_ref = ref_dof_vel(l.dof_vel, bl0, b);
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
   float *const wreg = sh_obs + (kStage ? (threadIdx.x >> 6) * kStWave : 0);
   if constexpr (kStage) {
@@ -601,7 +658,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   if (REPLAY) {
     v3 dv, f;
     s = ref0;
-    replay_perturb(e, r, ei, b, prog, s, l, bl0, dv, f);
+    replay_perturb(e, r, ei, b, prog, s, dv_ref, dv, f);
     if constexpr (kStage) {
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
       // the record goes out with the wave's rows at the end; dof vel / force and the PD map here
@@ -679,17 +736,9 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
     if (nv > 0) {
       wave_copy_out(e.obs + env0 * kObs, wreg, nv * kObs, wl);
       wave_copy_out(e.rb + env0 * kRowF, wreg + kStRec, nv * kRowF, wl);
-      if (r.actions) {  // R13 for the wave's envs, elementwise over their contiguous [nv, 69] span
-        const float *a = r.actions + env0 * PHC_NUM_DOF;
-        float *pd = r.pd + env0 * PHC_NUM_DOF;
-        for (int i = wl; i < nv * PHC_NUM_DOF; i += 64) {
-          const int d = i >= PHC_NUM_DOF ? i - PHC_NUM_DOF : i;
-          pd[i] = action_to_pd(a[i], d, r.off, r.scale, r.frozen, r.clip);
-        }
-      }
       if (e.opnd) {
-        if (e.opnd_bf16) operand_rows_out<__bf16>(e, wreg, env0, nv, wl, 64);
-        else operand_rows_out<_Float16>(e, wreg, env0, nv, wl, 64);
+        if (e.opnd_bf16) operand_rows_out_wave<__bf16>(e, wreg, env0, nv, wl);
+        else operand_rows_out_wave<_Float16>(e, wreg, env0, nv, wl);
       }
     }
     if (e.stats) flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
@@ -724,7 +773,7 @@ __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l,
   const v3 go = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
   BodyRec s = ref_body(l.frames, bl, b, &go);
   v3 dv, f;
-  replay_perturb(e, r, env, b, prog, s, l, bl, dv, f);
+  replay_perturb(e, r, env, b, prog, s, b >= 1 ? ref_dof_vel(l.dof_vel, bl, b) : v3{0.0f, 0.0f, 0.0f}, dv, f);
   store_replay(e, env, b, s, dv, f);
 }
 

@@ -12,4 +12,5 @@ done
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/trace_ppo" -o run --output-format csv -- \
   python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/trace_ppo.log" 2>&1 || { tail -5 "$O/trace_ppo.log"; exit 6; }
 f=$(find "$O/trace_ppo" -name "*kernel_stats.csv" | head -1); cp "$f" "$O/ppo_4096_kernel_stats.csv"
+t=$(find "$O/trace_ppo" -name "*kernel_trace.csv" | head -1); python tools/glue_kernels.py "$t" 2 > "$O/glue.txt" 2>&1 || true
 head -25 "$O/ppo_4096_kernel_stats.csv" | cut -d, -f1-6
