@@ -521,7 +521,10 @@ def main():
         env_bytes += opnd_bytes
         achieved = env_bytes * args.envs / kern_s / 1e9
         traffic = None
-        tf = args.traffic_file or os.path.join(ROOT, "profiles", f"traffic_{'fused_' if fused else ''}{args.envs}.json")
+        # HBM bytes of the env step from the committed PMC passes: the rollout-context launch (fused
+        # operand written) has its own file (tools/r04_final.sh)
+        kind = ("fused_ppo_" if opnd_bytes else "fused_") if fused else ""
+        tf = args.traffic_file or os.path.join(ROOT, "profiles", f"traffic_{kind}{args.envs}.json")
         if os.path.exists(tf):
             with open(tf) as f:
                 traffic = json.load(f).get("bytes_per_launch")
