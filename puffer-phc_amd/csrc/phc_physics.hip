@@ -50,6 +50,9 @@ __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x);
 #define PHC_PHYS_WAVES_PER_SIMD 2  // occupancy pinned (min = max): 3 waves per SIMD measured slower at 16384 envs
 #endif
 
+#ifndef PHC_PHYS_COMPACT
+#define PHC_PHYS_COMPACT 1  // self-collision: narrow phase over the compacted broad-phase hits
+#endif
 #ifndef PHC_PHYS_WAVESYNC
 #define PHC_PHYS_WAVESYNC 1  // single-wave workgroups: LDS hand-offs ordered without the workgroup barrier
 #endif
@@ -283,6 +286,9 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
   float(*segw)[kBodies][kSeg] = reinterpret_cast<float(*)[kBodies][kSeg]>(&outw[0][0][0]);
   __shared__ float fsc[kPhysEnvs][kBodies][6];  // self-contact wrench per body (world torque, force)
   __shared__ unsigned short pairs[kBodies * (kBodies - 1) / 2];  // colliding pairs i | j << 5, i < j
+#if PHC_PHYS_COMPACT
+  __shared__ unsigned short hits[kPhysEnvs][kBodies * (kBodies - 1) / 2];  // this substep's broad-phase hits
+#endif
   __shared__ int npairs_s;
   const int lane = threadIdx.x % kGroup, sub = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kPhysEnvs + sub;
@@ -453,6 +459,37 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         // narrow phase (clamped segment-segment closest points) on the overlapping ones, the
         // equal and opposite contact forces added into both bodies' LDS wrench slots (world
         // force, world torque about the body origin)
+#if PHC_PHYS_COMPACT
+        // broad phase over every pair, the overlapping ones compacted into the env's LDS hit list
+        // (wave ballot + prefix counts, no atomics); then the narrow phase over the hits only, spread
+        // over the env's lanes — one masked narrow-phase pass per 32 hits instead of one per pair
+        // iteration with any hit
+        int nh = 0;  // this env's hits (uniform per half-wave)
+        {
+          const int wl = threadIdx.x & 63;
+          const unsigned long long half = (wl >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+          const unsigned long long below = (1ull << wl) - 1ull;
+          for (int q0 = 0; q0 < npairs; q0 += kGroup) {  // npairs is block-uniform: every lane runs the ballots
+            const int q = q0 + lane;
+            bool hit = false;
+            if (env < e.n && q < npairs) {
+              const int pr = pairs[q], bi = pr & 31, bj = pr >> 5;
+              const float4 bsi = *reinterpret_cast<const float4 *>(segw[sub][bi]);
+              const float4 bsj = *reinterpret_cast<const float4 *>(segw[sub][bj]);
+              const float bx = bsj.x - bsi.x, by = bsj.y - bsi.y, bz = bsj.z - bsi.z, br = bsi.w + bsj.w;
+              hit = bx * bx + by * by + bz * bz <= br * br;
+            }
+            const unsigned long long m = __ballot(hit) & half;
+            if (hit) hits[sub][nh + __popcll(m & below)] = (unsigned short)q;
+            nh += __popcll(m);
+          }
+        }
+        phys_sync();  // the hit list is written (one wave: LDS operations in issue order)
+        if (env < e.n) {
+          for (int t = lane; t < nh; t += kGroup) {
+            const int pr = pairs[hits[sub][t]], bi = pr & 31, bj = pr >> 5;
+            const float *oi = segw[sub][bi], *oj = segw[sub][bj];
+#else
         if (env < e.n) {
           for (int q = lane; q < npairs; q += kGroup) {
             const int pr = pairs[q], bi = pr & 31, bj = pr >> 5;
@@ -460,6 +497,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
             const float4 bsi = *reinterpret_cast<const float4 *>(oi), bsj = *reinterpret_cast<const float4 *>(oj);
             const float bx = bsj.x - bsi.x, by = bsj.y - bsi.y, bz = bsj.z - bsi.z, br = bsi.w + bsj.w;
             if (bx * bx + by * by + bz * bz > br * br) continue;
+#endif
             const v3 p0 = ld3(oi + 4), d1 = ld3(oi + 7), q0 = ld3(oj + 4), d2 = ld3(oj + 7);
             const float ri = oi[10], rj = oj[10];
             const v3 r0 = vsub(p0, q0);

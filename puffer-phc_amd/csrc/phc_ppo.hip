@@ -70,7 +70,23 @@ __global__ __launch_bounds__(kPpoBlock) void k_ppo_fwd(PpoArgs p, float *__restr
                                  (act_ok[1] ? 0.5f + kLogSqrt2Pi + ls[1] : 0.0f));
   const float b = p.c.soft_bound;
   float lp = 0.0f, bound = 0.0f;
-#pragma unroll 4
+  // every load of the wave's rows first, unconditionally (clamped indices, masked below): a load
+  // behind a per-row condition makes hipcc branch around it and wait vmcnt(0) per row
+  float mv[kPpoWaveRows][2], av[kPpoWaveRows][2];
+#pragma unroll
+  for (int i = 0; i < kPpoWaveRows; ++i) {
+    const int64_t row = rbase + i < p.m ? rbase + i : p.m - 1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = act_ok[h] ? lane + 64 * h : 0;
+      mv[i][h] = p.mu[row * p.a + j];
+      av[i][h] = p.actions[row * p.a + j];
+    }
+  }
+  const int64_t rr = r < p.m ? r : p.m - 1;  // this lane's row of the tail below (lanes < kPpoWaveRows)
+  const float r_old_lp = p.old_logprob[rr], r_adv = p.adv[rr], r_v = p.value[rr], r_ret = p.returns[rr];
+  const float r_old_v = p.old_value[rr];
+#pragma unroll
   for (int i = 0; i < kPpoWaveRows; ++i) {
     const int64_t row = rbase + i;
     const bool row_ok = row < p.m;  // wave-uniform
@@ -78,9 +94,8 @@ __global__ __launch_bounds__(kPpoBlock) void k_ppo_fwd(PpoArgs p, float *__restr
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (!act_ok[h] || !row_ok) continue;
-      const int j = lane + 64 * h;
-      const float m = p.mu[row * p.a + j];
-      const float d = p.actions[row * p.a + j] - m;
+      const float m = mv[i][h];
+      const float d = av[i][h] - m;
       tl += -(d * d) / (2.0f * var[h]) - ls[h] - kLogSqrt2Pi;
       tb += m > b ? (m - b) * (m - b) : (m < -b ? (m + b) * (m + b) : 0.0f);
     }
@@ -95,21 +110,21 @@ __global__ __launch_bounds__(kPpoBlock) void k_ppo_fwd(PpoArgs p, float *__restr
 #pragma unroll
   for (int k = 0; k < kPpoStats; ++k) s[k] = 0.0f;
   if (lane < kPpoWaveRows && r < p.m) {
-    const float logratio = lp - p.old_logprob[r];
+    const float logratio = lp - r_old_lp;
     const float ratio = expf(logratio);
-    const float A = (p.adv[r] - p.adv_mean_std[0]) / (p.adv_mean_std[1] + 1e-8f);
+    const float A = (r_adv - p.adv_mean_std[0]) / (p.adv_mean_std[1] + 1e-8f);
     const float lo = 1.0f - p.c.clip_coef, hi = 1.0f + p.c.clip_coef;
     const float t1 = -A * ratio, t2 = -A * clampf(ratio, lo, hi);
     float g1, g2;
     dmax(t1, t2, &g1, &g2);
     const float inside = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
     const float dpg_dratio = -A * g1 + -A * inside * g2;  // per row, before the 1/M of the mean
-    const float v = p.value[r], ret = p.returns[r];
+    const float v = r_v, ret = r_ret;
     float vl, dv;
     if (p.c.clip_vloss) {
       const float vu = (v - ret) * (v - ret);
-      const float dvv = v - p.old_value[r];
-      const float vcl = p.old_value[r] + clampf(dvv, -p.c.vf_clip_coef, p.c.vf_clip_coef);
+      const float dvv = v - r_old_v;
+      const float vcl = r_old_v + clampf(dvv, -p.c.vf_clip_coef, p.c.vf_clip_coef);
       const float vc = (vcl - ret) * (vcl - ret);
       float gu, gc;
       dmax(vu, vc, &gu, &gc);

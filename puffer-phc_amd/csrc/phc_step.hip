@@ -168,10 +168,12 @@ __device__ __forceinline__ void reset_env_counters(const EnvView &e, int64_t env
   e.start_off[env] = 0.0f;
 }
 
+// rng_val: the env's rng counter e.rng[env], read by the caller (k_env_step loads it in its first
+// memory round)
 __device__ __forceinline__ float reset_draw(const EnvView &e, int64_t env, unsigned long long seed,
-                                            unsigned long long counter, bool at_start) {
+                                            unsigned long long counter, bool at_start, uint32_t rng_val) {
   if (at_start) return 0.0f;  // StateInit.Start / flag_test: motion_times[:] = 0
-  const unsigned long long ctr = e.rng ? (unsigned long long)e.rng[env] : counter;
+  const unsigned long long ctr = e.rng ? (unsigned long long)rng_val : counter;
   return uniform01(seed, ctr, (unsigned long long)env);
 }
 
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, Ste
   if (env >= e.n) return;
   if (!(mask ? mask[env] : e.reset[env])) return;  // uniform per half-wave
   const MotionScalars m = load_motion(l, e.motion_ids[env]);
-  const float u = phase ? phase[env] : reset_draw(e, env, seed, counter, c.reset_at_start != 0);
+  const float u = phase ? phase[env] : reset_draw(e, env, seed, counter, c.reset_at_start != 0, e.rng ? e.rng[env] : 0u);
   float mt;
   const BodyRec s = reset_env_state(e, l, env, lane, m, u, &mt);
   // obs of the reset env: progress 0, start = mt, offsets 0 (humanoid_phc.py:1061-1065)
@@ -246,10 +248,10 @@ struct ReplayArgs {
 // (reference + noise) and forces (noise), returned in dv / f.
 // dv_ref: body b's reference dof velocities at the blend (ref_dof_vel; the caller loads them early)
 __device__ __forceinline__ void replay_perturb(const EnvView &e, const ReplayArgs &r, int64_t env, int b, int prog,
-                                               BodyRec &s, v3 dv_ref, v3 &dv, v3 &f) {
+                                               BodyRec &s, v3 dv_ref, v3 &dv, v3 &f, uint32_t rng_val) {
   const float sigma = r.sigma;
   unsigned long long key = r.seed ^ mix64(r.counter);
-  if (e.rng) key ^= mix64(((unsigned long long)e.rng[env] << 20) ^ (unsigned long long)(unsigned)prog ^ 0x5bd1e995ull);
+  if (e.rng) key ^= mix64(((unsigned long long)rng_val << 20) ^ (unsigned long long)(unsigned)prog ^ 0x5bd1e995ull);
   const unsigned long long base = mix64(key ^ ((unsigned long long)(env * kBodies + b) << 8));
   unsigned long long h = mix64(base + 1);
   s.p.x += tri_noise(h, 0, sigma);
@@ -295,6 +297,13 @@ __device__ __forceinline__ void store_replay(const EnvView &e, int64_t env, int 
     fo[0] = f.x; fo[1] = f.y; fo[2] = f.z;
   }
 }
+
+__device__ const uint8_t kNoFrozen[PHC_NUM_DOF] = {};  // stands in for a null frozen-dof mask
+__device__ const uint32_t kZeroU32 = 0;                 // stands in for a null rng counter array
+// global-address-space views: a select between two pointers otherwise yields a generic pointer,
+// and a flat load forces vmcnt(0) waits on every later use of any load
+typedef const __attribute__((address_space(1))) uint8_t gu8;
+typedef const __attribute__((address_space(1))) uint32_t gu32;
 
 // R13 (clean_pufferl/env.py:91-93, humanoid_phc.py:1216-1226): clip(a, -1, 1) when cfg.clip_actions,
 // pd = offset + scale a, frozen dofs 0
@@ -556,11 +565,19 @@ __device__ __forceinline__ void operand_rows_out_wave(const EnvView &e, const fl
   for (int ch = wl; ch < chunks; ch += 64) {
     const int c0 = ch * 8;
     float mv[8], dv[8];
+    // unconditional loads at clamped columns, selected after: a load behind a per-column select
+    // makes hipcc branch around it and wait vmcnt(0) per load (16 dependent L2 round trips)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int cq = c0 + q < kObs ? c0 + q : kObs - 1;
+      mv[q] = e.opnd_mean[cq];
+      dv[q] = e.opnd_var[cq];
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const bool in = c0 + q < kObs;
-      mv[q] = in ? e.opnd_mean[c0 + q] : 0.0f;
-      dv[q] = in ? sqrtf(e.opnd_var[c0 + q] + e.opnd_eps) : 1.0f;
+      mv[q] = in ? mv[q] : 0.0f;
+      dv[q] = in ? sqrtf(dv[q] + e.opnd_eps) : 1.0f;
     }
     for (int rr = 0; rr < nv; ++rr) {
       const float *x = rows + rr * kObs;
@@ -613,14 +630,37 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
       const int nv = left <= 0 ? 0 : (left < kWaveEnvs ? (int)left : kWaveEnvs);
       const float *a = r.actions + env0 * PHC_NUM_DOF;
       float *pd = r.pd + env0 * PHC_NUM_DOF;
-      for (int i = wl; i < nv * PHC_NUM_DOF; i += 64) {
+      // every load of the span first (clamped indices, a zero row standing in for a null frozen
+      // mask): loads behind a select or a null check made hipcc wait vmcnt(0) per element
+      constexpr int kPdIt = (kWaveEnvs * PHC_NUM_DOF + 63) / 64;
+      const int cnt = nv * PHC_NUM_DOF;
+      gu8 *fz = r.frozen ? (gu8 *)r.frozen : (gu8 *)kNoFrozen;
+      float av[kPdIt], ov[kPdIt], sv[kPdIt];
+      uint8_t fv[kPdIt];
+#pragma unroll
+      for (int u = 0; u < kPdIt; ++u) {
+        const int i = wl + 64 * u < cnt ? wl + 64 * u : cnt - 1;
         const int d = i >= PHC_NUM_DOF ? i - PHC_NUM_DOF : i;
-        pd[i] = action_to_pd(a[i], d, r.off, r.scale, r.frozen, r.clip);
+        av[u] = a[i];
+        ov[u] = r.off[d];
+        sv[u] = r.scale[d];
+        fv[u] = fz[d];
+      }
+#pragma unroll
+      for (int u = 0; u < kPdIt; ++u) {
+        const int i = wl + 64 * u;
+        if (i >= cnt) break;
+        float x = av[u];
+        if (r.clip) x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+        pd[i] = fv[u] ? 0.0f : ov[u] + sv[u] * x;  // action_to_pd's expression
       }
     }
   }
 #endif
-  // per-env scalars (broadcast loads: every lane of the half-wave reads the same word)
+  // per-env scalars (broadcast loads: every lane of the half-wave reads the same word); the rng
+  // counter through a pointer select, so its load joins this round instead of waiting behind a
+  // null check where it is used
+  const uint32_t rng_val = *(e.rng ? (gu32 *)(e.rng + ei) : (gu32 *)&kZeroU32);
   const int prog = (int)e.progress[ei] + 1;
   const float st = e.start[ei];
   const float so = e.start_off[ei];
@@ -635,9 +675,16 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   BodyRec s;
   if (!REPLAY) s = load_body(e.rb + (ei * kBodies + b) * kRec);
   RowPair rows0, rows1;
-  // the replay's reference dof velocities: loaded before the row DMA's wait, in the same memory round
-  v3 dv_ref = {0.0f, 0.0f, 0.0f};
-  if (REPLAY && b >= 1) dv_ref = ref_dof_vel(l.dof_vel, bl0, b);
+  // the replay's reference dof velocity rows: loaded before the row DMA's wait, in the same memory
+  // round, and blended after it (ref_dof_vel's arithmetic)
+  v3 dva = {0.0f, 0.0f, 0.0f}, dvc = {0.0f, 0.0f, 0.0f};
+  if (REPLAY) {
+    const int bb = b >= 1 ? b : 1;
+    const float *pa = l.dof_vel + (bl0.f0 * (kBodies - 1) + (bb - 1)) * 3;
+    const float *pc = l.dof_vel + (bl0.f1 * (kBodies - 1) + (bb - 1)) * 3;
+    dva = {pa[0], pa[1], pa[2]};
+    dvc = {pc[0], pc[1], pc[2]};
+  }
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
   float *const wreg = sh_obs + (kStage ? (threadIdx.x >> 6) * kStWave : 0);
   if constexpr (kStage) {
@@ -658,7 +705,12 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   if (REPLAY) {
     v3 dv, f;
     s = ref0;
-    replay_perturb(e, r, ei, b, prog, s, dv_ref, dv, f);
+    v3 dv_ref = {0.0f, 0.0f, 0.0f};
+    if (b >= 1) {
+      const float tb = bl0.b, sb = 1.0f - tb;
+      dv_ref = {sb * dva.x + tb * dvc.x, sb * dva.y + tb * dvc.y, sb * dva.z + tb * dvc.z};
+    }
+    replay_perturb(e, r, ei, b, prog, s, dv_ref, dv, f, rng_val);
     if constexpr (kStage) {
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
       // the record goes out with the wave's rows at the end; dof vel / force and the PD map here
@@ -695,10 +747,11 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
     if (kStage) rec_stage = wreg + kStRec + (g & 1) * kRowF + b * kRec;
 #endif
-    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0), &mt, rec_stage);
+    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0, rng_val), &mt,
+                        rec_stage);
     if (lane == 0) {
       reset_env_counters(e, ei, mt);
-      if (e.rng) e.rng[ei] += 1u;
+      if (e.rng) e.rng[ei] = rng_val + 1u;
     }
     // obs of the re-initialised env: progress 0, start = mt, offsets 0 (humanoid_phc.py:1061-1065)
     bl1 = frame_blend((float)(0 + 1) * c.dt + mt + 0.0f, m);
@@ -773,7 +826,8 @@ __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l,
   const v3 go = {e.goff[3 * env], e.goff[3 * env + 1], e.goff[3 * env + 2]};
   BodyRec s = ref_body(l.frames, bl, b, &go);
   v3 dv, f;
-  replay_perturb(e, r, env, b, prog, s, b >= 1 ? ref_dof_vel(l.dof_vel, bl, b) : v3{0.0f, 0.0f, 0.0f}, dv, f);
+  replay_perturb(e, r, env, b, prog, s, b >= 1 ? ref_dof_vel(l.dof_vel, bl, b) : v3{0.0f, 0.0f, 0.0f}, dv, f,
+                 e.rng ? e.rng[env] : 0u);
   store_replay(e, env, b, s, dv, f);
 }
 

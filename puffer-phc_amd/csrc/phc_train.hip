@@ -136,16 +136,21 @@ __global__ __launch_bounds__(kRmsCols) void k_rms_partial(const float *__restric
     return float2{p[0], two ? p[1] : 0.0f};
   };
   int64_t r = r0;
-  for (; r + kRmsPf <= r1; r += kRmsPf) {
+  // the unrolled loads must not sit behind a per-load select: hipcc then branches around each
+  // load and waits vmcnt(0) per row (measured: 280 us for the 490 MB rollout batch, 1.75 TB/s)
+  if (vec) {
+    for (; r + kRmsPf <= r1; r += kRmsPf) {
+      const float *p = x + r * cols + col;
 #pragma unroll
-    for (int u = 0; u < kRmsPf; ++u) buf[u] = load(r + u);
+      for (int u = 0; u < kRmsPf; ++u) buf[u] = *reinterpret_cast<const float2 *>(p + u * cols);
 #pragma unroll
-    for (int u = 0; u < kRmsPf; ++u) {
-      const double a = (double)buf[u].x, b = (double)buf[u].y;
-      s0 += a;
-      q0 += a * a;
-      s1 += b;
-      q1 += b * b;
+      for (int u = 0; u < kRmsPf; ++u) {
+        const double a = (double)buf[u].x, b = (double)buf[u].y;
+        s0 += a;
+        q0 += a * a;
+        s1 += b;
+        q1 += b * b;
+      }
     }
   }
   for (; r < r1; ++r) {
