@@ -30,8 +30,16 @@ __global__ __launch_bounds__(kScanThreads) void k_rank_mask(const uint8_t *__res
   for (int64_t base = 0; base < n; base += 4 * kScanThreads) {
     const int64_t i0 = base + 4 * t;
     int f[4];
+    if (mask && i0 + 3 < n) {  // the 4 flags by one unconditional 4-byte-granule read (no per-flag waits)
+      uint8_t m4[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) f[q] = (i0 + q < n && (!mask || mask[i0 + q])) ? 1 : 0;
+      for (int q = 0; q < 4; ++q) m4[q] = mask[i0 + q];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[q] = m4[q] ? 1 : 0;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[q] = (i0 + q < n && (!mask || mask[i0 + q])) ? 1 : 0;
+    }
     const int v = (f[0] + f[1]) + (f[2] + f[3]);
     // inclusive wave scan of the per-thread counts
     int s = v;
