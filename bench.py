@@ -133,10 +133,14 @@ VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 
 def physics_roofline(args, kern_s, launches):
     """N3 physics kernel (phc_physics_step): VALU-issue bound.  achieved = the kernel's VALU
-    wave-instructions per launch (SQ_INSTS_VALU from the committed PMC pass,
-    profiles/physics_valu_4096.json, scaled by the wave count: one wave per 2 envs) / its mean launch
-    duration timed live by the launch's own events; peak = VALU_ISSUE_PEAK."""
-    f = os.path.join(ROOT, "profiles", "physics_valu_4096.json")
+    wave-instructions per launch (SQ_INSTS_VALU from the committed PMC pass over this bench
+    command's own launches, profiles/physics_valu_4096_bench.json — the count depends on the contact
+    and self-collision state — else the standing probe's, profiles/physics_valu_4096.json; scaled by
+    the wave count: one wave per 2 envs) / its mean launch duration timed live by the launch's own
+    events; peak = VALU_ISSUE_PEAK."""
+    f = os.path.join(ROOT, "profiles", "physics_valu_4096_bench.json")
+    if not os.path.exists(f):
+        f = os.path.join(ROOT, "profiles", "physics_valu_4096.json")
     instr = None
     if os.path.exists(f):
         with open(f) as fh:
@@ -146,7 +150,7 @@ def physics_roofline(args, kern_s, launches):
     return {"bound": "valu-issue", "kernel": "phc_physics_step", "achieved": ach, "peak": VALU_ISSUE_PEAK,
             "unit": "wave-instr/s", "frac": ach / VALU_ISSUE_PEAK if ach else None, "kernel_us": kern_s * 1e6,
             "launches_timed": launches, "env_steps_per_s_kernel": args.envs / kern_s if kern_s > 0 else None,
-            "valu_instr_per_launch": instr}
+            "valu_instr_per_launch": instr, "valu_count_file": os.path.basename(f) if instr else None}
 
 
 def physics_cpu_baseline(seconds):
