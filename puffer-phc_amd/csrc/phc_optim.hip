@@ -61,28 +61,37 @@ __global__ __launch_bounds__(kOptBlock) void k_grad_partials(const float *__rest
   for (int64_t t = s + threadIdx.x; t < vs; t += kOptBlock) one(t);  // < 4 elements when aligned
   int64_t i = vs + 4 * (int64_t)threadIdx.x;
   if (p0) {  // uniform: no select around the loads (it would serialise them)
-    for (; i + 4 * kOptBlock < ve; i += 8 * kOptBlock) {  // two 16-B loads per buffer in flight
-      const float4 v0 = *reinterpret_cast<const float4 *>(g + i);
-      const float4 v1 = *reinterpret_cast<const float4 *>(g + i + 4 * kOptBlock);
-      const float4 a0 = *reinterpret_cast<const float4 *>(p + i);
-      const float4 a1 = *reinterpret_cast<const float4 *>(p + i + 4 * kOptBlock);
-      const float4 b0 = *reinterpret_cast<const float4 *>(p0 + i);
-      const float4 b1 = *reinterpret_cast<const float4 *>(p0 + i + 4 * kOptBlock);
-      four(v0, a0, b0);
-      four(v1, a1, b1);
+    // four 16-B loads per buffer in flight (12 per thread); the chunks are summed in the thread's
+    // address order whatever the unroll, so the partials do not depend on it
+    for (; i + 12 * kOptBlock < ve; i += 16 * kOptBlock) {
+      float4 v[4], a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = *reinterpret_cast<const float4 *>(g + i + 4 * u * kOptBlock);
+        a[u] = *reinterpret_cast<const float4 *>(p + i + 4 * u * kOptBlock);
+        b[u] = *reinterpret_cast<const float4 *>(p0 + i + 4 * u * kOptBlock);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) four(v[u], a[u], b[u]);
     }
-    if (i < ve)
+    for (; i < ve; i += 4 * kOptBlock)
       four(*reinterpret_cast<const float4 *>(g + i), *reinterpret_cast<const float4 *>(p + i),
            *reinterpret_cast<const float4 *>(p0 + i));
   } else {
+    // the gradient alone: four 16-B loads per thread in flight (two left the pass latency-bound at
+    // a quarter of HBM); the chunks are still summed in the thread's address order
     const float4 z4{0.0f, 0.0f, 0.0f, 0.0f};
-    for (; i + 4 * kOptBlock < ve; i += 8 * kOptBlock) {
+    for (; i + 12 * kOptBlock < ve; i += 16 * kOptBlock) {
       const float4 v0 = *reinterpret_cast<const float4 *>(g + i);
       const float4 v1 = *reinterpret_cast<const float4 *>(g + i + 4 * kOptBlock);
+      const float4 v2 = *reinterpret_cast<const float4 *>(g + i + 8 * kOptBlock);
+      const float4 v3 = *reinterpret_cast<const float4 *>(g + i + 12 * kOptBlock);
       four(v0, z4, z4);
       four(v1, z4, z4);
+      four(v2, z4, z4);
+      four(v3, z4, z4);
     }
-    if (i < ve) four(*reinterpret_cast<const float4 *>(g + i), z4, z4);
+    for (; i < ve; i += 4 * kOptBlock) four(*reinterpret_cast<const float4 *>(g + i), z4, z4);
   }
   for (int64_t t = ve + threadIdx.x; t < e; t += kOptBlock) one(t);
 #pragma unroll

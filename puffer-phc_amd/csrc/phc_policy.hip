@@ -192,6 +192,9 @@ __device__ __forceinline__ void ln_silu_row(float x[C][4], const float *__restri
 // rows of action j over the k quarter kq — per k step one dword of W^T row k (the 4 x A threads of a
 // step read one contiguous run of every W^T row: coalesced, where w_mu's rows put 64 lanes on 64
 // lines) and one broadcast float4 of each h row from LDS; the quarters are summed in a fixed order.
+#ifndef PHC_ACT_WT_UNROLL
+#define PHC_ACT_WT_UNROLL 8  // 4-deep k steps in flight: the W^T dwords come from L2, one round trip per unrolled group
+#endif
 template <int H>
 __device__ __forceinline__ void act_tail_wt(const phc_policy_act_args &a, float (*hs)[H], float (*part)[kActMaxA],
                                             int64_t r0, int tid) {
@@ -205,7 +208,7 @@ __device__ __forceinline__ void act_tail_wt(const phc_policy_act_args &a, float 
     for (int r = 0; r < kActRows; ++r) acc[r] = 0.0f;
     const int64_t ld = a.ld_w_mu_t;
     const float *wt = a.w_mu_t + (int64_t)(kq * KQ) * ld + j;
-#pragma unroll 2
+#pragma unroll PHC_ACT_WT_UNROLL
     for (int kk = 0; kk < KQ; kk += 4) {
       const float w0 = wt[(kk + 0) * ld], w1 = wt[(kk + 1) * ld], w2 = wt[(kk + 2) * ld], w3 = wt[(kk + 3) * ld];
 #pragma unroll

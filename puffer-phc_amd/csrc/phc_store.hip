@@ -10,6 +10,9 @@
 namespace phc {
 
 constexpr int kScanThreads = 1024;
+#ifndef PHC_COPY_FLAT
+#define PHC_COPY_FLAT 1
+#endif
 
 struct RowFields {
   phc_row_field f[PHC_MAX_ROW_FIELDS];
@@ -112,6 +115,66 @@ __global__ __launch_bounds__(256) void k_copy_rows(RowFields fs, const uint8_t *
   }
 }
 
+// The row's fields as one flat run of 4-byte words (each field's words = its 4-byte elements, two per
+// 8-byte element, one per flag byte): thread t moves words t + 256 u.  Every load of the row — the
+// control words (mask flag, rank, take, start) and IT data words per thread — is issued in one
+// memory round at clamped addresses before the first store: a per-field copy loop put one
+// load -> store round trip per field (and per 256-word chunk) on the block's critical path.
+// Flag bytes are read through their aligned word (at most 3 bytes past a flag array's end:
+// inside the allocation's 512-B rounding for every torch tensor).
+typedef const __attribute__((address_space(1))) uint8_t cu8;
+typedef const __attribute__((address_space(1))) uint32_t cu32;
+__device__ const uint32_t kOneWord = 1u;  // stands in for a null mask (every row valid)
+
+struct FlatFields {
+  const char *src[PHC_MAX_ROW_FIELDS];
+  char *dst[PHC_MAX_ROW_FIELDS];
+  int64_t srb[PHC_MAX_ROW_FIELDS], drb[PHC_MAX_ROW_FIELDS];  // source / destination bytes per row
+  int32_t woff[PHC_MAX_ROW_FIELDS + 1];                      // first flat word of each field; woff[n] = W
+  uint32_t u8_mask;                                          // bit k: field k is flag bytes -> float
+  int32_t n;
+};
+
+template <int IT>
+__global__ __launch_bounds__(256) void k_copy_rows_flat(FlatFields fs, const uint8_t *__restrict__ mask, int64_t n,
+                                                        const int64_t *__restrict__ counts,
+                                                        const int64_t *__restrict__ ws) {
+  const int64_t row = blockIdx.x;  // grid = n
+  const int t = threadIdx.x;
+  const uint32_t mk = *(mask ? (cu8 *)(mask + row) : (cu8 *)&kOneWord);  // pointer select: one load
+  const int64_t r = reinterpret_cast<const int32_t *>(ws + 1)[row];
+  const int64_t take = counts[1], start = ws[0];
+  const int W = fs.woff[fs.n];
+  uint32_t v[IT];
+  const char *sp[IT];
+  int k_of[IT], w_of[IT];
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    int vw = t + 256 * u;
+    vw = vw < W ? vw : W - 1;
+    int k = 0;
+#pragma unroll
+    for (int q = 1; q < PHC_MAX_ROW_FIELDS; ++q) k = (q < fs.n && vw >= fs.woff[q]) ? q : k;
+    const int w = vw - fs.woff[k];
+    const bool b8 = (fs.u8_mask >> k) & 1u;
+    const char *a = fs.src[k] + row * fs.srb[k] + (b8 ? w : 4 * w);
+    sp[u] = a;
+    k_of[u] = k;
+    w_of[u] = w;
+    v[u] = *(cu32 *)((uintptr_t)a & ~(uintptr_t)3);
+  }
+  if (!mk || r >= take) return;
+  const int64_t dst_row = start + r;
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    if (t + 256 * u >= W) break;
+    const int k = k_of[u];
+    uint32_t x = v[u];
+    if ((fs.u8_mask >> k) & 1u) x = ((x >> (8 * ((uintptr_t)sp[u] & 3))) & 0xFFu) ? 0x3F800000u : 0u;
+    *reinterpret_cast<uint32_t *>(fs.dst[k] + dst_row * fs.drb[k] + 4 * w_of[u]) = x;
+  }
+}
+
 }  // namespace phc
 
 using namespace phc;
@@ -139,6 +202,39 @@ extern "C" int phc_compact_rows(const phc_row_field *fields, int32_t num_fields,
   hipStream_t st = as_stream(stream);
   int64_t *ws = static_cast<int64_t *>(workspace);
   hipLaunchKernelGGL(k_rank_mask, dim3(1), dim3(kScanThreads), 0, st, mask, n, cursor, capacity, counts, ws);
-  if (n > 0) hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)n), dim3(256), 0, st, fs, mask, n, counts, ws);
+  if (n == 0) return check_launch("compact_rows");
+  // the flat form when the row's words fit 8 per thread (the rollout's 934-float obs row + the
+  // scalar fields: 1,010 words); PHC_COPY_FLAT=0 keeps the per-field loop (A/B)
+  FlatFields ff{};
+  int64_t words = 0;
+  bool flat = PHC_COPY_FLAT != 0;
+  for (int k = 0; k < num_fields && flat; ++k) {
+    const phc_row_field &f = fields[k];
+    const int64_t e = f.row_elems;
+    const int64_t w = f.kind == PHC_ROW_COPY64 ? 2 * e : e;
+    ff.src[k] = static_cast<const char *>(f.src);
+    ff.dst[k] = static_cast<char *>(f.dst);
+    ff.srb[k] = f.kind == PHC_ROW_COPY64 ? 8 * e : (f.kind == PHC_ROW_U8_TO_F32 ? e : 4 * e);
+    ff.drb[k] = f.kind == PHC_ROW_COPY64 ? 8 * e : 4 * e;
+    if (f.kind == PHC_ROW_U8_TO_F32) ff.u8_mask |= 1u << k;
+    // word loads: 4-byte aligned sources (flag bytes are read through their aligned word)
+    if (f.kind != PHC_ROW_U8_TO_F32 && ((reinterpret_cast<uintptr_t>(f.src) | reinterpret_cast<uintptr_t>(f.dst)) & 3))
+      flat = false;
+    if (f.kind == PHC_ROW_U8_TO_F32 && (reinterpret_cast<uintptr_t>(f.dst) & 3)) flat = false;
+    ff.woff[k] = (int32_t)words;
+    words += w;
+  }
+  flat = flat && words <= 8 * 256;
+  if (flat) {
+    ff.woff[num_fields] = (int32_t)words;
+    ff.n = num_fields;
+    const dim3 g((unsigned)n), b(256);
+    if (words <= 256) hipLaunchKernelGGL(k_copy_rows_flat<1>, g, b, 0, st, ff, mask, n, counts, ws);
+    else if (words <= 512) hipLaunchKernelGGL(k_copy_rows_flat<2>, g, b, 0, st, ff, mask, n, counts, ws);
+    else if (words <= 1024) hipLaunchKernelGGL(k_copy_rows_flat<4>, g, b, 0, st, ff, mask, n, counts, ws);
+    else hipLaunchKernelGGL(k_copy_rows_flat<8>, g, b, 0, st, ff, mask, n, counts, ws);
+  } else {
+    hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)n), dim3(256), 0, st, fs, mask, n, counts, ws);
+  }
   return check_launch("compact_rows");
 }

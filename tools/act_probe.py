@@ -29,6 +29,14 @@ def run_act():
     N.policy_act(y, ln[0], ln[1], 1e-5, w_mu, b_mu, w_v, b_v, sigma, noise, act, lp, val, mu=mu)
 
 
+w_mu_t = torch.zeros((H, 72), device=dev)
+w_mu_t[:, :A] = w_mu.t()
+
+
+def run_act_t():
+    N.policy_act(y, ln[0], ln[1], 1e-5, w_mu, b_mu, w_v, b_v, sigma, noise, act, lp, val, mu=mu, w_mu_t=w_mu_t)
+
+
 def run_obs():
     N.obs_half(obs, mean, var, 1e-5, 5.0, out, None)
 
@@ -46,4 +54,6 @@ def timeit(fn, reps=200):
     return s.elapsed_time(e) / reps * 1e3
 
 
-print(f"policy_act {timeit(run_act):.1f} us  obs_half {timeit(run_obs):.1f} us  lp_sum {float(lp.double().sum()):.6f}")
+t_wt = timeit(run_act_t)
+lp_t = float(lp.double().sum())
+print(f"policy_act w_mu_t {t_wt:.1f} us (lp_sum {lp_t:.6f})  policy_act {timeit(run_act):.1f} us  obs_half {timeit(run_obs):.1f} us  lp_sum {float(lp.double().sum()):.6f}")
