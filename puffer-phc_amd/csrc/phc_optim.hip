@@ -273,6 +273,16 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_into(ReduceJobs js) {
       const int64_t r = i / job.cols, c = i - r * job.cols;
       const float *src = job.src + r * job.src_ld + c;
       int s = s0;
+      // 16 loads in flight, added in the same order as 8 per step (bit-equal to that form)
+      for (; s + 16 <= s1; s += 16) {
+        float v[16];
+#pragma unroll
+        for (int l = 0; l < 16; ++l) v[l] = src[(int64_t)(s + l) * job.part_stride];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) a8[l] += v[l];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) a8[l] += v[8 + l];
+      }
       for (; s + 8 <= s1; s += 8) {
 #pragma unroll
         for (int l = 0; l < 8; ++l) a8[l] += src[(int64_t)(s + l) * job.part_stride];
@@ -288,17 +298,31 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_into(ReduceJobs js) {
     }
     return;
   }
+  // few parts: every part of the thread's kRedPerThread elements loaded at clamped indices in one
+  // memory round (a bounds break or a part loop with loads behind it serialised them), then summed
+  // in part order as before
   const int64_t base = ((int64_t)blockIdx.x - js.first_block[q]) * kRedThreads * kRedPerThread + threadIdx.x;
+  const int P = job.parts;
+  float v[kRedPerThread][kRedManyParts], dv[kRedPerThread];
+#pragma unroll
+  for (int u = 0; u < kRedPerThread; ++u) {
+    int64_t i = base + (int64_t)u * kRedThreads;
+    i = i < total ? i : total - 1;
+    const int64_t r = i / job.cols, c = i - r * job.cols;
+    const float *src = job.src + r * job.src_ld + c;
+#pragma unroll
+    for (int sp = 0; sp < kRedManyParts; ++sp) v[u][sp] = src[(int64_t)(sp < P ? sp : P - 1) * job.part_stride];
+    dv[u] = job.dst[i];  // read even when not accumulating: one round with the parts
+  }
 #pragma unroll
   for (int u = 0; u < kRedPerThread; ++u) {
     const int64_t i = base + (int64_t)u * kRedThreads;
     if (i >= total) break;
-    const int64_t r = i / job.cols, c = i - r * job.cols;
-    const float *src = job.src + r * job.src_ld + c;
-    float acc = src[0];
-    for (int s = 1; s < job.parts; ++s) acc += src[s * job.part_stride];
-    if (job.accumulate) job.dst[i] += acc;
-    else job.dst[i] = acc;
+    float acc = v[u][0];
+#pragma unroll
+    for (int sp = 1; sp < kRedManyParts; ++sp)
+      if (sp < P) acc += v[u][sp];
+    job.dst[i] = job.accumulate ? dv[u] + acc : acc;
   }
 }
 
