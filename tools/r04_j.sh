@@ -3,7 +3,7 @@
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$ROOT"; O=$ROOT/gpurun_out/r04j; mkdir -p "$O"; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_row_store.py \
-  tests/test_gpu_policy_fused.py tests/test_gpu_weight_cache.py tests/test_gpu_env_trainer.py tests/test_gpu_fused_ppo.py > "$O/pytest.log" 2>&1 || { tail -30 "$O/pytest.log"; exit 3; }
+  tests/test_gpu_policy_fused.py tests/test_gpu_weight_cache.py tests/test_gpu_env_trainer.py tests/test_gpu_fused_ppo.py tests/test_gpu_optim.py tests/test_gpu_twin_mlp.py > "$O/pytest.log" 2>&1 || { tail -30 "$O/pytest.log"; exit 3; }
 tail -2 "$O/pytest.log"
 for so in libphc_hip_u2.so libphc_hip.so libphc_hip_u16.so libphc_hip_u2.so libphc_hip.so libphc_hip_u16.so; do
   echo -n "$so: "; PHC_HIP_LIB=$ROOT/puffer-phc_amd/lib/$so timeout -k 10 120 python tools/act_probe.py 2>&1 | grep -v amdgpu.ids | tail -1 || exit 4
