@@ -1,5 +1,6 @@
 // phc_common.h — shared host/device plumbing of libphc_hip.so.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -50,6 +51,16 @@ inline bool phc_timer_take(phc_kernel_timer *t, hipEvent_t *ev0, hipEvent_t *ev1
   *ev1 = t->stop[t->used];
   t->used += 1;
   return true;
+}
+
+// a dispatch the timer samples records its events through hipExtLaunchKernel; every other one is a
+// plain launch (the GEMMs already did this; the env / physics steps went through the extended path
+// with null events on every step)
+template <typename F, typename... Args>
+inline void phc_launch(F kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
+                       Args... args) {
+  if (ev0) hipExtLaunchKernelGGL(kernel, grid, block, lds, st, ev0, ev1, 0, args...);
+  else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
 }
 
 namespace phc {

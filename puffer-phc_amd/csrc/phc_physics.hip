@@ -809,7 +809,7 @@ static int physics_launch(const phc_env_buffers *env, const float *pd_target, co
   if (phc_timer_take(timer, &ev0, &ev1)) timer->work += (double)env->num_envs;  // env-steps
   const PdArgs pa{pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
                   pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr, pd ? pd->clip : 1};
-  hipExtLaunchKernelGGL(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), ev0, ev1, 0, v,
+  phc_launch(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), ev0, ev1, v,
                         body_model, pd_target, pa, c);
   return check_launch("physics_step");
 }

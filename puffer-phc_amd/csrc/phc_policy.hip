@@ -193,7 +193,7 @@ __device__ __forceinline__ void ln_silu_row(float x[C][4], const float *__restri
 // step read one contiguous run of every W^T row: coalesced, where w_mu's rows put 64 lanes on 64
 // lines) and one broadcast float4 of each h row from LDS; the quarters are summed in a fixed order.
 #ifndef PHC_ACT_WT_UNROLL
-#define PHC_ACT_WT_UNROLL 8  // 4-deep k steps in flight: the W^T dwords come from L2, one round trip per unrolled group
+#define PHC_ACT_WT_UNROLL 2  // 4-deep k steps per unrolled group (measured: 2 -> 25.0 us, 8 -> 26.8 us, 16 -> 27.1 us per 4096-row launch)
 #endif
 template <int H>
 __device__ __forceinline__ void act_tail_wt(const phc_policy_act_args &a, float (*hs)[H], float (*part)[kActMaxA],

@@ -960,9 +960,9 @@ extern "C" int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_l
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot && lib->dof_vel, "env_step: auto_reset needs local_rot and dof_vel");
     PHC_REQUIRE(env->rng_counter, "env_step: auto_reset needs rng_counter");
-    hipExtLaunchKernelGGL(k_env_step<true, false>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs, none);
+    phc_launch(k_env_step<true, false>, grid, block, 0, st, ev0, ev1, ev, lv, cs, none);
   } else {
-    hipExtLaunchKernelGGL(k_env_step<false, false>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs, none);
+    phc_launch(k_env_step<false, false>, grid, block, 0, st, ev0, ev1, ev, lv, cs, none);
   }
   return check_launch("env_step");
 }
@@ -988,9 +988,9 @@ extern "C" int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot, "env_step_replay: auto_reset needs local_rot");
     PHC_REQUIRE(env->rng_counter, "env_step_replay: auto_reset needs rng_counter");
-    hipExtLaunchKernelGGL(k_env_step<true, true>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs, ra);
+    phc_launch(k_env_step<true, true>, grid, block, 0, st, ev0, ev1, ev, lv, cs, ra);
   } else {
-    hipExtLaunchKernelGGL(k_env_step<false, true>, grid, block, 0, st, ev0, ev1, 0, ev, lv, cs, ra);
+    phc_launch(k_env_step<false, true>, grid, block, 0, st, ev0, ev1, ev, lv, cs, ra);
   }
   return check_launch("env_step_replay");
 }
