@@ -355,6 +355,14 @@ class Runner:
     def mark(self):
         self._skip0 = self.skipped()
         self._gpu_phases = [] if self.args.mode == "ppo" else None
+        if self._gpu_phases is not None:
+            # the phase events of every timed step, created (and their HIP events materialised by a
+            # record) before the timed region: a torch Event creates its hipEvent at its first record
+            self._event_pool = [self._phase_events() for _ in range(self.args.steps + 1)]
+            for ev in self._event_pool:
+                for e in ev:
+                    e.record()
+            torch.cuda.synchronize()
         if self.args.mode == "ppo":
             p = self.info.profile
             self._p0 = {k: getattr(p, k).elapsed for k in ("evaluate", "env", "eval_forward", "train",
@@ -376,7 +384,10 @@ class Runner:
             self.env.send(actions)
             return a.envs
         g0 = self.info.global_step
-        ev = self._phase_events() if self._gpu_phases is not None else None
+        ev = None
+        if self._gpu_phases is not None:
+            pool = getattr(self, "_event_pool", None)
+            ev = pool.pop() if pool else self._phase_events()
         if ev:
             ev[0].record()
         self.cp.evaluate(self.components, self.info)

@@ -21,3 +21,5 @@ for r in 1 2; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$O/bench_ppo_$r.log" 2>&1 || { tail -5 "$O/bench_ppo_$r.log"; exit 6; }
   tail -1 "$O/bench_ppo_$r.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); e=d['roofline_env_step']; print(round(d['value']/1e6,4), 'M', round(d['ms_per_step'],2), 'ms gemm', round(d['roofline']['frac'],4), 'env', round(e['kernel_us'],2), d['config']['phase_gpu_ms_per_step'])"
 done
+timeout -k 10 300 python tools/host_profile.py 3 > "$O/host_profile.txt" 2>&1 || { tail -5 "$O/host_profile.txt"; exit 7; }
+grep -A30 "tottime" "$O/host_profile.txt" | head -45
