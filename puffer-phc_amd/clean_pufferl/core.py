@@ -279,12 +279,11 @@ def _evaluate_graph(components, info):
         n = max(1, rs.store.n)
         min_steps = max(1, -(-(experience.batch_size - start) // n))
         steps = 0
+        step_infos = []  # read after the loop: a mean_and_log info resolves by waiting for its copy
         while True:
             with profile.env:
                 _, _, _, _, env_info, _, _ = vecenv.recv()
-            for i in env_info:
-                for k, v in i.items():
-                    env_infos[k].append(v)
+            step_infos.extend(env_info)
             with profile.eval_forward:
                 rs.run(train_cfg.rollout_graph)
             with profile.env:
@@ -296,6 +295,9 @@ def _evaluate_graph(components, info):
                         break
         with profile.eval_misc:
             n_valid, taken = rs.store.counts[2:4].tolist()
+            for i in step_infos:
+                for k, v in i.items():
+                    env_infos[k].append(v)
             # data parallel: every rank advances the same whole-job step count (its own mask-true
             # rows differ with the envs' truncation patterns), so loop exits agree across ranks
             info.global_step += _global_count(n_valid, rs.store.counts.device)
@@ -435,6 +437,64 @@ class _PinnedRing:
 _PINNED = _PinnedRing()
 
 
+# train()'s advantage / minibatch-layout pass replayed from a captured hipGraph: ~20 small launches
+# (sort, gathers, the operand build, GAE, reshapes) whose Python launch overhead left the GPU idle
+# between the rollout and the first trunk GEMM.  The pass reads only device buffers that keep their
+# addresses (the experience arrays, the RunningNorm statistics) and writes its outputs into the
+# graph's own memory, which the experience attributes set during capture keep pointing at.
+ADV_GRAPH = os.environ.get("PHC_ADV_GRAPH", "1") != "0"
+
+
+_ADV_ATTRS = ("b_idxs_obs", "b_idxs", "b_idxs_flat", "b_obs_half", "b_obs", "b_actions", "b_logprobs", "b_dones",
+              "b_truncated", "b_values", "b_advantages", "returns", "sorted_values", "b_returns")
+
+
+def _adv_graph_key(components, info):
+    exp, cfg = components.experience, info.config
+    pol = components.policy.policy if hasattr(components.policy, "policy") else components.policy
+    nm = getattr(pol, "obs_norm", None)
+    ptrs = tuple(t.data_ptr() for t in (exp.obs, exp.actions, exp.logprobs, exp.values, exp.rewards, exp.dones,
+                                         exp.truncateds, exp.env_ids))
+    norm = (nm.running_mean.data_ptr(), nm.running_var.data_ptr(), float(nm.epsilon), float(nm.clip)) if nm else None
+    return (ptrs, norm, exp.batch_size, exp.minibatch_size, exp.num_minibatches, exp.bptt_horizon,
+            float(cfg.gamma), float(cfg.gae_lambda), cfg.fused_obs, cfg.fused_loss, cfg.precision,
+            id(components.gae))
+
+
+def _compute_advantages_train(components, info):
+    """compute_advantages for train(): eager on the first call, captured on the second, replayed
+    after (re-captured when a key input changes; eager for AMP, recurrent or host tensors)."""
+    exp = components.experience
+    if not (ADV_GRAPH and exp.obs.is_cuda and not info.use_amp_obs and exp.lstm_h is None):
+        return compute_advantages(components, info)
+    st = getattr(components, "_adv_graph", None)
+    if st is None:
+        st = {"graph": None, "key": None, "out": None, "failed": False}
+        components._adv_graph = st
+    key = _adv_graph_key(components, info)
+    if st["graph"] is not None and st["key"] == key:
+        st["graph"].replay()
+        for k, v in st["attrs"].items():  # an eager call in between may have re-pointed them
+            setattr(exp, k, v)
+        return st["out"]
+    if st["failed"] or st["key"] != key:  # first sight of this key: eager (lazy initialisation)
+        st["graph"], st["key"] = None, key
+        return compute_advantages(components, info)
+    try:
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = compute_advantages(components, info)
+    except Exception:  # noqa: BLE001  (an op that cannot be captured: stay eager)
+        st["failed"] = True
+        torch.cuda.synchronize()
+        return compute_advantages(components, info)
+    st["graph"], st["out"] = g, out
+    st["attrs"] = {k: getattr(exp, k) for k in _ADV_ATTRS}
+    g.replay()
+    return out
+
+
 def _fill_losses(losses, a):
     """The logged loss row (train's device accumulators, var_y, explained variance) into the
     LossComponents fields."""
@@ -459,7 +519,7 @@ def train(components, info, utilization=None):
         and cfg.l2_reg_coef == 0
     with profile.train:
         with profile.train_misc:
-            compute_advantages(components, info)
+            _compute_advantages_train(components, info)
             if info.use_amp_obs:
                 amp_obs_demo = components.vecenv.fetch_amp_obs_demo()
                 amp_mb = amp_obs_demo.shape[0]

@@ -10,6 +10,7 @@ every `log_interval` ticks (the reference's logging cadence, :145-162).
 """
 
 import functools
+from collections.abc import Mapping
 
 import numpy as np
 import torch
@@ -24,6 +25,34 @@ def env_creator(name="puffer_phc"):
 
 def make(cfg, motion_data=None):
     return PHCPufferEnv(cfg, motion_data=motion_data)
+
+
+class PendingInfo(Mapping):
+    """One mean_and_log() info dict whose statistics are still on their way from the device; any
+    read waits for the copy and builds the dict (PHCPufferEnv._resolve_info)."""
+
+    def __init__(self, env, host, event):
+        self._src, self._d = (env, host, event), None
+
+    def resolve(self):
+        if self._d is None:
+            env, host, event = self._src
+            event.synchronize()
+            self._d = env._resolve_info(host.numpy().copy())
+            self._src = None
+        return self._d
+
+    def __getitem__(self, k):
+        return self.resolve()[k]
+
+    def __iter__(self):
+        return iter(self.resolve())
+
+    def __len__(self):
+        return len(self.resolve())
+
+    def __repr__(self):
+        return repr(self.resolve())
 
 
 class PHCPufferEnv:
@@ -52,6 +81,10 @@ class PHCPufferEnv:
         self.episode_count = 0
         self.tick = 0
         self._pending = None
+        # pinned buffers for mean_and_log's non-blocking readback, reused round-robin
+        self._info_ring = [[torch.empty(_native.STATS_SLOTS, dtype=torch.float64, pin_memory=True), None]
+                           for _ in range(4)]
+        self._info_i = 0
 
     @property
     def num_agents(self):
@@ -96,9 +129,25 @@ class PHCPufferEnv:
         return self.observations, rew, self.terminals, self.truncations, info
 
     def mean_and_log(self):
-        """Host reduction of the per-block statistics (clean_pufferl/env.py:145-188)."""
-        s = self.stats.sum(0).cpu().numpy()
+        """Host reduction of the per-block statistics (clean_pufferl/env.py:145-188).  The sums come
+        back by a non-blocking copy into pinned memory: the returned info resolves (waits for the
+        copy) when first read, so the rollout does not drain the stream every log_interval steps;
+        the trainer reads the step infos after its rollout loop."""
+        s = self.stats.sum(0)
+        slot = self._info_ring[self._info_i % len(self._info_ring)]
+        self._info_i += 1
+        if slot[1] is not None:
+            slot[1].resolve()  # the copy that last used this buffer finished long ago
+        host = slot[0]
+        host.copy_(s, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record()
         self.stats.zero_()
+        info = PendingInfo(self, host, done)
+        slot[1] = info
+        return [info]
+
+    def _resolve_info(self, s):
         n_ep = s[7]
         self.episode_count += int(n_ep)
         denom = self.cfg.log_interval * self.num_agents
@@ -111,7 +160,7 @@ class PHCPufferEnv:
         }
         if n_ep > 0:
             info.update(episode_return=s[5] / n_ep, episode_length=s[6] / n_ep, truncated_rate=s[8] / n_ep)
-        return [info]
+        return info
 
     # -------------------------------------------- pufferlib vecenv protocol --
     def async_reset(self, seed=None):

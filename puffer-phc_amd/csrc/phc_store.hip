@@ -116,13 +116,12 @@ __global__ __launch_bounds__(256) void k_copy_rows(RowFields fs, const uint8_t *
 }
 
 // The row's fields as one flat run of 4-byte words (each field's words = its 4-byte elements, two per
-// 8-byte element, one per flag byte); one wave per row, lane l moving words l + 64 u.  Every load of
-// the row — the control words (mask flag, rank, take, start) and IT data words per lane — is issued
-// in one memory round at clamped addresses before the first store: the per-field copy loop put one
-// load -> store round trip per field on the critical path, and a 256-thread block per row ran 64
-// short-lived waves per CU in 4 dispatch rounds.  Flag bytes are read through their aligned word
-// (at most 3 bytes past a flag array's end: inside the allocation's 512-B rounding for every torch
-// tensor).
+// 8-byte element, one per flag byte): thread t moves words t + 256 u.  Every load of the row — the
+// control words (mask flag, rank, take, start) and IT data words per thread — is issued in one
+// memory round at clamped addresses before the first store: a per-field copy loop put one
+// load -> store round trip per field (and per 256-word chunk) on the block's critical path.
+// Flag bytes are read through their aligned word (at most 3 bytes past a flag array's end:
+// inside the allocation's 512-B rounding for every torch tensor).
 typedef const __attribute__((address_space(1))) uint8_t cu8;
 typedef const __attribute__((address_space(1))) uint32_t cu32;
 __device__ const uint32_t kOneWord = 1u;  // stands in for a null mask (every row valid)
@@ -135,15 +134,13 @@ struct FlatFields {
   uint32_t u8_mask;                                          // bit k: field k is flag bytes -> float
   int32_t n;
 };
-constexpr int kFlatRowsPerBlock = 4;  // one wave per row
 
 template <int IT>
-__global__ __launch_bounds__(64 * kFlatRowsPerBlock) void k_copy_rows_flat(FlatFields fs, const uint8_t *__restrict__ mask,
-                                                                         int64_t n, const int64_t *__restrict__ counts,
-                                                                         const int64_t *__restrict__ ws) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row0 = (int64_t)blockIdx.x * kFlatRowsPerBlock + (threadIdx.x >> 6);
-  const int64_t row = row0 < n ? row0 : n - 1;
+__global__ __launch_bounds__(256) void k_copy_rows_flat(FlatFields fs, const uint8_t *__restrict__ mask, int64_t n,
+                                                        const int64_t *__restrict__ counts,
+                                                        const int64_t *__restrict__ ws) {
+  const int64_t row = blockIdx.x;  // grid = n
+  const int t = threadIdx.x;
   const uint32_t mk = *(mask ? (cu8 *)(mask + row) : (cu8 *)&kOneWord);  // pointer select: one load
   const int64_t r = reinterpret_cast<const int32_t *>(ws + 1)[row];
   const int64_t take = counts[1], start = ws[0];
@@ -153,7 +150,7 @@ __global__ __launch_bounds__(64 * kFlatRowsPerBlock) void k_copy_rows_flat(FlatF
   int k_of[IT], w_of[IT];
 #pragma unroll
   for (int u = 0; u < IT; ++u) {
-    int vw = lane + 64 * u;
+    int vw = t + 256 * u;
     vw = vw < W ? vw : W - 1;
     int k = 0;
 #pragma unroll
@@ -166,11 +163,11 @@ __global__ __launch_bounds__(64 * kFlatRowsPerBlock) void k_copy_rows_flat(FlatF
     w_of[u] = w;
     v[u] = *(cu32 *)((uintptr_t)a & ~(uintptr_t)3);
   }
-  if (row0 >= n || !mk || r >= take) return;
+  if (!mk || r >= take) return;
   const int64_t dst_row = start + r;
 #pragma unroll
   for (int u = 0; u < IT; ++u) {
-    if (lane + 64 * u >= W) break;
+    if (t + 256 * u >= W) break;
     const int k = k_of[u];
     uint32_t x = v[u];
     if ((fs.u8_mask >> k) & 1u) x = ((x >> (8 * ((uintptr_t)sp[u] & 3))) & 0xFFu) ? 0x3F800000u : 0u;
@@ -206,7 +203,7 @@ extern "C" int phc_compact_rows(const phc_row_field *fields, int32_t num_fields,
   int64_t *ws = static_cast<int64_t *>(workspace);
   hipLaunchKernelGGL(k_rank_mask, dim3(1), dim3(kScanThreads), 0, st, mask, n, cursor, capacity, counts, ws);
   if (n == 0) return check_launch("compact_rows");
-  // the flat form when the row's words fit 32 per lane (the rollout's 934-float obs row + the
+  // the flat form when the row's words fit 8 per thread (the rollout's 934-float obs row + the
   // scalar fields: 1,010 words); PHC_COPY_FLAT=0 keeps the per-field loop (A/B)
   FlatFields ff{};
   int64_t words = 0;
@@ -227,15 +224,15 @@ extern "C" int phc_compact_rows(const phc_row_field *fields, int32_t num_fields,
     ff.woff[k] = (int32_t)words;
     words += w;
   }
-  flat = flat && words <= 32 * 64;
+  flat = flat && words <= 8 * 256;
   if (flat) {
     ff.woff[num_fields] = (int32_t)words;
     ff.n = num_fields;
-    const dim3 g((unsigned)((n + kFlatRowsPerBlock - 1) / kFlatRowsPerBlock)), b(64 * kFlatRowsPerBlock);
-    if (words <= 4 * 64) hipLaunchKernelGGL(k_copy_rows_flat<4>, g, b, 0, st, ff, mask, n, counts, ws);
-    else if (words <= 8 * 64) hipLaunchKernelGGL(k_copy_rows_flat<8>, g, b, 0, st, ff, mask, n, counts, ws);
-    else if (words <= 16 * 64) hipLaunchKernelGGL(k_copy_rows_flat<16>, g, b, 0, st, ff, mask, n, counts, ws);
-    else hipLaunchKernelGGL(k_copy_rows_flat<32>, g, b, 0, st, ff, mask, n, counts, ws);
+    const dim3 g((unsigned)n), b(256);
+    if (words <= 256) hipLaunchKernelGGL(k_copy_rows_flat<1>, g, b, 0, st, ff, mask, n, counts, ws);
+    else if (words <= 512) hipLaunchKernelGGL(k_copy_rows_flat<2>, g, b, 0, st, ff, mask, n, counts, ws);
+    else if (words <= 1024) hipLaunchKernelGGL(k_copy_rows_flat<4>, g, b, 0, st, ff, mask, n, counts, ws);
+    else hipLaunchKernelGGL(k_copy_rows_flat<8>, g, b, 0, st, ff, mask, n, counts, ws);
   } else {
     hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)n), dim3(256), 0, st, fs, mask, n, counts, ws);
   }

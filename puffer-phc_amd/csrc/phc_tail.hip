@@ -143,28 +143,11 @@ __global__ __launch_bounds__(kFwdThreads) void k_tail_ln_fwd(phc_tail_ln_args a)
 // LayerNorm + SiLU backward of one row held per lane (k_ln_silu_bwd's arithmetic): dh is the
 // gradient of the SiLU output (critic: dh = dvalue * w_v with d w_v += dvalue * silu(ln));
 // accumulates the gamma / beta / output-bias column sums of the lane's 8 columns, writes dy (T)
-// gamma / beta (and the critic's w_v, its dh) come from the block's LDS copy, read at the point of
-// use: held in registers for the whole persistent loop they pushed the kernel past 256 VGPRs
 template <typename T, bool CRITIC>
-__device__ __forceinline__ void t_ln_bwd_row(const float x[kTC][4], const float dh_in[kTC][4], const float *gm_s,
-                                             const float *bt_s, const float *wv_s, float eps, float dvalue, int lane,
-                                             T *dst, float pg[kTC][4], float pb[kTC][4], float p6[kTC][4],
+__device__ __forceinline__ void t_ln_bwd_row(const float x[kTC][4], const float dh[kTC][4], const float gm[kTC][4],
+                                             const float bt[kTC][4], float eps, float dvalue, int lane, T *dst,
+                                             float pg[kTC][4], float pb[kTC][4], float p6[kTC][4],
                                              float pwv[kTC][4]) {
-  float gm[kTC][4], bt[kTC][4], dh[kTC][4];
-#pragma unroll
-  for (int k = 0; k < kTC; ++k) {
-    const float4 g = *reinterpret_cast<const float4 *>(gm_s + 4 * (lane + 64 * k));
-    const float4 b = *reinterpret_cast<const float4 *>(bt_s + 4 * (lane + 64 * k));
-    gm[k][0] = g.x; gm[k][1] = g.y; gm[k][2] = g.z; gm[k][3] = g.w;
-    bt[k][0] = b.x; bt[k][1] = b.y; bt[k][2] = b.z; bt[k][3] = b.w;
-    if constexpr (CRITIC) {
-      const float4 w = *reinterpret_cast<const float4 *>(wv_s + 4 * (lane + 64 * k));
-      dh[k][0] = w.x; dh[k][1] = w.y; dh[k][2] = w.z; dh[k][3] = w.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dh[k][e] = dh_in[k][e];
-    }
-  }
   const LnStat st = t_ln_stat(x, eps);
   float xh[kTC][4], dx[kTC][4];
   float s1 = 0.0f, s2 = 0.0f;
@@ -207,121 +190,91 @@ __device__ __forceinline__ void t_ln_bwd_row(const float x[kTC][4], const float 
   }
 }
 
-// Waves specialise by trunk: even waves run actor rows, odd waves critic rows (rows advance by 4
-// per block step), so a wave holds one trunk's row, prefetch and column sums — a wave running both
-// trunks held twice that and spilled past 256 VGPRs, and the spill reloads drained its prefetch.
 template <typename T>
 __global__ __launch_bounds__(kBwdThreads) void k_tail_ln_bwd(phc_tail_ln_args a, const float *__restrict__ dh_actor,
                                                             const float *__restrict__ dmu,
                                                             const float *__restrict__ dvalue, int A,
                                                             T *__restrict__ dy, float *__restrict__ partial) {
-  constexpr int kWaves = kBwdThreads / 64, kSlots = kWaves / 2;
+  constexpr int kWaves = kBwdThreads / 64;
   __shared__ __attribute__((aligned(16))) float red[4][kWaves][kTH];  // 64 KB
-  __shared__ __attribute__((aligned(16))) float prm[5][kTH];           // gamma 0 / 1, beta 0 / 1, w_v
-  __shared__ float sbv[kWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int trunk = wave & 1, slot = wave >> 1;
   const int64_t M = a.rows;
-  static_assert(kBwdThreads == kTH, "one parameter column per thread");
-  prm[0][tid] = a.ln_gamma[0][tid];
-  prm[1][tid] = a.ln_gamma[1][tid];
-  prm[2][tid] = a.ln_beta[0][tid];
-  prm[3][tid] = a.ln_beta[1][tid];
-  prm[4][tid] = a.w_value[tid];
-  __syncthreads();
-  float pg[kTC][4], pb[kTC][4], p6[kTC][4], pwv[kTC][4];
+  float gm[2][kTC][4], bt[2][kTC][4], wv[kTC][4];
+  t_load_param(a.ln_gamma[0], lane, gm[0]);
+  t_load_param(a.ln_gamma[1], lane, gm[1]);
+  t_load_param(a.ln_beta[0], lane, bt[0]);
+  t_load_param(a.ln_beta[1], lane, bt[1]);
+  t_load_param(a.w_value, lane, wv);
+  float pg[2][kTC][4], pb[2][kTC][4], p6[2][kTC][4], pwv[kTC][4];
 #pragma unroll
   for (int k = 0; k < kTC; ++k)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) pg[k][e] = pb[k][e] = p6[k][e] = pwv[k][e] = 0.0f;
-  float pm0 = 0.0f, pm1 = 0.0f;  // actor: b_mu sums (lanes < A, lanes + 64 < A); critic: pm0 = b_v sum
-  // the wave's next row is loaded while this one is processed; every fetch is unconditional at a
-  // clamped row (behind a branch, the join before the row's arithmetic costs a vmcnt(0) that
-  // waits for the prefetch too); dmu through clamped loads masked after
+    for (int e = 0; e < 4; ++e) {
+      pg[0][k][e] = pg[1][k][e] = pb[0][k][e] = pb[1][k][e] = 0.0f;
+      p6[0][k][e] = p6[1][k][e] = pwv[k][e] = 0.0f;
+    }
+  float pbmu0 = 0.0f, pbmu1 = 0.0f, pbv = 0.0f;
+  // one row (both trunks) per wave at a time; the wave's next row is loaded while this one is
+  // processed (its loads land during the reductions), dmu through clamped loads masked after
   struct RowIn {
-    float x[kTC][4], d[kTC][4];
-    float s0, s1;
+    float xa[kTC][4], xc[kTC][4], da[kTC][4];
+    float dv, m0, m1;
   };
   const int l0 = lane < A ? lane : A - 1, l1 = lane + 64 < A ? lane + 64 : A - 1;
-  // one load shape for both trunks (pointer selects, no branch): the critic's second row is its
-  // own x row again (an L2 hit; its dh is w_v, read from LDS) and both its scalars are dvalue[r]
-  const float *xsrc = a.trunk_out + (trunk ? M * kTH : 0);
-  const float *dsrc = trunk ? xsrc : dh_actor;
-  const float *s0src = trunk ? dvalue : dmu + l0, *s1src = trunk ? dvalue : dmu + l1;
-  const int64_t sstr = trunk ? 1 : A;
   auto fetch = [&](int64_t r, RowIn &in) {
-    t_load_row(xsrc + r * kTH, lane, in.x);
-    t_load_row(dsrc + r * kTH, lane, in.d);
-    in.s0 = s0src[r * sstr];
-    in.s1 = s1src[r * sstr];
+    t_load_row(a.trunk_out + r * kTH, lane, in.xa);
+    t_load_row(a.trunk_out + (M + r) * kTH, lane, in.xc);
+    t_load_row(dh_actor + r * kTH, lane, in.da);
+    in.dv = dvalue[r];
+    in.m0 = dmu[r * A + l0];
+    in.m1 = dmu[r * A + l1];
   };
-  const int64_t step = (int64_t)gridDim.x * kSlots;
-  int64_t row = (int64_t)blockIdx.x * kSlots + slot;
-  T *dst0 = dy + (trunk ? M * kTH : 0);
-  // two rows in flight as a ping-pong pair (no register rotation: a copy of a loaded row waits for
-  // its loads): while row A is processed row B's loads are in flight, then A is refetched two rows
-  // on.  One row ahead left a one-trunk wave half the bytes in flight of the two-trunk form
-  // (measured slower: 84.7 vs 72.2 us)
-  auto clampr = [&](int64_t r) { return r < M ? r : M - 1; };
-  auto process = [&](int64_t r, const RowIn &in) {
-    if (trunk == 0) {
-      pm0 += lane < A ? in.s0 : 0.0f;
-      pm1 += lane + 64 < A ? in.s1 : 0.0f;
-      t_ln_bwd_row<T, false>(in.x, in.d, prm[0], prm[2], prm[4], a.ln_eps, 0.0f, lane, dst0 + r * kTH, pg, pb, p6,
-                             pwv);
-    } else {
-      pm0 += in.s0;
-      t_ln_bwd_row<T, true>(in.x, in.d, prm[1], prm[3], prm[4], a.ln_eps, in.s0, lane, dst0 + r * kTH, pg, pb, p6,
-                            pwv);
-    }
-  };
-  RowIn ra, rb;
-  fetch(clampr(row), ra);
-  fetch(clampr(row + step), rb);
-  for (; row < M; row += 2 * step) {
-    process(row, ra);
-    fetch(clampr(row + 2 * step), ra);
-    if (row + step < M) process(row + step, rb);
-    fetch(clampr(row + 3 * step), rb);
+  const int64_t step = (int64_t)gridDim.x * kWaves;
+  int64_t row = (int64_t)blockIdx.x * kWaves + wave;
+  RowIn cur;
+  if (row < M) fetch(row, cur);
+  for (; row < M; row += step) {
+    RowIn nxt;
+    if (row + step < M) fetch(row + step, nxt);
+    pbmu0 += lane < A ? cur.m0 : 0.0f;
+    pbmu1 += lane + 64 < A ? cur.m1 : 0.0f;
+    pbv += cur.dv;
+    t_ln_bwd_row<T, false>(cur.xa, cur.da, gm[0], bt[0], a.ln_eps, 0.0f, lane, dy + row * kTH, pg[0], pb[0], p6[0],
+                           pwv);
+    t_ln_bwd_row<T, true>(cur.xc, wv, gm[1], bt[1], a.ln_eps, cur.dv, lane, dy + (M + row) * kTH, pg[1], pb[1], p6[1],
+                          pwv);
+    cur = nxt;
   }
-  // the block's partial row (tail_layout): per trunk, its 4 waves' column sums added through LDS
-  // in wave order
+  // the block's partial row (tail_layout): the 8 waves' column sums added through LDS in order
   const TailLayout L = tail_layout(A, kTH);
   float *pr = partial + (int64_t)blockIdx.x * L.stride;
-  auto put = [&](int s, const float v[kTC][4]) {
+  auto put = [&](int slot, const float v[kTC][4]) {
 #pragma unroll
     for (int k = 0; k < kTC; ++k)
-      *reinterpret_cast<float4 *>(&red[s][wave][4 * (lane + 64 * k)]) = float4{v[k][0], v[k][1], v[k][2], v[k][3]};
+      *reinterpret_cast<float4 *>(&red[slot][wave][4 * (lane + 64 * k)]) = float4{v[k][0], v[k][1], v[k][2], v[k][3]};
   };
-  auto take = [&](int s, int tr, float *dst) {  // column tid of slot s over trunk tr's waves
-    float acc = 0.0f;
+  auto take = [&](int slot, float *dst) {
+    float s = 0.0f;
 #pragma unroll
-    for (int w = tr; w < kWaves; w += 2) acc += red[s][w][tid];
-    dst[tid] = acc;
+    for (int w = 0; w < kWaves; ++w) s += red[slot][w][tid];
+    dst[tid] = s;
   };
-  put(0, pg); put(1, pb); put(2, p6);
-  if (trunk == 1) {
-    put(3, pwv);
-    if (lane == 0) sbv[wave] = pm0;
-  } else {
-    red[3][wave][lane] = pm0;
-    red[3][wave][64 + lane] = pm1;
-  }
+  put(0, pg[0]); put(1, pg[1]); put(2, pb[0]); put(3, pb[1]);
   __syncthreads();
-  take(0, 0, pr + L.gamma); take(0, 1, pr + L.gamma + kTH);
-  take(1, 0, pr + L.beta);  take(1, 1, pr + L.beta + kTH);
-  take(2, 0, pr + L.b6);    take(2, 1, pr + L.b6 + kTH);
-  take(3, 1, pr + L.wv);
-  if (tid < A) {
-    float acc = 0.0f;
+  take(0, pr + L.gamma); take(1, pr + L.gamma + kTH); take(2, pr + L.beta); take(3, pr + L.beta + kTH);
+  __syncthreads();
+  put(0, p6[0]); put(1, p6[1]); put(2, pwv);
+  red[3][wave][lane] = pbmu0;
+  red[3][wave][64 + lane] = pbmu1;
+  if (lane == 0) red[3][wave][128] = pbv;
+  __syncthreads();
+  take(0, pr + L.b6); take(1, pr + L.b6 + kTH); take(2, pr + L.wv);
+  if (tid < A || tid == 128) {
+    float s = 0.0f;
 #pragma unroll
-    for (int w = 0; w < kWaves; w += 2) acc += red[3][w][tid];
-    pr[L.bmu + tid] = acc;
-  } else if (tid == 128) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int w = 1; w < kWaves; w += 2) acc += sbv[w];
-    pr[L.bv] = acc;
+    for (int w = 0; w < kWaves; ++w) s += red[3][w][tid];
+    if (tid < A) pr[L.bmu + tid] = s;
+    else pr[L.bv] = s;
   }
 }
 
