@@ -394,6 +394,14 @@ def compute_advantages(components, info):
     experience.returns = advantages + values
     experience.sorted_values = values
     experience.b_returns = experience.b_advantages + experience.b_values
+    # what train() needs from these fixed arrays, computed here so the graphed pass carries it:
+    # the per-minibatch advantage (mean, std) of norm_adv (single process; data parallel reduces
+    # over the ranks in train()) and the explained-variance pair logged at the end (core.py:397-399)
+    experience.b_adv_ms = None if D.is_dist() else torch.stack(
+        [experience.b_advantages.mean(1), experience.b_advantages.std(1)], 1).contiguous()
+    var_y = torch.var(experience.returns, unbiased=False)
+    ev_t = 1 - torch.var(experience.returns - values, unbiased=False) / var_y
+    experience.ev_pair = torch.stack([var_y, ev_t]).double()
     return advantages
 
 
@@ -446,7 +454,8 @@ ADV_GRAPH = os.environ.get("PHC_ADV_GRAPH", "1") != "0"
 
 
 _ADV_ATTRS = ("b_idxs_obs", "b_idxs", "b_idxs_flat", "b_obs_half", "b_obs", "b_actions", "b_logprobs", "b_dones",
-              "b_truncated", "b_values", "b_advantages", "returns", "sorted_values", "b_returns")
+              "b_truncated", "b_values", "b_advantages", "returns", "sorted_values", "b_returns", "b_adv_ms",
+              "ev_pair")
 
 
 def _adv_graph_key(components, info):
@@ -493,6 +502,13 @@ def _compute_advantages_train(components, info):
     st["attrs"] = {k: getattr(exp, k) for k in _ADV_ATTRS}
     g.replay()
     return out
+
+
+def _adv_mean_std(experience):
+    """Per-minibatch advantage (mean, std): the copy compute_advantages made (single process),
+    else the all-rank reduction."""
+    ms = getattr(experience, "b_adv_ms", None)
+    return ms if ms is not None else D.global_mean_std_rows(experience.b_advantages)
 
 
 def _fill_losses(losses, a):
@@ -560,7 +576,7 @@ def train(components, info, utilization=None):
                         fused_mb = True
                         if cfg.norm_adv:
                             if adv_ms is None:
-                                adv_ms = D.global_mean_std_rows(experience.b_advantages)
+                                adv_ms = _adv_mean_std(experience)
                             ms = adv_ms[mb]
                         else:
                             ms = torch.tensor([0.0, 1.0], dtype=torch.float32, device=obs.device)
@@ -588,7 +604,7 @@ def train(components, info, utilization=None):
                         # per-minibatch advantage mean / std of every minibatch at once
                         if cfg.norm_adv:
                             if adv_ms is None:
-                                adv_ms = D.global_mean_std_rows(experience.b_advantages)
+                                adv_ms = _adv_mean_std(experience)
                             mean, std = adv_ms[mb], None
                         else:
                             mean, std = 0.0, 1.0
@@ -708,11 +724,14 @@ def train(components, info, utilization=None):
             # explained variance (core.py:397-399) in fp32 on the device; the loss row, var_y and
             # it come back in ONE device -> host copy, non-blocking into pinned memory: the values
             # are read (and waited for) only when the losses are first looked at
-            y_pred = experience.sorted_values
-            y_true = experience.returns
-            var_y = torch.var(y_true, unbiased=False)
-            ev_t = 1 - torch.var(y_true - y_pred, unbiased=False) / var_y
-            row = torch.cat([acc, torch.stack([var_y, ev_t]).double()])
+            ev_pair = getattr(experience, "ev_pair", None)
+            if ev_pair is None:
+                y_pred = experience.sorted_values
+                y_true = experience.returns
+                var_y = torch.var(y_true, unbiased=False)
+                ev_t = 1 - torch.var(y_true - y_pred, unbiased=False) / var_y
+                ev_pair = torch.stack([var_y, ev_t]).double()
+            row = torch.cat([acc, ev_pair])
             if row.is_cuda:
                 slot = _PINNED.take(row, None)
                 host = slot[0]

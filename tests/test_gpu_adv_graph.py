@@ -8,7 +8,7 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 FIELDS = ("b_obs_half", "b_actions", "b_logprobs", "b_values", "b_advantages", "b_returns", "returns",
-          "sorted_values", "b_dones", "b_truncated", "b_idxs_flat")
+          "sorted_values", "b_dones", "b_truncated", "b_idxs_flat", "b_adv_ms", "ev_pair")
 
 
 @pytest.fixture(scope="module")
