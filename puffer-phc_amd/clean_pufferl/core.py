@@ -158,6 +158,7 @@ class RolloutStep:
         self.store = _native.RowCompactor(pairs, n, exp.batch_size, dev)
         self.graph = None
         self.eager_steps = 0
+        self._noise_ready = False
         pol = self.policy.policy if hasattr(self.policy, "policy") else self.policy
         self.twin = getattr(pol, "_twin", None)
         # R17 fused into the env step: the step kernel writes RunningNorm(obs) as the policy's first
@@ -212,7 +213,8 @@ class RolloutStep:
             refresh_twin(self.twin, _compute_dtype(self.cfg))  # in-place refresh after optimizer steps
         if self.opnd is not None:
             self._refresh_operand()
-        if self.fused_act:
+        ahead = self.fused_act and NOISE_AHEAD
+        if self.fused_act and not (ahead and self._noise_ready):
             self.noise.normal_()
         if self.graph is not None:
             self.graph.replay()
@@ -226,6 +228,11 @@ class RolloutStep:
                 self._body()
             self.graph = g
             g.replay()
+        if ahead:
+            # the next step's Normal draw, queued between this step's policy graph and its env step
+            # (the buffer is read only by the next replay, stream-ordered after this draw)
+            self.noise.normal_()
+            self._noise_ready = True
 
 
 def _global_count(n, device):
@@ -451,6 +458,8 @@ _PINNED = _PinnedRing()
 # addresses (the experience arrays, the RunningNorm statistics) and writes its outputs into the
 # graph's own memory, which the experience attributes set during capture keep pointing at.
 ADV_GRAPH = os.environ.get("PHC_ADV_GRAPH", "1") != "0"
+# rollout: draw the next step's action noise right after the policy graph instead of before it
+NOISE_AHEAD = os.environ.get("PHC_NOISE_AHEAD", "0") != "0"
 
 
 _ADV_ATTRS = ("b_idxs_obs", "b_idxs", "b_idxs_flat", "b_obs_half", "b_obs", "b_actions", "b_logprobs", "b_dones",
