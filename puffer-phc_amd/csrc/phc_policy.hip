@@ -142,7 +142,10 @@ __global__ __launch_bounds__(256) void k_obs_half_rows(const float *__restrict__
 }
 
 // --------------------------------------------------------------- policy_act --
-constexpr int kActRows = 8;      // rows per block
+#ifndef PHC_ACT_ROWS
+#define PHC_ACT_ROWS 8
+#endif
+constexpr int kActRows = PHC_ACT_ROWS;  // rows per block
 constexpr int kActMaxA = 72;     // actions supported (PHC_NUM_DOF + 3)
 constexpr int kActThreads = 320; // 2 k halves x 2 row groups x up to 72 actions (288), 5 waves
 constexpr int kActTasks = (2 * kActRows + kActThreads / 64 - 1) / (kActThreads / 64);  // LN rows per wave
