@@ -58,3 +58,29 @@ def test_explained_variance_nan_when_var_y_zero():
     row[12] = 0
     p = PendingLossComponents(row, _Event(), _fill_losses)
     assert np.isnan(p.explained_variance)
+
+
+def test_pinned_ring_resolves_a_slot_before_reuse(monkeypatch):
+    """train()'s loss-row buffers are reused round-robin (clean_pufferl/core.py _PinnedRing): a slot
+    whose PendingLossComponents was never read is resolved, with its own values, before it is
+    overwritten."""
+    from puffer_phc_amd.clean_pufferl import core
+
+    real_empty = torch.empty
+    monkeypatch.setattr(torch, "empty", lambda *a, pin_memory=False, **k: real_empty(*a, **k))
+    ring = core._PinnedRing(n=2)
+    owners = []
+    for i in range(3):
+        row = _row() + 100.0 * i
+        slot = ring.take(row, None)
+        if i < 2:
+            assert len(ring.slots[(tuple(row.shape), row.dtype)]) == i + 1
+        else:  # the first slot again: its unread owner resolved first
+            assert slot is ring.slots[(tuple(row.shape), row.dtype)][0]
+            assert object.__getattribute__(owners[0], "__dict__").get("_pending") is None
+        slot[0].copy_(row)
+        p = PendingLossComponents(slot[0], _Event(), _fill_losses)
+        slot[1] = p
+        owners.append(p)
+    assert owners[0].policy_loss == 0.5  # the values it held before the buffer was reused
+    assert owners[2].policy_loss == 200.5
