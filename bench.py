@@ -63,9 +63,11 @@ BYTES_PER_ENV_STEP_FUSED = 11714
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16 / bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
 DEFAULTS = {"env": (200, 20), "rollout": (64, 8), "ppo": (3, 1)}
-# kernel-timer sampling (module docstring): every 4th env-step / physics launch, every 11th trunk GEMM
+# kernel-timer sampling (module docstring): every 4th env-step / physics launch, every 16th trunk GEMM
+# (16 is coprime to a minibatch's 13 GEMM launches and divides an iteration's 16 x 13: each layer's
+# launch exactly once per iteration)
 ENV_TIMER_PERIOD = 4
-GEMM_TIMER_PERIOD = 11
+GEMM_TIMER_PERIOD = 16
 
 
 def parse():
@@ -460,19 +462,25 @@ def main():
     env, packed, env_cfg = build_env(args, rank)
     runner = Runner(args, env, env_cfg)
 
-    for _ in range(args.warmup):
-        runner.step()
-    torch.cuda.synchronize()
     from puffer_phc_amd._native import KernelTimer, gemm_set_timer
 
+    # the kernel timers are attached before the warmup, so launches captured into hipGraphs during it
+    # (the train / rollout graphs) carry timer slots; reset() after the warmup keeps only what the
+    # timed region stamps (a graph's slots: its last replay)
     timer = env.env.kernel_timer = KernelTimer(capacity=max(4096, 64 * args.steps), period=ENV_TIMER_PERIOD)
-    # phc_twin_gemm launches outside the replayed rollout graph (the training trunks' fused-epilogue
-    # GEMMs), every GEMM_TIMER_PERIOD-th timed by its own dispatch events, with its 2 m n k FLOPs
+    # the PPO update's trunk GEMMs (phc_twin_gemm of more than 4,096 rows + the weight gradients), every
+    # GEMM_TIMER_PERIOD-th stamped by the kernel itself, with its 2 m n k FLOPs
     gtimer = KernelTimer(capacity=max(4096, 256 * args.steps), period=GEMM_TIMER_PERIOD)
     gemm_set_timer(gtimer)
     ptimer = None
-    if args.physics == "articulated":  # every phc_physics_step launch, timed by its dispatch events
+    if args.physics == "articulated":  # phc_physics_step launches, stamped by the kernel
         ptimer = env.env.physics.timer = KernelTimer(capacity=max(4096, 64 * args.steps), period=ENV_TIMER_PERIOD)
+    for _ in range(args.warmup):
+        runner.step()
+    torch.cuda.synchronize()
+    for tm in (timer, gtimer, ptimer):
+        if tm is not None:
+            tm.reset()
     flat = getattr(getattr(runner, "components", None), "flat_grads", None)
     if flat is not None and world > 1:
         flat.timing, flat.exposed = True, []

@@ -132,23 +132,32 @@ int phc_motion_state(const phc_motion_lib *lib, const int64_t *motion_ids, const
 int phc_env_step(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
                  void *stream);
 
-/* Kernel timer for measurement: phc_env_step_timed records start/stop events from the kernel
- * dispatch itself (hipExtLaunchKernel), one pair per launch, up to `capacity` launches;
- * phc_timer_total_ms waits for them and returns the summed kernel time (negative on error). */
+/* Kernel timer for measurement (bench.py): a timed launch stamps its own start (per workgroup) and
+ * end (per wave, after its memory operations complete) from the device's constant-rate clock into a
+ * slot of the timer's device buffer, so the span is the kernel's own execution as rocprofv3 reports
+ * it, no event is recorded around the dispatch (the stream sees no idle time), and launches captured
+ * into a hipGraph are timed too (their slots hold the LAST replay).  Up to `capacity` timed launches.
+ * phc_timer_reset starts a new measurement: launches stamped before it no longer count, except slots
+ * inside a captured graph that a later replay re-stamps.  count / work / total_ms wait for the device
+ * and report the counted launches (total_ms negative on error). */
 typedef struct phc_kernel_timer phc_kernel_timer;
 phc_kernel_timer *phc_timer_create(int32_t capacity);
 void phc_timer_destroy(phc_kernel_timer *timer);
 void phc_timer_reset(phc_kernel_timer *timer);
-int32_t phc_timer_count(const phc_kernel_timer *timer);
+int32_t phc_timer_count(phc_kernel_timer *timer);
 /* Sample: time only every period-th launch offered to the timer (1 = every launch, the default).
- * A timed dispatch leaves the stream idle for 5-10 us around it; sampling keeps a timed region's
- * wall time close to an untimed one's.  phc_timer_offered counts every launch offered. */
+ * A timed launch costs its workgroups one store and its waves one wait + atomic at the end;
+ * phc_timer_offered counts every launch offered. */
 void phc_timer_set_period(phc_kernel_timer *timer, int32_t period);
 int64_t phc_timer_offered(const phc_kernel_timer *timer);
 double phc_timer_total_ms(phc_kernel_timer *timer);
-double phc_timer_work(const phc_kernel_timer *timer); /* algorithmic work of the timed launches (GEMM: FLOPs) */
-/* phc_twin_gemm launches outside graph capture record into `timer` (NULL: off) with their
- * 2 m n k batch FLOPs; a measurement aid for bench.py's GEMM roofline. */
+double phc_timer_work(phc_kernel_timer *timer); /* algorithmic work of the counted launches (GEMM: FLOPs) */
+/* per-launch ms of the counted launches in the order they were taken (up to cap; diagnostics);
+ * returns the number counted, negative on error */
+int32_t phc_timer_durations(phc_kernel_timer *timer, double *out, int32_t cap);
+/* the PPO update's trunk GEMMs (phc_twin_gemm launches of more than 4,096 rows, phc_weight_grad,
+ * phc_weight_grad_group) are offered to `timer` (NULL: off) with their 2 m n k batch FLOPs; a
+ * measurement aid for bench.py's GEMM roofline. */
 void phc_gemm_set_timer(phc_kernel_timer *timer);
 int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
                        phc_kernel_timer *timer, void *stream);
@@ -216,7 +225,7 @@ typedef struct phc_replay_params {
  * the same buffers and values as phc_actions_to_pd (pd nullable: skipped) -> phc_physics_replay ->
  * phc_env_step, bit for bit; the replayed state IS the blended reference at the step's time, so its
  * frame rows are gathered once and the sim record / dof velocities / forces never make an HBM round
- * trip.  timer nullable (start/stop events of the launch, as phc_env_step_timed). */
+ * trip.  timer nullable (the launch stamps itself into it, as phc_env_step_timed). */
 int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
                         const phc_replay_params *replay, const phc_pd_map *pd, phc_kernel_timer *timer,
                         void *stream);
@@ -257,7 +266,7 @@ typedef struct phc_physics_params {
 } phc_physics_params;
 int phc_physics_step(const phc_env_buffers *env, const float *pd_target, const float *body_model,
                      const phc_physics_params *p, void *stream);
-/* the same launch with its start/stop events recorded into `timer` (bench.py); timer work += num_envs */
+/* the same launch stamped into `timer` (bench.py; work = num_envs env-steps) */
 int phc_physics_step_timed(const phc_env_buffers *env, const float *pd_target, const float *body_model,
                            const phc_physics_params *p, phc_kernel_timer *timer, void *stream);
 /* the same step with R13 folded in: PD targets computed in-kernel from pd->actions (and written to
@@ -463,12 +472,18 @@ int phc_ln_silu_bwd(const void *y, const float *gamma, const float *beta, const 
  * counts are device int64 so a captured hipGraph can replay the call. */
 #define PHC_MAX_ROW_FIELDS 12
 enum { PHC_ROW_COPY32 = 0, PHC_ROW_COPY64 = 1, PHC_ROW_U8_TO_F32 = 2 };
+/* flags: PHC_ROW_SRC_WORDS = the caller guarantees that every aligned 4-byte word overlapping the
+ * source's bytes lies inside the source allocation.  A PHC_ROW_U8_TO_F32 field may then be read
+ * through its aligned words (the one-round flat copy); without it a flag field takes the per-field
+ * byte-load path, so a source that ends (or starts) exactly at an allocation edge is never
+ * over-read. */
+enum { PHC_ROW_SRC_WORDS = 1 };
 typedef struct phc_row_field {
   const void *src;
   void *dst;
   int64_t row_elems; /* elements per row (4-byte, 8-byte or 1-byte source elements by kind) */
   int32_t kind;
-  int32_t reserved;
+  int32_t flags; /* PHC_ROW_SRC_WORDS */
 } phc_row_field;
 size_t phc_compact_workspace_bytes(int64_t n);
 int phc_compact_rows(const phc_row_field *fields, int32_t num_fields, const uint8_t *mask, int64_t n,
@@ -492,7 +507,8 @@ typedef struct phc_adam_params {
   int32_t use_loss_scale;
   float growth_factor, backoff_factor;
   int32_t growth_interval;
-  int32_t reserved;
+  int32_t lr_from_state; /* 1: the learning rate is state->lr (device memory), so a captured hipGraph of
+                          * the update follows a schedule written between replays; 0: lr above */
 } phc_adam_params;
 typedef struct phc_opt_state {
   float loss_scale;
@@ -501,12 +517,37 @@ typedef struct phc_opt_state {
   int32_t skipped; /* steps skipped for inf / nan gradients */
   float grad_mul, step_size, bc2_sqrt; /* this step's coefficients (written by the call) */
   int32_t skip;
+  float lr; /* the learning rate read when phc_adam_params.lr_from_state */
+  int32_t reserved;
 } phc_opt_state;
 int64_t phc_opt_block_elems(void);
 size_t phc_opt_workspace_bytes(int32_t nblk);
 int phc_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const int64_t *blk_range,
                  int32_t nblk, const int32_t *seg_blk, int32_t nseg, const phc_adam_params *hp, phc_opt_state *state,
                  float *norm_out, const float *param_init, void *workspace, void *stream);
+/* The same step with the GEMM-operand copies of the parameters written by the Adam pass itself
+ * (what phc_pack_weights would write right after it, from the same fp32 values: f16 / bf16 / fp32
+ * copies, row-wise into dst and transposed into dst_t), so no separate operand refresh re-reads the
+ * parameters.  `jobs` is a DEVICE table of njobs entries covering [0, n) in order: kind
+ * PHC_ADAM_FLAT = elements [off, off + rows) with no copy; kind PHC_ADAM_TILE = a parameter [rows,
+ * cols] (row-major, cols contiguous) at flat offset off, processed in 64 x 64 tiles, with
+ * dst (nullable, ld dst_ld) and dst_t (nullable, ld dst_t_ld) in `dtype`.  first_block = the job's
+ * first workgroup (ascending, first_block[0] = 0), tiles_c = its column tiles (tile jobs);
+ * nblocks = the total.  phc_adam_job_blocks() gives a job's workgroup count. */
+enum { PHC_ADAM_FLAT = 0, PHC_ADAM_TILE = 1 };
+#define PHC_MAX_ADAM_JOBS 256
+typedef struct phc_adam_job {
+  int64_t off, rows, cols;
+  void *dst, *dst_t;
+  int64_t dst_ld, dst_t_ld;
+  int64_t first_block, tiles_c;
+  int32_t dtype, kind;
+} phc_adam_job;
+int64_t phc_adam_job_blocks(int32_t kind, int64_t rows, int64_t cols);
+int phc_opt_step_operands(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                          const int64_t *blk_range, int32_t nblk, const int32_t *seg_blk, int32_t nseg,
+                          const phc_adam_params *hp, phc_opt_state *state, float *norm_out, const float *param_init,
+                          void *workspace, const phc_adam_job *jobs, int32_t njobs, int64_t nblocks, void *stream);
 
 /* R21 gradient plumbing: for each job, dst[r, c] (+= when accumulate) = sum over s < parts of
  * src[s * part_stride + r * src_ld + c] (parts summed in order; dst dense [rows, cols]).  Writes

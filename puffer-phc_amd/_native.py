@@ -102,11 +102,22 @@ class ReplayParamsC(ctypes.Structure):
 
 class RowFieldC(ctypes.Structure):
     _fields_ = [("src", c_vp), ("dst", c_vp), ("row_elems", c_i64), ("kind", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("flags", ctypes.c_int32)]
 
 
 MAX_ROW_FIELDS = 12
 ROW_COPY32, ROW_COPY64, ROW_U8_TO_F32 = 0, 1, 2
+ROW_SRC_WORDS = 1  # phc_row_field.flags: the source's covering aligned words are inside its allocation
+
+
+def _words_inside_storage(t):
+    """Whether every aligned 4-byte word overlapping t's bytes lies inside t's storage (what
+    PHC_ROW_SRC_WORDS vouches for: a flag field may then be read through its aligned words)."""
+    st = t.untyped_storage()
+    base, end = st.data_ptr(), st.data_ptr() + st.nbytes()
+    lo = t.data_ptr()
+    hi = lo + t.numel() * t.element_size()
+    return t.numel() > 0 and (lo & ~3) >= base and ((hi - 1) & ~3) + 4 <= end
 
 
 class PpoCoefsC(ctypes.Structure):
@@ -173,6 +184,16 @@ class PackJobC(ctypes.Structure):
 MAX_PACK_JOBS = 32
 
 
+class AdamJobC(ctypes.Structure):
+    _fields_ = [("off", c_i64), ("rows", c_i64), ("cols", c_i64), ("dst", c_vp), ("dst_t", c_vp), ("dst_ld", c_i64),
+                ("dst_t_ld", c_i64), ("first_block", c_i64), ("tiles_c", c_i64), ("dtype", ctypes.c_int32),
+                ("kind", ctypes.c_int32)]
+
+
+MAX_ADAM_JOBS = 256
+ADAM_FLAT, ADAM_TILE = 0, 1
+
+
 class PolicyActArgsC(ctypes.Structure):
     _fields_ = [("trunk_out", c_vp), ("ln_gamma", c_vp * 2), ("ln_beta", c_vp * 2), ("w_mu", c_vp), ("b_mu", c_vp),
                 ("w_value", c_vp), ("b_value", c_vp), ("log_sigma", c_vp), ("noise", c_vp), ("actions", c_vp),
@@ -184,13 +205,15 @@ class PolicyActArgsC(ctypes.Structure):
 class AdamParamsC(ctypes.Structure):
     _fields_ = [("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
                 ("max_norm", ctypes.c_float), ("use_loss_scale", ctypes.c_int32), ("growth_factor", ctypes.c_float),
-                ("backoff_factor", ctypes.c_float), ("growth_interval", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("backoff_factor", ctypes.c_float), ("growth_interval", ctypes.c_int32),
+                ("lr_from_state", ctypes.c_int32)]
 
 
 class OptStateC(ctypes.Structure):
     _fields_ = [("loss_scale", ctypes.c_float), ("growth_tracker", ctypes.c_int32), ("step", ctypes.c_int32),
                 ("skipped", ctypes.c_int32), ("grad_mul", ctypes.c_float), ("step_size", ctypes.c_float),
-                ("bc2_sqrt", ctypes.c_float), ("skip", ctypes.c_int32)]
+                ("bc2_sqrt", ctypes.c_float), ("skip", ctypes.c_int32), ("lr", ctypes.c_float),
+                ("reserved", ctypes.c_int32)]
 
 
 _EXPORTS = {
@@ -209,6 +232,7 @@ _EXPORTS = {
     "phc_timer_offered": (ctypes.c_int64, [c_vp]),
     "phc_timer_total_ms": (ctypes.c_double, [c_vp]),
     "phc_timer_work": (ctypes.c_double, [c_vp]),
+    "phc_timer_durations": (ctypes.c_int32, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32]),
     "phc_gemm_set_timer": (None, [c_vp]),
     "phc_env_step_timed": (ctypes.c_int, [ctypes.POINTER(EnvBuffersC), ctypes.POINTER(MotionLibC),
                                            ctypes.POINTER(StepParamsC), c_vp, c_vp]),
@@ -241,6 +265,10 @@ _EXPORTS = {
     "phc_opt_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int32]),
     "phc_opt_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, ctypes.c_int32, c_vp, ctypes.c_int32,
                                      ctypes.POINTER(AdamParamsC), c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "phc_opt_step_operands": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, ctypes.c_int32, c_vp,
+                                              ctypes.c_int32, ctypes.POINTER(AdamParamsC), c_vp, c_vp, c_vp, c_vp,
+                                              c_vp, ctypes.c_int32, c_i64, c_vp]),
+    "phc_adam_job_blocks": (c_i64, [ctypes.c_int32, c_i64, c_i64]),
     "phc_ppo_workspace_bytes": (ctypes.c_size_t, [c_i64]),
     "phc_tail_layout": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     "phc_tail_blocks": (ctypes.c_int32, [c_i64]),
@@ -452,8 +480,9 @@ def env_step(env_c, mlib, params, timer=None):
 
 
 class KernelTimer:
-    """Start/stop events recorded by the kernel dispatch (phc_timer_*): per-launch kernel time
-    without the event-record overhead of stream events."""
+    """Per-launch kernel time stamped by the timed kernels themselves (phc_timer_*: workgroup starts
+    and wave ends from the device's constant-rate clock): no event is recorded around the dispatch,
+    and launches inside a captured hipGraph are timed too (a graph's slots hold its last replay)."""
 
     def __init__(self, capacity=4096, period=1):
         self.handle = lib().phc_timer_create(int(capacity))
@@ -486,15 +515,34 @@ class KernelTimer:
         """Algorithmic work of the timed launches (phc_twin_gemm: FLOPs)."""
         return lib().phc_timer_work(self.handle)
 
+    def durations_ms(self, cap=65536):
+        """Per-launch ms of the counted launches, in the order they were taken (diagnostics)."""
+        buf = (ctypes.c_double * cap)()
+        n = lib().phc_timer_durations(self.handle, buf, cap)
+        if n < 0:
+            raise RuntimeError("phc_timer_durations failed")
+        return list(buf[:min(n, cap)])
+
     def __del__(self):
         if getattr(self, "handle", None) and _lib is not None:
             _lib.phc_timer_destroy(self.handle)
             self.handle = None
 
 
+_GEMM_TIMER = [None]
+
+
 def gemm_set_timer(timer):
-    """Time every phc_twin_gemm launch outside graph capture into `timer` (None: off)."""
+    """Offer the PPO update's trunk GEMM launches to `timer` (None: off); a launch captured into a
+    graph keeps the timer it was captured with (its slot)."""
     lib().phc_gemm_set_timer(timer.handle if timer is not None else None)
+    _GEMM_TIMER[0] = timer
+
+
+def gemm_timer_id():
+    """Identity of the timer set by gemm_set_timer (a captured graph's key: its launches carry
+    that timer's slots, or none)."""
+    return id(_GEMM_TIMER[0]) if _GEMM_TIMER[0] is not None else None
 
 
 def reset_envs(env_c, mlib, params, mask=None, phase=None, seed=0, counter=0, num_envs=None):
@@ -1021,9 +1069,12 @@ class RowCompactor:
         if not 1 <= len(pairs) <= MAX_ROW_FIELDS:
             raise ValueError(f"RowCompactor: 1..{MAX_ROW_FIELDS} fields")
         self.n, self.capacity = n, capacity
-        self.cursor = torch.zeros(1, dtype=torch.int64, device=device)
+        # [cursor, n_valid, taken, sum n_valid, sum taken] in ONE buffer: the rollout reads the cursor
+        # and the running sums back in one copy (state())
+        self._buf = torch.zeros(5, dtype=torch.int64, device=device)
+        self.cursor = self._buf[0:1]
         # {n_valid, taken} of the last call, then their running sums since reset()
-        self.counts = torch.zeros(4, dtype=torch.int64, device=device)
+        self.counts = self._buf[1:5]
         self.workspace = torch.empty(lib().phc_compact_workspace_bytes(n), dtype=torch.uint8, device=device)
         self._keep = []
         arr = (RowFieldC * len(pairs))()
@@ -1042,7 +1093,8 @@ class RowCompactor:
                 raise ValueError(f"RowCompactor field {k}: unsupported {src.dtype} -> {dst.dtype}")
             _ptr(src, src.dtype, None, f"src{k}")
             _ptr(dst, dst.dtype, None, f"dst{k}")
-            arr[k] = RowFieldC(src.data_ptr(), dst.data_ptr(), elems, kind, 0)
+            flags = ROW_SRC_WORDS if kind == ROW_U8_TO_F32 and _words_inside_storage(src) else 0
+            arr[k] = RowFieldC(src.data_ptr(), dst.data_ptr(), elems, kind, flags)
             self._keep += [src, dst]
         self._arr, self._nf = arr, len(pairs)
 
@@ -1054,8 +1106,14 @@ class RowCompactor:
                "phc_compact_rows")
 
     def reset(self, ptr=0):
-        self.cursor.fill_(ptr)
-        self.counts.zero_()
+        self._buf.zero_()
+        if ptr:
+            self.cursor.fill_(ptr)
+
+    def state(self):
+        """(cursor, sum of n_valid, sum of taken) since reset(), in one device -> host read."""
+        c, _, _, nv, tk = self._buf.tolist()
+        return c, nv, tk
 
 
 def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):

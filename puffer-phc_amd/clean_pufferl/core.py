@@ -22,6 +22,7 @@ import torch
 from .. import _native
 from .. import distributed as D
 from ..optim import FlatAdam
+from ..policies import weight_cache
 from ..policies.fused_ppo import fused_ppo_loss, fused_ppo_supported
 from ..policies.twin_mlp import half_input_width, refresh_twin
 from .ppo_loss import ppo_coefs, ppo_objective
@@ -298,10 +299,10 @@ def _evaluate_graph(components, info):
             steps += 1
             if steps >= min_steps:
                 with profile.eval_misc:
-                    if int(rs.store.cursor.item()) >= experience.batch_size:
+                    cursor, n_valid, taken = rs.store.state()  # one read: the cursor and the running sums
+                    if cursor >= experience.batch_size:
                         break
         with profile.eval_misc:
-            n_valid, taken = rs.store.counts[2:4].tolist()
             for i in step_infos:
                 for k, v in i.items():
                     env_infos[k].append(v)
@@ -474,9 +475,14 @@ def _adv_graph_key(components, info):
     ptrs = tuple(t.data_ptr() for t in (exp.obs, exp.actions, exp.logprobs, exp.values, exp.rewards, exp.dones,
                                          exp.truncateds, exp.env_ids))
     norm = (nm.running_mean.data_ptr(), nm.running_var.data_ptr(), float(nm.epsilon), float(nm.clip)) if nm else None
+    # what decides which outputs compute_advantages produces: the half-precision operand build
+    # (fused policy, its twin layout) and the single-process advantage statistics
+    twin = getattr(pol, "_twin", None)
+    width = half_input_width(twin, _compute_dtype(cfg)) if twin is not None else None
     return (ptrs, norm, exp.batch_size, exp.minibatch_size, exp.num_minibatches, exp.bptt_horizon,
             float(cfg.gamma), float(cfg.gae_lambda), cfg.fused_obs, cfg.fused_loss, cfg.precision,
-            id(components.gae))
+            id(components.gae), bool(getattr(pol, "fused", False)), hasattr(pol, "obs_half_input"), width,
+            D.is_dist())
 
 
 def _compute_advantages_train(components, info):
@@ -490,10 +496,12 @@ def _compute_advantages_train(components, info):
         st = {"graph": None, "key": None, "out": None, "failed": False}
         components._adv_graph = st
     key = _adv_graph_key(components, info)
+    st["replayed"] = False
     if st["graph"] is not None and st["key"] == key:
         st["graph"].replay()
         for k, v in st["attrs"].items():  # an eager call in between may have re-pointed them
             setattr(exp, k, v)
+        st["replayed"] = True
         return st["out"]
     if st["failed"] or st["key"] != key:  # first sight of this key: eager (lazy initialisation)
         st["graph"], st["key"] = None, key
@@ -530,6 +538,121 @@ def _fill_losses(losses, a):
     losses.explained_variance = float(a[13]) if a[12] != 0 else float("nan")
 
 
+# train()'s minibatch loop (update_epochs x num_minibatches fused minibatches: trunks, tail, PPO
+# objective, backward, clip + Adam) and the logged loss row replayed from ONE captured hipGraph: the
+# ~40 launches per minibatch run back to back with no host in between.  Eligible: the single-process
+# fused path with FlatAdam and the reference's defaults (no AMP, no recurrent policy, no target-KL early
+# stop, no L2-init loss, the bound term a no-grad constant), once train()'s advantage pass itself
+# replays from its graph (fixed input addresses).  PHC_TRAIN_GRAPH=0: eager.
+TRAIN_GRAPH = os.environ.get("PHC_TRAIN_GRAPH", "1") != "0"
+
+
+def _train_graph_eligible(components, info, pol):
+    cfg, exp, opt = info.config, components.experience, components.optimizer
+    adv = getattr(components, "_adv_graph", None)
+    if not (TRAIN_GRAPH and exp.obs.is_cuda and not info.use_amp_obs and exp.lstm_h is None and not D.is_dist()
+            and isinstance(opt, FlatAdam) and opt.param_init is not None and cfg.l2_reg_coef == 0
+            and cfg.target_kl is None and not cfg.bound_loss_grad and STORE_GRADS and cfg.fused_loss
+            and adv is not None and adv.get("replayed") and getattr(exp, "b_obs_half", None) is not None
+            and hasattr(pol, "forward_train") and getattr(pol, "fused", False)):
+        return False
+    with autocast(cfg):
+        return fused_ppo_supported(pol, exp.b_obs_half[:exp.minibatch_size])
+
+
+_UNIT_MS = {}
+
+
+def _fused_update(components, info, pol):
+    """The minibatch loop of the eligible path (the same launches as train()'s general loop with
+    fused_mb and opt_l2) and the loss row; returns the row (device float64 [14]).  Captured into the
+    train graph, or run eagerly (first sight of a configuration)."""
+    cfg, exp, opt = info.config, components.experience, components.optimizer
+    dev = exp.obs.device
+    acc_ppo = torch.zeros(7, dtype=torch.float64, device=dev)
+    acc_opt = torch.zeros(3, dtype=torch.float64, device=dev)
+    mbl_ref = _rollout_bound_loss(components, pol)
+    total = exp.num_minibatches * cfg.update_epochs
+    mbs = exp.minibatch_size
+    coefs = ppo_coefs(cfg, pol.soft_bound)
+    if cfg.norm_adv:
+        adv_ms = _adv_mean_std(exp)
+    else:
+        key = str(dev)
+        if key not in _UNIT_MS:
+            _UNIT_MS[key] = torch.tensor([0.0, 1.0], dtype=torch.float32, device=dev)
+        unit = _UNIT_MS[key]
+    for _epoch in range(cfg.update_epochs):
+        for mb in range(exp.num_minibatches):
+            obs = exp.b_obs_half[mb * mbs:(mb + 1) * mbs]
+            atn = exp.b_actions[mb].reshape(-1, exp.b_actions.shape[-1])
+            with autocast(cfg):
+                loss, st = fused_ppo_loss(pol, obs, atn, exp.b_logprobs[mb].reshape(-1), exp.b_advantages[mb],
+                                          adv_ms[mb] if cfg.norm_adv else unit, exp.b_values[mb], exp.b_returns[mb],
+                                          coefs, store_grads=True)
+            opt.backward(loss)
+            opt.fused_step(cfg.max_grad_norm)
+            with torch.no_grad():
+                acc_ppo += st
+                acc_opt += opt.norms
+    with torch.no_grad():
+        acc = torch.zeros(12, dtype=torch.float64, device=dev)
+        i7, i67, i02 = _row_index(dev)
+        acc.index_add_(0, i7, acc_ppo / total)
+        acc.index_add_(0, i67, acc_opt.index_select(0, i02) / total)
+        if mbl_ref is not None:
+            acc[9] = mbl_ref.double()
+        return torch.cat([acc, exp.ev_pair])
+
+
+def _train_graph_key(components, info, pol):
+    cfg, exp = info.config, components.experience
+    rs = getattr(components, "rollout", None)
+    return (id(components._adv_graph.get("graph")), id(rs), rs.mu.data_ptr() if rs is not None else None,
+            cfg.update_epochs, cfg.norm_adv, float(cfg.max_grad_norm), float(cfg.clip_coef), float(cfg.vf_clip_coef),
+            float(cfg.vf_coef), float(cfg.ent_coef), float(cfg.bound_coef), bool(cfg.clip_vloss), cfg.precision,
+            id(components.optimizer), components.optimizer.use_loss_scale, _native.gemm_timer_id(),
+            weight_cache.layout_key(None, list(pol.parameters())), weight_cache.plans_version())
+
+
+def _train_minibatches_graphed(components, info, pol):
+    """The loss row of this train() call from the train graph (captured on the second eligible call
+    with an unchanged key, replayed after), or eagerly; None when not eligible."""
+    if not _train_graph_eligible(components, info, pol):
+        return None
+    opt = components.optimizer
+    st = components.__dict__.setdefault("_train_graph", {"graph": None, "key": None, "row": None, "failed": False})
+    key = _train_graph_key(components, info, pol)
+    opt.sync_lr()
+    if st["graph"] is not None and st["key"] == key:
+        fresh = opt.fresh_operand_owners() if st["writes_operands"] else []
+        st["graph"].replay()
+        # the replay rewrote the parameters behind every host-side cache key (FlatAdam.fused_step
+        # bumps the generation when it runs on the host; a replay does not run it); the operand
+        # caches its captured steps rewrote stay current
+        opt.operands_written(fresh)
+        return st["row"]
+    if st["failed"] or st["key"] != key:  # first sight of this configuration: eager
+        st["graph"], st["key"] = None, key
+        return _fused_update(components, info, pol)
+    try:
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            row = _fused_update(components, info, pol)
+    except Exception:  # noqa: BLE001  (an op that cannot be captured: stay eager)
+        st["failed"] = True
+        torch.cuda.synchronize()
+        return _fused_update(components, info, pol)
+    st["graph"], st["row"] = g, row
+    # captured with the step writing the operand copies (FlatAdam's job table in use)
+    st["writes_operands"] = opt._ops is not None and opt._ops_v == weight_cache.plans_version()
+    fresh = opt.fresh_operand_owners() if st["writes_operands"] else []
+    g.replay()
+    opt.operands_written(fresh)
+    return row
+
+
 def train(components, info, utilization=None):
     """PPO update (core.py:206-440)."""
     cfg, profile = info.config, info.profile
@@ -545,6 +668,10 @@ def train(components, info, utilization=None):
     with profile.train:
         with profile.train_misc:
             _compute_advantages_train(components, info)
+            row = _train_minibatches_graphed(components, info, pol)
+        if row is not None:
+            return _finish_train(components, info, row)
+        with profile.train_misc:
             if info.use_amp_obs:
                 amp_obs_demo = components.vecenv.fetch_amp_obs_demo()
                 amp_mb = amp_obs_demo.shape[0]
@@ -741,27 +868,38 @@ def train(components, info, utilization=None):
                 ev_t = 1 - torch.var(y_true - y_pred, unbiased=False) / var_y
                 ev_pair = torch.stack([var_y, ev_t]).double()
             row = torch.cat([acc, ev_pair])
-            if row.is_cuda:
-                slot = _PINNED.take(row, None)
-                host = slot[0]
-                host.copy_(row, non_blocking=True)
-                done = torch.cuda.Event()
-                done.record()
-                losses = PendingLossComponents(host, done, _fill_losses)
-                slot[1] = losses
-            else:
-                losses = LossComponents()
-                _fill_losses(losses, row.numpy())
-            info.epoch += 1
-            info.losses = losses
-            done_training = info.global_step >= cfg.total_timesteps
-            if done_training or profile.update(components, info):
-                info.stats.mean_and_log(components, info, losses)
-                info.stats.clear()
-            if D.rank() == 0 and (info.epoch % cfg.checkpoint_interval == 0 or done_training):
-                save_checkpoint(components.uncompiled_policy, components.optimizer, cfg, info.exp_id, info.epoch,
-                                info.global_step)
-                info.msg = f"Checkpoint saved at update {info.epoch}"
+        return _finish_train(components, info, row, anneal=False)
+
+
+def _finish_train(components, info, row, anneal=True):
+    """train()'s host tail: the lr anneal, the loss row's non-blocking readback, logging and the
+    checkpoint cadence (core.py:397-440).  Runs inside train()'s profile.train context."""
+    cfg, profile = info.config, info.profile
+    with profile.train_misc:
+        if anneal and cfg.anneal_lr:  # core.py:405-408 (the caller's exp decay overrides it, as there)
+            frac = 1.0 - info.global_step / cfg.total_timesteps
+            components.optimizer.param_groups[0]["lr"] = frac * cfg.learning_rate
+        if row.is_cuda:
+            slot = _PINNED.take(row, None)
+            host = slot[0]
+            host.copy_(row, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record()
+            losses = PendingLossComponents(host, done, _fill_losses)
+            slot[1] = losses
+        else:
+            losses = LossComponents()
+            _fill_losses(losses, row.numpy())
+        info.epoch += 1
+        info.losses = losses
+        done_training = info.global_step >= cfg.total_timesteps
+        if done_training or profile.update(components, info):
+            info.stats.mean_and_log(components, info, losses)
+            info.stats.clear()
+        if D.rank() == 0 and (info.epoch % cfg.checkpoint_interval == 0 or done_training):
+            save_checkpoint(components.uncompiled_policy, components.optimizer, cfg, info.exp_id, info.epoch,
+                            info.global_step)
+            info.msg = f"Checkpoint saved at update {info.epoch}"
     return losses
 
 

@@ -12,6 +12,20 @@ from typing import Literal, Optional, Tuple
 from .envs.state_init import StateInit
 
 
+def env_flag(name, default):
+    """A boolean switch from the environment, read when a config is constructed (not at import):
+    1 / true / yes / on enable it, 0 / false / no / off disable it, anything else is an error."""
+    v = os.environ.get(name)
+    if v is None or v.strip() == "":
+        return default
+    v = v.strip().lower()
+    if v in ("1", "true", "yes", "on"):
+        return True
+    if v in ("0", "false", "no", "off"):
+        return False
+    raise ValueError(f"{name}={v!r}: expected 1/true/yes/on or 0/false/no/off")
+
+
 @dataclass
 class DeviceConfig:
     device_type: Literal["cpu", "cuda"] = "cuda"
@@ -196,7 +210,7 @@ class TrainConfig(DeviceConfig):
     precision: str = "fp16"
     # replay policy inference + experience store of each rollout step from a captured hipGraph
     # (the env step itself stays eager); False = the reference's eager loop
-    rollout_graph: bool = os.environ.get("PHC_ROLLOUT_GRAPH", "1") == "1"
+    rollout_graph: bool = field(default_factory=lambda: env_flag("PHC_ROLLOUT_GRAPH", True))
     # PPO objective (ratio / clipping / value / bound losses and their gradients) in two HIP
     # kernels (clean_pufferl/ppo_loss.py); False = the reference's eager expression
     fused_loss: bool = True
@@ -208,4 +222,4 @@ class TrainConfig(DeviceConfig):
     fused_obs: bool = True
     # rollout: the env step kernel also writes RunningNorm(obs) as the first GEMM's half operand
     # (HumanoidPHC.set_obs_operand); False = a phc_obs_half launch per rollout step
-    fused_obs_operand: bool = os.environ.get("PHC_FUSED_OBS_OPERAND", "1") == "1"
+    fused_obs_operand: bool = field(default_factory=lambda: env_flag("PHC_FUSED_OBS_OPERAND", True))

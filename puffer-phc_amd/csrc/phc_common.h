@@ -28,40 +28,74 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 
 }  // namespace phc
 
-// measurement timer (phc_timer_*): one start/stop event pair per timed launch, recorded by the
-// dispatch itself, plus the algorithmic work (bytes or FLOPs) the timed launches did
+// Measurement timer (phc_timer_*): a timed launch stamps itself.  Each timed launch gets a slot in the
+// timer's device buffer, [2 * grid] words: word w = the start of workgroup w, word grid + w = its end
+// (after every wave of it has drained its memory operations), both read from s_memrealtime (the
+// constant-rate clock every CU reads alike, hipDeviceAttributeWallClockRate).  The launch's duration is
+// the latest end minus the earliest start.  Plain stores, one word per workgroup each: no atomics (2,048
+// waves adding to one word serialised at the memory side and lengthened a timed env step by 16 us).
+// Unlike start / stop events (hipExtLaunchKernel) this works inside a captured hipGraph (events recorded
+// during a capture cannot be timed on ROCm 7.2: tools/graph_timer_probe.py) and leaves the stream no idle
+// time around the launch; a slot captured into a graph holds its LAST replay.
 struct phc_kernel_timer {
-  std::vector<hipEvent_t> start, stop;
-  int32_t used = 0;
-  double work = 0.0;
-  int32_t period = 1;  // time every period-th launch (phc_timer_set_period)
-  int64_t seen = 0;    // launches offered to the timer
+  struct Slot {
+    int64_t off;                   // first word of the slot
+    int32_t grid;                  // workgroups of the launch
+    bool graph;                    // taken while its stream was capturing: re-stamped by every replay
+    double work;                   // the launch's algorithmic work (bytes or FLOPs)
+    unsigned long long end_at_reset;
+  };
+  unsigned long long *dev = nullptr;
+  int64_t cap_words = 0, used_words = 0;
+  int32_t capacity = 0;            // slots
+  std::vector<Slot> slots;
+  size_t base = 0;                 // slots taken before the last reset (graph slots among them still count)
+  int32_t period = 1;              // stamp every period-th launch offered (phc_timer_set_period)
+  int64_t seen = 0;                // launches offered since the last reset
+  double tick_hz = 1.0e8;
 };
 
-// The start / stop events for this launch when the timer samples it (every period-th launch offered,
-// while capacity lasts), else null events: the dispatch then records nothing.  A timed dispatch
-// costs the stream 5-10 us of idle time around it (bench.py's PPO iteration: ~140 us per minibatch
-// with every GEMM timed), so bench.py samples instead of timing every launch.
-inline bool phc_timer_take(phc_kernel_timer *t, hipEvent_t *ev0, hipEvent_t *ev1) {
-  *ev0 = *ev1 = nullptr;
-  if (!t) return false;
-  const bool take = t->seen++ % t->period == 0 && t->used < (int32_t)t->start.size();
-  if (!take) return false;
-  *ev0 = t->start[t->used];
-  *ev1 = t->stop[t->used];
-  t->used += 1;
-  return true;
+// The slot for this launch when the timer samples it (every period-th launch offered, while space
+// lasts), else null: the kernel then stamps nothing.
+inline unsigned long long *phc_timer_take(phc_kernel_timer *t, hipStream_t st, int64_t grid, double work) {
+  if (!t || grid <= 0) return nullptr;
+  if (t->seen++ % t->period != 0) return nullptr;
+  if ((int32_t)t->slots.size() >= t->capacity || t->used_words + 2 * grid > t->cap_words) return nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool graph = hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+  phc_kernel_timer::Slot s{t->used_words, (int32_t)grid, graph, work, 0ull};
+  t->slots.push_back(s);
+  t->used_words += 2 * grid;
+  return t->dev + s.off;
 }
 
-// a dispatch the timer samples records its events through hipExtLaunchKernel; every other one is a
-// plain launch (the GEMMs already did this; the env / physics steps went through the extended path
-// with null events on every step)
 template <typename F, typename... Args>
-inline void phc_launch(F kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
-                       Args... args) {
-  if (ev0) hipExtLaunchKernelGGL(kernel, grid, block, lds, st, ev0, ev1, 0, args...);
-  else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+inline void phc_launch(F kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, Args... args) {
+  hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
 }
+
+#ifdef __HIPCC__
+// kernel side of the timer: every workgroup stamps its start, and its end once all of its waves have
+// drained their memory operations; clk null = untimed launch (uniform branches; every thread of the
+// workgroup must reach launch_clock_end)
+__device__ __forceinline__ void launch_clock_begin(unsigned long long *clk) {
+  if (clk && threadIdx.x == 0) {
+    const unsigned wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    clk[wg] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+__device__ __forceinline__ void launch_clock_end(unsigned long long *clk) {
+  if (clk) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned g = gridDim.x * gridDim.y * gridDim.z;
+      const unsigned wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+      clk[g + wg] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+#endif
 
 namespace phc {
 
@@ -126,6 +160,16 @@ struct Blend {
 };
 
 __device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+
+// Cross-lane hand-off through a wave's own LDS region: a lane reads what other lanes of the same wave
+// wrote (or overwrites what they read).  The LDS instructions of one wave execute in issue order, so
+// only the compiler could break the hand-off by moving a ds_read / ds_write across it (the two sides
+// touch different addresses per lane, so nothing else orders them): a wavefront-scope fence plus the
+// wave barrier pin the issue order.  No instruction is emitted.
+__device__ __forceinline__ void wave_lds_handoff() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // motion_lib.py:655-665 _calc_frame_blend (bit-exact with -ffp-contract=off)
 __device__ __forceinline__ Blend frame_blend(float time, const MotionScalars &m) {

@@ -96,6 +96,7 @@ struct GemmArgs {
   int discard;
   int aux_half;  // aux in the operand type T instead of fp32
   int nt;        // non-temporal epilogue traffic: 1 = out stores, 2 = aux stores, 4 = aux loads
+  unsigned long long *clk;  // the launch's timer slot (phc_timer_take), null when untimed
 };
 
 // 4 consecutive aux values (fp32, or the operand type T when g.aux_half) at element offset off
@@ -909,6 +910,7 @@ template <typename T, typename OutT, int EPI, typename TL, bool PERSIST>
 __global__ __launch_bounds__(TL::kThreads) __attribute__((amdgpu_waves_per_eu(TL::kWavesPerEU, 8))) void k_twin_gemm(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][A BM rows | B BN rows]
   const int nwg = gridDim.x, orig = blockIdx.x;
+  launch_clock_begin(g.clk);
   if constexpr (!PERSIST) {
     twin_gemm_tile<T, OutT, EPI, TL>(g, smem, xcd_first(nwg, orig % 8) + orig / 8);
   } else {
@@ -920,6 +922,7 @@ __global__ __launch_bounds__(TL::kThreads) __attribute__((amdgpu_waves_per_eu(TL
       lds_barrier();  // the epilogue image is read out before the next tile's operands land
     }
   }
+  launch_clock_end(g.clk);
 }
 
 // ------------------------------------------------------------------ weight gradients (R21) --
@@ -942,6 +945,7 @@ struct WgradArgs {
   int tiles_m, tiles_n;
   float *out;
   int discard;
+  unsigned long long *clk;  // the launch's timer slot, null when untimed
 };
 
 __device__ __forceinline__ int wg_swz(int r) { return ((r & 3) | ((r >> 1) & 4)) << 1; }
@@ -1046,6 +1050,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad(WgradArgs g) {
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
 
   const int nwg = gridDim.x, orig = blockIdx.x;
+  launch_clock_begin(g.clk);
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int tn = wg % g.tiles_n;
@@ -1098,6 +1103,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad(WgradArgs g) {
         if (row + e < g.m) o[(int64_t)(row + e) * g.n + col] = acc[i][j][e];
     }
   }
+  launch_clock_end(g.clk);
 }
 
 // Grouped form: the weight gradients of several layers in ONE launch, no split: every output tile
@@ -1116,6 +1122,7 @@ struct WgradGroupArgs {
   WgradProblem p[kWgradGroupMax];
   int count, accumulate, discard;
   int64_t rows;
+  unsigned long long *clk;  // the launch's timer slot, null when untimed
 };
 
 template <typename T, typename TL>
@@ -1126,6 +1133,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad_group(WgradGroupArgs ga)
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
 
   const int nwg = gridDim.x, orig = blockIdx.x;
+  launch_clock_begin(ga.clk);
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   int pi = 0;
@@ -1187,6 +1195,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad_group(WgradGroupArgs ga)
       }
     }
   }
+  launch_clock_end(ga.clk);
 }
 
 // tile configurations
@@ -1217,7 +1226,9 @@ static void gemm_tile_dims(int cfg, int *bm, int *bn) {
 }
 
 static phc_kernel_timer *g_gemm_timer = nullptr;  // bench.py measurement aid (phc_gemm_set_timer)
-static thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;  // this launch's timer events
+// phc_twin_gemm launches of more rows than this are offered to the timer (the PPO minibatch's trunk
+// GEMMs; the rollout's 4,096-row layers are not part of the measured family)
+constexpr int64_t kTimedMinRows = 4096;
 
 template <typename T, typename OutT, int EPI, typename TL>
 static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
@@ -1230,10 +1241,7 @@ static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
     return true;
   }();
   (void)attr;
-  if (g_ev0)
-    hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), lds, st, g_ev0, g_ev1, 0, g);
-  else
-    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), lds, st, g);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), lds, st, g);
 }
 
 template <typename T, typename OutT, int EPI>
@@ -1275,10 +1283,7 @@ static void launch_wgrad(const WgradArgs &g, int64_t blocks, hipStream_t st) {
     return true;
   }();
   (void)attr;
-  if (g_ev0)
-    hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g_ev0, g_ev1, 0, g);
-  else
-    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
 }
 
 template <typename T>
@@ -1291,10 +1296,7 @@ static void launch_wgrad_group(const WgradGroupArgs &g, int64_t blocks, hipStrea
     return true;
   }();
   (void)attr;
-  if (g_ev0)
-    hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g_ev0, g_ev1, 0, g);
-  else
-    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(TL::kThreads), TL::kLdsBytes, st, g);
 }
 
 }  // namespace phc
@@ -1391,15 +1393,9 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   }();
   const int64_t out_bytes = d->m * (int64_t)d->batch * d->n * (d->out_dtype == PHC_DT_F32 ? 4 : 2);
   g.nt = (out_bytes >= nt_out_min ? 1 : 0) | ((nt_aux & 1) ? 2 : 0) | ((nt_aux & 2) ? 4 : 0);
-  g_ev0 = g_ev1 = nullptr;
-  if (g_gemm_timer) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
-        phc_timer_take(g_gemm_timer, &g_ev0, &g_ev1))
-      g_gemm_timer->work += 2.0 * (double)d->m * d->n * d->k * d->batch;
-  }
+  // the training GEMMs only: the rollout's (inside its captured graph, 4096 rows) stay untimed
+  if (d->m > kTimedMinRows) g.clk = phc_timer_take(g_gemm_timer, st, blocks, 2.0 * (double)d->m * d->n * d->k * d->batch);
   launch_gemm(d->dtype, d->out_dtype, d->epilogue, cfg, g, blocks, st);
-  g_ev0 = g_ev1 = nullptr;
   if (bias_grad) {
     const int c = d->batch * d->n;
     hipLaunchKernelGGL(k_colsum<>, dim3((unsigned)((c + 63) / 64)), dim3(256), 0, st,
@@ -1442,16 +1438,9 @@ extern "C" int phc_weight_grad(const phc_wgrad_desc *d, void *stream) {
   static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
   g.discard = discard ? 1 : 0;
   hipStream_t st = as_stream(stream);
-  g_ev0 = g_ev1 = nullptr;
-  if (g_gemm_timer) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
-        phc_timer_take(g_gemm_timer, &g_ev0, &g_ev1))
-      g_gemm_timer->work += 2.0 * (double)d->m * d->n * d->rows * d->batch;
-  }
+  g.clk = phc_timer_take(g_gemm_timer, st, blocks, 2.0 * (double)d->m * d->n * d->rows * d->batch);
   if (d->dtype == PHC_DT_F16) launch_wgrad<_Float16>(g, blocks, st);
   else launch_wgrad<__bf16>(g, blocks, st);
-  g_ev0 = g_ev1 = nullptr;
   return check_launch("weight_grad");
 }
 
@@ -1506,15 +1495,8 @@ extern "C" int phc_weight_grad_group(const phc_wgrad_problem *probs, int32_t cou
   static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
   ga.discard = discard ? 1 : 0;
   hipStream_t st = as_stream(stream);
-  g_ev0 = g_ev1 = nullptr;
-  if (g_gemm_timer) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
-        phc_timer_take(g_gemm_timer, &g_ev0, &g_ev1))
-      g_gemm_timer->work += flops;
-  }
+  ga.clk = phc_timer_take(g_gemm_timer, st, blocks, flops);
   if (dtype == PHC_DT_F16) launch_wgrad_group<_Float16>(ga, blocks, st);
   else launch_wgrad_group<__bf16>(ga, blocks, st);
-  g_ev0 = g_ev1 = nullptr;
   return check_launch("weight_grad_group");
 }

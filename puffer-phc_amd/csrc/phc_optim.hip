@@ -190,7 +190,8 @@ __global__ __launch_bounds__(kFinThreads) void k_opt_finish(const double *__rest
   const double t = (double)st->step;
   const double bc1 = 1.0 - pow((double)hp.beta1, t), bc2 = 1.0 - pow((double)hp.beta2, t);
   st->grad_mul = inv * clip;
-  st->step_size = (float)((double)hp.lr / bc1);
+  const float lr = hp.lr_from_state ? st->lr : hp.lr;
+  st->step_size = (float)((double)lr / bc1);
   st->bc2_sqrt = (float)sqrt(bc2);
   st->skip = skip;
   if (norm_out) {
@@ -423,6 +424,135 @@ __global__ __launch_bounds__(kPackThreads) void k_pack_weights(PackJobs js) {
   }
 }
 
+// ------------------------------------------------- Adam + GEMM-operand copies (phc_opt_step_operands) --
+// k_adam's arithmetic (same expression order: bit-identical parameters and moments) over a job table:
+// tile jobs take a 64 x 64 tile of one parameter per workgroup (thread t: 4 consecutive columns of rows
+// t / 16 + 16 i) and write the updated values converted row-wise (dst) and, through the LDS tile,
+// transposed (dst_t) — what phc_pack_weights would write from the same fp32 values; flat jobs take
+// 4,096 consecutive elements per workgroup.
+__device__ __forceinline__ void adam_one(float &p, float g, float &m, float &v, float gm, float ss, float bc2s, float b1,
+                                         float b2, float eps) {
+  const float gk = g * gm;
+  m = b1 * m + (1.0f - b1) * gk;
+  v = b2 * v + (1.0f - b2) * gk * gk;
+  p -= ss * m / (sqrtf(v) / bc2s + eps);
+}
+
+constexpr int kAdamFlatElems = 4096;
+
+__global__ __launch_bounds__(kPackThreads) void k_adam_ops(float *__restrict__ p, const float *__restrict__ g,
+                                                           float *__restrict__ m, float *__restrict__ v,
+                                                           const phc_adam_job *__restrict__ jobs, int njobs,
+                                                           phc_adam_params hp, const phc_opt_state *__restrict__ st) {
+  __shared__ float tile[kPackTile][kPackTile + 1];
+  if (st->skip) return;
+  // this workgroup's job: every thread tests one job's first block (one memory round, njobs <= 256)
+  const int flag = (int)threadIdx.x < njobs && jobs[threadIdx.x].first_block <= (int64_t)blockIdx.x;
+  const int q = __syncthreads_count(flag) - 1;
+  const phc_adam_job &job = jobs[q];
+  const int64_t t = (int64_t)blockIdx.x - job.first_block;
+  const float gm = st->grad_mul, ss = st->step_size, bc2s = st->bc2_sqrt;
+  const float b1 = hp.beta1, b2 = hp.beta2, eps = hp.eps;
+  if (job.kind == PHC_ADAM_FLAT) {
+    const int64_t e0 = job.off + t * kAdamFlatElems, e1 = job.off + job.rows;
+#pragma unroll 4
+    for (int k = 0; k < kAdamFlatElems / kPackThreads; ++k) {
+      const int64_t e = e0 + threadIdx.x + (int64_t)k * kPackThreads;
+      if (e < e1) {
+        float pe = p[e], me = m[e], ve = v[e];
+        adam_one(pe, g[e], me, ve, gm, ss, bc2s, b1, b2, eps);
+        p[e] = pe; m[e] = me; v[e] = ve;
+      }
+    }
+    return;
+  }
+  const int64_t r0 = (t / job.tiles_c) * kPackTile, c0 = (t % job.tiles_c) * kPackTile;
+  const int cq = (threadIdx.x & 15) * 4, rq = threadIdx.x >> 4;
+  const int esz = job.dtype == PHC_DT_F32 ? 4 : 2;
+  // 16-B accesses when every tile row starts 16-B aligned (FlatGrads aligns each parameter's slice
+  // to 64 B); 8-B pairs when rows are only 8-B aligned (the 934-column first layer)
+  const bool vec = (job.off % 4 == 0) && (job.cols % 4 == 0);
+  const bool vec2 = !vec && (job.off % 2 == 0) && (job.cols % 2 == 0);
+  const bool dst_vec = job.dst && ((job.dst_ld * esz) % (4 * esz) == 0) &&
+                       ((reinterpret_cast<uintptr_t>(job.dst) & (4 * esz - 1)) == 0);
+#pragma unroll
+  for (int i = 0; i < kPackTile / 16; ++i) {
+    const int rr = rq + 16 * i;
+    const int64_t r = r0 + rr, c = c0 + cq;
+    float nv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const bool row_in = r < job.rows;
+    const bool full = row_in && c + 3 < job.cols;
+    const int64_t e = job.off + r * job.cols + c;
+    if (full && vec) {
+      float4 pv = *reinterpret_cast<float4 *>(p + e);
+      const float4 gv = *reinterpret_cast<const float4 *>(g + e);
+      float4 mv = *reinterpret_cast<float4 *>(m + e);
+      float4 vv = *reinterpret_cast<float4 *>(v + e);
+      float *pp = &pv.x, *mm = &mv.x, *vq = &vv.x;
+      const float *gg = &gv.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        adam_one(pp[k], gg[k], mm[k], vq[k], gm, ss, bc2s, b1, b2, eps);
+        nv[k] = pp[k];
+      }
+      *reinterpret_cast<float4 *>(p + e) = pv;
+      *reinterpret_cast<float4 *>(m + e) = mv;
+      *reinterpret_cast<float4 *>(v + e) = vv;
+    } else if (full && vec2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float2 pv = *reinterpret_cast<float2 *>(p + e + 2 * h);
+        const float2 gv = *reinterpret_cast<const float2 *>(g + e + 2 * h);
+        float2 mv = *reinterpret_cast<float2 *>(m + e + 2 * h);
+        float2 vv = *reinterpret_cast<float2 *>(v + e + 2 * h);
+        adam_one(pv.x, gv.x, mv.x, vv.x, gm, ss, bc2s, b1, b2, eps);
+        adam_one(pv.y, gv.y, mv.y, vv.y, gm, ss, bc2s, b1, b2, eps);
+        nv[2 * h] = pv.x;
+        nv[2 * h + 1] = pv.y;
+        *reinterpret_cast<float2 *>(p + e + 2 * h) = pv;
+        *reinterpret_cast<float2 *>(m + e + 2 * h) = mv;
+        *reinterpret_cast<float2 *>(v + e + 2 * h) = vv;
+      }
+    } else if (row_in) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < job.cols) {
+          float pe = p[e + k], me = m[e + k], ve = v[e + k];
+          adam_one(pe, g[e + k], me, ve, gm, ss, bc2s, b1, b2, eps);
+          p[e + k] = pe; m[e + k] = me; v[e + k] = ve;
+          nv[k] = pe;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tile[rr][cq + k] = nv[k];
+    if (job.dst && row_in) {
+      if (full) {
+        pack_store4(job.dst, r * job.dst_ld + c, job.dtype, nv, dst_vec);
+      } else {
+        for (int k = 0; k < 4; ++k)
+          if (c + k < job.cols) pack_store(job.dst, r * job.dst_ld + c + k, job.dtype, nv[k]);
+      }
+    }
+  }
+  if (!job.dst_t) return;
+  __syncthreads();
+  const bool t_vec = ((job.dst_t_ld * esz) % (4 * esz) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(job.dst_t) & (4 * esz - 1)) == 0);
+#pragma unroll
+  for (int i = 0; i < kPackTile / 16; ++i) {  // dst_t row c0 + cc, columns r0 + rq4 .. +3
+    const int cc = (threadIdx.x >> 4) + 16 * i, rq4 = (threadIdx.x & 15) * 4;
+    const int64_t c = c0 + cc, r = r0 + rq4;
+    if (c >= job.cols) continue;
+    const float w4[4] = {tile[rq4][cc], tile[rq4 + 1][cc], tile[rq4 + 2][cc], tile[rq4 + 3][cc]};
+    if (r + 3 < job.rows) {
+      pack_store4(job.dst_t, c * job.dst_t_ld + r, job.dtype, w4, t_vec);
+    } else {
+      for (int k = 0; k < 4; ++k)
+        if (r + k < job.rows) pack_store(job.dst_t, c * job.dst_t_ld + r + k, job.dtype, w4[k]);
+    }
+  }
+}
+
 }  // namespace phc
 
 using namespace phc;
@@ -505,6 +635,37 @@ extern "C" int phc_opt_step(float *param, const float *grad, float *exp_avg, flo
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptBlock), 0, st, param, grad, exp_avg, exp_avg_sq, n,
                      *hp, state);
   return check_launch("opt_step");
+}
+
+extern "C" int64_t phc_adam_job_blocks(int32_t kind, int64_t rows, int64_t cols) {
+  if (rows <= 0) return 0;
+  if (kind == PHC_ADAM_FLAT) return (rows + kAdamFlatElems - 1) / kAdamFlatElems;
+  if (cols <= 0) return 0;
+  return ((rows + kPackTile - 1) / kPackTile) * ((cols + kPackTile - 1) / kPackTile);
+}
+
+extern "C" int phc_opt_step_operands(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                                     const int64_t *blk_range, int32_t nblk, const int32_t *seg_blk, int32_t nseg,
+                                     const phc_adam_params *hp, phc_opt_state *state, float *norm_out,
+                                     const float *param_init, void *workspace, const phc_adam_job *jobs, int32_t njobs,
+                                     int64_t nblocks, void *stream) {
+  PHC_REQUIRE(param && grad && exp_avg && exp_avg_sq && blk_range && seg_blk && hp && state && workspace && jobs,
+              "opt_step_operands: null argument");
+  PHC_REQUIRE(n > 0 && nblk > 0 && nseg > 0, "opt_step_operands: empty parameter set");
+  PHC_REQUIRE(njobs >= 1 && njobs <= PHC_MAX_ADAM_JOBS && nblocks >= 1 && nblocks < (1ll << 31),
+              "opt_step_operands: 1..%d jobs, 1..2^31 workgroups", PHC_MAX_ADAM_JOBS);
+  PHC_REQUIRE(!hp->use_loss_scale || hp->growth_interval > 0, "opt_step_operands: bad loss-scale growth interval");
+  hipStream_t st = as_stream(stream);
+  double *part_sq = static_cast<double *>(workspace);
+  double *part_l2 = param_init ? part_sq + nblk : nullptr;
+  int *part_bad = reinterpret_cast<int *>(part_sq + 2 * (int64_t)nblk);
+  hipLaunchKernelGGL(k_grad_partials, dim3((unsigned)nblk), dim3(kOptBlock), 0, st, grad, blk_range, part_sq,
+                     part_bad, param, param_init, part_l2);
+  hipLaunchKernelGGL(k_opt_finish, dim3(1), dim3(kFinThreads), 0, st, part_sq, part_bad, part_l2, blk_range, seg_blk,
+                     (int)nseg, *hp, state, norm_out);
+  hipLaunchKernelGGL(k_adam_ops, dim3((unsigned)nblocks), dim3(kPackThreads), 0, st, param, grad, exp_avg, exp_avg_sq,
+                     jobs, (int)njobs, *hp, state);
+  return check_launch("opt_step_operands");
 }
 
 extern "C" size_t phc_opt_workspace_bytes(int32_t nblk) {

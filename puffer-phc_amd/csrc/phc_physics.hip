@@ -79,6 +79,7 @@ struct PhysConsts {
   float kp_scale, kd_scale, kn, cn, mu, ct, g;
   float ang_damp, max_w;
   int self_col;
+  unsigned long long *clk;  // the launch's timer slot (phc_timer_take), null when untimed
 };
 
 struct M3 {
@@ -297,6 +298,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
   const int64_t ev = env < e.n ? env : e.n - 1;
   float(*S)[kSlot] = slots[sub];
   float(*O)[kOut] = outw[sub];
+  launch_clock_begin(c.clk);
   const float dt = c.dt;
 
   // ---- body table (indices clamped: a corrupt model cannot address outside the slots)
@@ -744,8 +746,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     }
   }
   kinematics();
-  if (!act) return;  // no barrier follows
-  {
+  if (act) {  // no barrier follows
     const M3 R = m3_quat(Q.x, Q.y, Q.z, Q.w);
     // the centre of mass's linear velocity (PhysX's rigid-body velocity): v + w x com
     const v3 vw = m3_v(R, vadd(v, cross3(w, ld3(T + T_COM)))), ww = m3_v(R, w);
@@ -760,13 +761,14 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       for (int k = 0; k < kRec; ++k) rt[k] = o[k];
     }
   }
-  if (b > 0) {
+  if (act && b > 0) {
     const v3 ej = rotvec_of(r);
     float *d = e.dof_state + (env * PHC_NUM_DOF + 3 * (b - 1)) * 2;
     d[0] = ej.x; d[1] = om.x; d[2] = ej.y; d[3] = om.y; d[4] = ej.z; d[5] = om.z;
     float *f = e.dof_force + env * PHC_NUM_DOF + 3 * (b - 1);
     f[0] = applied.x; f[1] = applied.y; f[2] = applied.z;
   }
+  launch_clock_end(c.clk);
 }
 
 }  // namespace phc
@@ -805,11 +807,10 @@ static int physics_launch(const phc_env_buffers *env, const float *pd_target, co
   const PhysView v = {env->num_envs, env->rigid_body_state, env->root_state, env->dof_state,
                        const_cast<float *>(env->dof_force)};  // read-only for the env step, written here
   const int64_t blocks = (env->num_envs + kPhysEnvs - 1) / kPhysEnvs;
-  hipEvent_t ev0, ev1;
-  if (phc_timer_take(timer, &ev0, &ev1)) timer->work += (double)env->num_envs;  // env-steps
+  c.clk = phc_timer_take(timer, as_stream(stream), blocks, (double)env->num_envs);  // work: env-steps
   const PdArgs pa{pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
                   pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr, pd ? pd->clip : 1};
-  phc_launch(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), ev0, ev1, v,
+  phc_launch(k_physics_step, dim3((unsigned)blocks), dim3(kPhysBlock), 0, as_stream(stream), v,
                         body_model, pd_target, pa, c);
   return check_launch("physics_step");
 }

@@ -17,6 +17,11 @@
 #ifndef PHC_ENV_ABLATE
 #define PHC_ENV_ABLATE 0
 #endif
+// k_env_step's minimum waves per SIMD (its register budget): 4 = at most 128 VGPRs, which with 40 KB of
+// LDS per 8-env workgroup keeps 4 workgroups (16 waves) per CU; 3 let the fused kernel take 129
+#ifndef PHC_ENV_WAVES
+#define PHC_ENV_WAVES 4
+#endif
 
 namespace phc {
 
@@ -34,6 +39,7 @@ struct StepConsts {
   float inv_nreset;   // 1 / number of reset bodies
   int reset_at_start;  // reset to motion time 0
   unsigned long long seed;
+  unsigned long long *clk;  // the launch's timer slot (phc_timer_take), null when untimed
 };
 
 static StepConsts make_consts(const phc_step_params *p) {
@@ -58,6 +64,7 @@ static StepConsts make_consts(const phc_step_params *p) {
   c.inv_nreset = n > 0 ? 1.0f / (float)n : 0.0f;
   c.reset_at_start = p->reset_at_start;
   c.seed = p->seed;
+  c.clk = nullptr;
   return c;
 }
 
@@ -599,7 +606,7 @@ __device__ __forceinline__ void operand_rows_out_wave(const EnvView &e, const fl
 }
 
 template <bool AUTO, bool REPLAY>
-__global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
+__global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
   constexpr bool kStage = REPLAY && PHC_ENV_STAGE && PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0;
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
@@ -618,6 +625,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
   return;
 #endif
 
+  launch_clock_begin(c.clk);
   const double st_prev = stats_prefetch(e);
   // kStage: R13 for the wave's envs first (elementwise over their contiguous [nv, 69] action span,
   // independent of everything else: its loads join the first memory round)
@@ -693,6 +701,8 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
     const float *rw = wreg + (g & 1) * (4 * kRowF) + b * kRec;
     rows0 = {load_body(rw), load_body(rw + kRowF)};
     rows1 = {load_body(rw + 2 * kRowF), load_body(rw + 3 * kRowF)};
+    // the region is reused below (replayed records, obs rows) by other lanes of this wave
+    wave_lds_handoff();
   } else
 #endif
   {
@@ -781,7 +791,8 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
 #if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
   if constexpr (kStage) {
     // the wave writes out its envs' rows (LDS operations of one wave complete in order: the lanes'
-    // row writes above are visible to the copy without a barrier)
+    // row writes above are visible to the copy once their issue order is pinned)
+    wave_lds_handoff();
     const int wl = threadIdx.x & 63;
     const int64_t env0 = (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6) * kWaveEnvs;
     const int64_t left = e.n - env0;
@@ -795,6 +806,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
       }
     }
     if (e.stats) flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
+    launch_clock_end(c.clk);
     return;
   }
   __syncthreads();  // the staged rows and the stats rows are complete
@@ -812,6 +824,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_env_step(EnvView e, LibView l, St
 #else
   if (e.stats) flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
 #endif
+  launch_clock_end(c.clk);
 }
 
 __global__ __launch_bounds__(kBlock) void k_physics_replay(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
@@ -888,38 +901,54 @@ extern "C" int phc_motion_state(const phc_motion_lib *lib, const int64_t *ids, c
   return check_launch("motion_state");
 }
 
-// Kernel timer (struct in phc_common.h): start/stop events recorded by the dispatch itself
-// (hipExtLaunchKernel), so the measured span is the kernel's own execution, as rocprofv3 reports it.
+// Kernel timer (struct and kernel side in phc_common.h): every timed launch stamps its own start and
+// end into its slot of the timer's device buffer.
 
 extern "C" phc_kernel_timer *phc_timer_create(int32_t capacity) {
   if (capacity <= 0) return nullptr;
   auto *t = new phc_kernel_timer;
-  t->start.resize(capacity);
-  t->stop.resize(capacity);
-  for (int32_t i = 0; i < capacity; ++i) {
-    if (hipEventCreate(&t->start[i]) != hipSuccess || hipEventCreate(&t->stop[i]) != hipSuccess) {
-      set_error("timer: hipEventCreate failed");
-      return nullptr;  // events created so far are leaked on this error path only
-    }
+  t->capacity = capacity;
+  // 2 x grid words per slot: room for every slot at up to 1,024 workgroups (the rollout's largest grid)
+  t->cap_words = (int64_t)capacity * 2048;
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+      khz <= 0 || hipMalloc(&t->dev, (size_t)t->cap_words * 8) != hipSuccess ||
+      hipMemset(t->dev, 0, (size_t)t->cap_words * 8) != hipSuccess) {
+    set_error("timer: device buffer / clock rate unavailable");
+    if (t->dev) (void)hipFree(t->dev);
+    delete t;
+    return nullptr;
   }
+  t->tick_hz = 1000.0 * (double)khz;
   return t;
 }
 
 extern "C" void phc_timer_destroy(phc_kernel_timer *t) {
   if (!t) return;
-  for (size_t i = 0; i < t->start.size(); ++i) {
-    (void)hipEventDestroy(t->start[i]);
-    (void)hipEventDestroy(t->stop[i]);
-  }
+  (void)hipDeviceSynchronize();  // no launch may still stamp into the buffer
+  (void)hipFree(t->dev);
   delete t;
 }
 
+// host copy of the slot words (after every launch issued so far has finished)
+static bool timer_words(phc_kernel_timer *t, std::vector<unsigned long long> &w) {
+  w.assign((size_t)t->used_words, 0ull);
+  if (t->used_words == 0) return true;
+  return hipDeviceSynchronize() == hipSuccess &&
+         hipMemcpy(w.data(), t->dev, (size_t)t->used_words * 8, hipMemcpyDeviceToHost) == hipSuccess;
+}
+
 extern "C" void phc_timer_reset(phc_kernel_timer *t) {
-  if (t) {
-    t->used = 0;
-    t->work = 0.0;
-    t->seen = 0;
+  if (!t) return;
+  std::vector<unsigned long long> w;
+  const bool ok = timer_words(t, w);
+  for (auto &s : t->slots) {
+    unsigned long long end = 0ull;  // the slot's latest workgroup end so far
+    for (int32_t g = 0; ok && s.graph && g < s.grid; ++g) end = w[(size_t)(s.off + s.grid + g)] > end ? w[(size_t)(s.off + s.grid + g)] : end;
+    s.end_at_reset = ok && s.graph ? end : ~0ull;
   }
+  t->base = t->slots.size();
+  t->seen = 0;
 }
 
 extern "C" void phc_timer_set_period(phc_kernel_timer *t, int32_t period) {
@@ -928,20 +957,58 @@ extern "C" void phc_timer_set_period(phc_kernel_timer *t, int32_t period) {
 
 extern "C" int64_t phc_timer_offered(const phc_kernel_timer *t) { return t ? t->seen : 0; }
 
-extern "C" double phc_timer_work(const phc_kernel_timer *t) { return t ? t->work : 0.0; }
+// the slots that count since the last reset: the eager ones taken after it, and the graph slots
+// re-stamped by a replay after it; -> (launches, work, summed ms)
+static bool timer_collect(phc_kernel_timer *t, int32_t *count, double *work, double *ms, double *each = nullptr,
+                          int32_t cap = 0) {
+  *count = 0;
+  *work = *ms = 0.0;
+  std::vector<unsigned long long> w;
+  if (!timer_words(t, w)) return false;
+  for (size_t i = 0; i < t->slots.size(); ++i) {
+    const auto &s = t->slots[i];
+    unsigned long long start = ~0ull, end = 0ull;
+    bool all = true;
+    for (int32_t g = 0; g < s.grid; ++g) {
+      const unsigned long long v0 = w[(size_t)(s.off + g)], v1 = w[(size_t)(s.off + s.grid + g)];
+      all = all && v0 != 0ull && v1 != 0ull;
+      start = v0 < start ? v0 : start;
+      end = v1 > end ? v1 : end;
+    }
+    if (!all || (i < t->base && !(s.graph && end != s.end_at_reset))) continue;
+    if (!all || end < start) continue;
+    const double d = (double)(end - start) / t->tick_hz * 1.0e3;
+    if (each && *count < cap) each[*count] = d;
+    *count += 1;
+    *work += s.work;
+    *ms += d;
+  }
+  return true;
+}
 
-extern "C" int32_t phc_timer_count(const phc_kernel_timer *t) { return t ? t->used : 0; }
+// per-launch ms of the counted launches, in the order they were taken (diagnostics); returns the count
+extern "C" int32_t phc_timer_durations(phc_kernel_timer *t, double *out, int32_t cap) {
+  int32_t c;
+  double w, ms;
+  return t && timer_collect(t, &c, &w, &ms, out, cap) ? c : -1;
+}
+
+extern "C" double phc_timer_work(phc_kernel_timer *t) {
+  int32_t c;
+  double w, ms;
+  return t && timer_collect(t, &c, &w, &ms) ? w : 0.0;
+}
+
+extern "C" int32_t phc_timer_count(phc_kernel_timer *t) {
+  int32_t c;
+  double w, ms;
+  return t && timer_collect(t, &c, &w, &ms) ? c : 0;
+}
 
 extern "C" double phc_timer_total_ms(phc_kernel_timer *t) {
-  if (!t) return -1.0;
-  double total = 0.0;
-  for (int32_t i = 0; i < t->used; ++i) {
-    if (hipEventSynchronize(t->stop[i]) != hipSuccess) return -1.0;
-    float ms = 0.0f;
-    if (hipEventElapsedTime(&ms, t->start[i], t->stop[i]) != hipSuccess) return -1.0;
-    total += ms;
-  }
-  return total;
+  int32_t c;
+  double w, ms;
+  return t && timer_collect(t, &c, &w, &ms) ? ms : -1.0;
 }
 
 extern "C" int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_lib *lib, const phc_step_params *p,
@@ -949,20 +1016,19 @@ extern "C" int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_l
   if (int rc = check_env(env)) return rc;
   if (int rc = check_lib(lib)) return rc;
   PHC_REQUIRE(p && p->dt > 0.0f, "env_step: bad params");
-  hipEvent_t ev0, ev1;
-  phc_timer_take(timer, &ev0, &ev1);
   const dim3 block(kBlock), grid(grid_envs(env->num_envs));
   hipStream_t st = as_stream(stream);
   const EnvView ev = env_view(env);
   const LibView lv = lib_view(lib);
-  const StepConsts cs = make_consts(p);
+  StepConsts cs = make_consts(p);
+  cs.clk = phc_timer_take(timer, st, grid.x, (double)env->num_envs);  // work: env-steps
   const ReplayArgs none{};
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot && lib->dof_vel, "env_step: auto_reset needs local_rot and dof_vel");
     PHC_REQUIRE(env->rng_counter, "env_step: auto_reset needs rng_counter");
-    phc_launch(k_env_step<true, false>, grid, block, 0, st, ev0, ev1, ev, lv, cs, none);
+    phc_launch(k_env_step<true, false>, grid, block, 0, st, ev, lv, cs, none);
   } else {
-    phc_launch(k_env_step<false, false>, grid, block, 0, st, ev0, ev1, ev, lv, cs, none);
+    phc_launch(k_env_step<false, false>, grid, block, 0, st, ev, lv, cs, none);
   }
   return check_launch("env_step");
 }
@@ -975,8 +1041,6 @@ extern "C" int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_
   PHC_REQUIRE(p && p->dt > 0.0f && rp, "env_step_replay: bad params");
   PHC_REQUIRE(lib->dof_vel, "env_step_replay: motion lib needs dof_vel");
   PHC_REQUIRE(!pd || (pd->actions && pd->pd_target && pd->offset && pd->scale), "env_step_replay: bad pd map");
-  hipEvent_t ev0, ev1;
-  phc_timer_take(timer, &ev0, &ev1);
   ReplayArgs ra{rp->pos_sigma, rp->force_scale, (unsigned long long)rp->seed, (unsigned long long)rp->counter,
                 pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
                 pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr, pd ? pd->clip : 1};
@@ -984,13 +1048,14 @@ extern "C" int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_
   hipStream_t st = as_stream(stream);
   const EnvView ev = env_view(env);
   const LibView lv = lib_view(lib);
-  const StepConsts cs = make_consts(p);
+  StepConsts cs = make_consts(p);
+  cs.clk = phc_timer_take(timer, st, grid.x, (double)env->num_envs);  // work: env-steps
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot, "env_step_replay: auto_reset needs local_rot");
     PHC_REQUIRE(env->rng_counter, "env_step_replay: auto_reset needs rng_counter");
-    phc_launch(k_env_step<true, true>, grid, block, 0, st, ev0, ev1, ev, lv, cs, ra);
+    phc_launch(k_env_step<true, true>, grid, block, 0, st, ev, lv, cs, ra);
   } else {
-    phc_launch(k_env_step<false, true>, grid, block, 0, st, ev0, ev1, ev, lv, cs, ra);
+    phc_launch(k_env_step<false, true>, grid, block, 0, st, ev, lv, cs, ra);
   }
   return check_launch("env_step_replay");
 }

@@ -120,8 +120,8 @@ __global__ __launch_bounds__(256) void k_copy_rows(RowFields fs, const uint8_t *
 // control words (mask flag, rank, take, start) and IT data words per thread — is issued in one
 // memory round at clamped addresses before the first store: a per-field copy loop put one
 // load -> store round trip per field (and per 256-word chunk) on the block's critical path.
-// Flag bytes are read through their aligned word (at most 3 bytes past a flag array's end:
-// inside the allocation's 512-B rounding for every torch tensor).
+// Flag bytes are read through their aligned word, only for fields whose caller vouches that those
+// words lie inside the allocation (PHC_ROW_SRC_WORDS); other flag fields take k_copy_rows.
 typedef const __attribute__((address_space(1))) uint8_t cu8;
 typedef const __attribute__((address_space(1))) uint32_t cu32;
 __device__ const uint32_t kOneWord = 1u;  // stands in for a null mask (every row valid)
@@ -220,7 +220,8 @@ extern "C" int phc_compact_rows(const phc_row_field *fields, int32_t num_fields,
     // word loads: 4-byte aligned sources (flag bytes are read through their aligned word)
     if (f.kind != PHC_ROW_U8_TO_F32 && ((reinterpret_cast<uintptr_t>(f.src) | reinterpret_cast<uintptr_t>(f.dst)) & 3))
       flat = false;
-    if (f.kind == PHC_ROW_U8_TO_F32 && (reinterpret_cast<uintptr_t>(f.dst) & 3)) flat = false;
+    if (f.kind == PHC_ROW_U8_TO_F32 && ((reinterpret_cast<uintptr_t>(f.dst) & 3) || !(f.flags & PHC_ROW_SRC_WORDS)))
+      flat = false;
     ff.woff[k] = (int32_t)words;
     words += w;
   }

@@ -50,6 +50,9 @@ def init_from_env(backend=None, force=False):
     return rank(), world_size()
 
 
+PARAM_ALIGN = 16  # elements: each parameter's slice of the flat buffers starts 64-B aligned
+
+
 class FlatGrads:
     """Parameters' gradients as views into one flat buffer, all-reduced (averaged) in buckets.
 
@@ -70,16 +73,21 @@ class FlatGrads:
             ids = {id(p) for p in first}
             params = first + [p for p in params if id(p) not in ids]
         self.params = params
-        n = sum(p.numel() for p in self.params)
-        dev = self.params[0].device
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-        self._range = {}
-        off = 0
+        # every parameter starts on a 64-B boundary (PARAM_ALIGN elements): the optimizer's per-tile
+        # passes (phc_opt_step_operands) then read whole aligned float4s of any parameter; the gaps
+        # stay zero (no gradient, no parameter, Adam keeps them at zero)
+        offs, off = [], 0
         for p in self.params:
+            off = -(-off // PARAM_ALIGN) * PARAM_ALIGN
+            offs.append(off)
+            off += p.numel()
+        dev = self.params[0].device
+        self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        self._range = {}
+        for p, o in zip(self.params, offs):
             k = p.numel()
-            p.grad = self.flat[off:off + k].view_as(p)
-            self._range[id(p)] = (off, off + k)
-            off += k
+            p.grad = self.flat[o:o + k].view_as(p)
+            self._range[id(p)] = (o, o + k)
         self.bucket = max(1, bucket_bytes // 4)
         self._works = None
         self._done = None
@@ -103,7 +111,7 @@ class FlatGrads:
             self._done.add(id(p))
         s0 = e0 = None
         for s, e in spans + [(None, None)]:
-            if s is not None and e0 == s:
+            if s is not None and e0 is not None and 0 <= s - e0 < PARAM_ALIGN:  # adjacent (alignment gap)
                 e0 = e
                 continue
             if s0 is not None:

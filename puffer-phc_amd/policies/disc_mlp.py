@@ -25,6 +25,7 @@ import torch
 
 from .. import _native as N
 from .twin_mlp import _compute_dtype, _pad64, _wgrad_splits, _wgrad_tiles
+from . import weight_cache
 from .weight_cache import cache_key, layout_key
 
 
@@ -70,9 +71,12 @@ def disc_operands(pol, dtype):
             ops.w2t = torch.empty((l2.weight.shape[1], l2.weight.shape[0]), dtype=dtype, device=dev)
         lk = layout_key(dtype, ps)
         if fresh or ops.plan_key != lk:
-            ops.plan = N.PackPlan([(l1.weight.detach(), ops.w1[:, :k1], None),
-                                   (l2.weight.detach(), ops.w2, ops.w2t)])
+            ops.plan_jobs = [(l1.weight.detach(), ops.w1[:, :k1], None), (l2.weight.detach(), ops.w2, ops.w2t)]
+            ops.plan = N.PackPlan(ops.plan_jobs)
             ops.plan_key = lk
+            # key of the copies: the two weights (the biases are read in place)
+            ops.fresh_dtype, ops.fresh_params = dtype, ps
+            weight_cache.register_plan(ops)
         ops.plan.run()
         ops.b1 = l1.bias.detach().float().contiguous()
         ops.b2 = l2.bias.detach().float().contiguous()

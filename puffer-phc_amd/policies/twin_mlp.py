@@ -28,6 +28,7 @@ import os
 import torch
 
 from .. import _native as N
+from . import weight_cache
 from .weight_cache import cache_key, layout_key
 
 
@@ -221,7 +222,10 @@ def mfma_operands(weights, dtype):
                      for a, _ in weights.pairs]
         lk = layout_key(dtype, ps)
         if fresh or ops.plan_key != lk:
-            ops.plan, ops.plan_key = N.PackPlan(_pack_jobs(weights, ops)), lk
+            ops.plan_jobs = _pack_jobs(weights, ops)
+            ops.plan, ops.plan_key = N.PackPlan(ops.plan_jobs), lk
+            ops.fresh_dtype, ops.fresh_params = dtype, ps
+            weight_cache.register_plan(ops)  # FlatAdam's step may write these copies itself
         ops.plan.run()
     ops.key = key
     return ops

@@ -178,3 +178,40 @@ def test_rollout_graph_sees_optimizer_updates():
     # weight loads coalesce across the actions)
     assert inner._w_mu_aligned.data_ptr() % 16 == 0 and inner._w_mu_aligned.stride(0) % 4 == 0
     assert torch.equal(inner._w_mu_aligned, inner.mu[0].weight.detach().t())
+
+
+def test_step_writes_operand_copies_bit_exact(monkeypatch):
+    """FlatAdam's step writes the registered operand copies itself (phc_opt_step_operands): the
+    caches stay current with no refresh launch, every copy equals param.to(dtype), and the
+    parameters / moments are bit-identical to the plain step followed by the caches' own refresh
+    (PHC_OPERANDS_IN_STEP=0)."""
+    from puffer_phc_amd import optim
+    from puffer_phc_amd.distributed import FlatGrads
+    from puffer_phc_amd.optim import FlatAdam
+    from puffer_phc_amd.policies import PHCPolicy, Policy, disc_mlp, twin_mlp, weight_cache
+
+    runs = []
+    for in_step in (True, False):
+        monkeypatch.setattr(optim, "OPERANDS_IN_STEP", in_step)
+        torch.manual_seed(0)
+        pol = Policy(PHCPolicy(_Env())).to(DEV)
+        inner = pol.policy
+        fg = FlatGrads(pol.parameters(), order=inner.grad_ready_order())
+        opt = FlatAdam(fg, lr=1e-2, use_loss_scale=True)
+        ops = twin_mlp.mfma_operands(inner._twin, torch.float16)
+        dops = disc_mlp.disc_operands(inner, torch.float16)
+        g = torch.Generator(device=DEV).manual_seed(1)
+        for _ in range(3):
+            fg.flat.copy_(torch.randn(fg.flat.shape, device=DEV, generator=g) * 1e3)
+            opt.fused_step(10.0)
+            if in_step:
+                assert weight_cache.is_fresh(ops) and weight_cache.is_fresh(dops)
+                assert opt._ops is not None and len(opt._ops_owners) == 2
+            else:
+                assert not weight_cache.is_fresh(ops)
+            _check_trunk_operands(inner, torch.float16)
+            _check_disc_operands(inner, torch.float16)
+        torch.cuda.synchronize()
+        runs.append((opt.param_flat.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt._state.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
