@@ -192,8 +192,12 @@ def _host_cpu():
 
 
 def _host_workers():
-    """Worker processes for the all-cores leg: the CPUs this process may run on, capped at 16
-    (a GPU box's CPU share for one GPU; OMP_NUM_THREADS is set to it there)."""
+    """Worker processes for the all-cores leg: the CPUs this process may run on, capped at the GPU's
+    share of its host.  The measurement boxes lease one GPU of an 8-GPU host together with 16 of the
+    host's CPUs (OMP_NUM_THREADS / MAX_JOBS are set to 16 there), while os.sched_getaffinity and
+    nproc report every CPU of the machine, so the affinity set alone would time cores that belong
+    to the other seven GPUs' jobs.  16 is therefore the fair all-cores figure per GPU; on a host
+    whose affinity set is smaller, that set is used."""
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
     return max(1, min(avail, cap, 16))
@@ -294,6 +298,8 @@ def cpu_baseline(env, packed, seconds):
             "comparison": "env step only (motion state x2 + reward + reset + obs); no policy inference or PPO "
                           "update, which the headline value includes",
             "value_1_thread": one, "value_all_cores": allc, "cores_all": workers,
+            "cores_note": "all-cores leg = min(affinity set, OMP_NUM_THREADS, 16): the one-GPU lease's CPU share "
+                          "(bench._host_workers)",
             "host_nproc": os.cpu_count(), "host_cpu_model": _host_cpu(),
             "gae_ms_131072_rows_1_thread": gae_ms,
             "sample": f"{n} envs: {steps1} oracle env steps at 1 thread ({dt1:.1f}s); {steps_all} steps over "
@@ -426,6 +432,47 @@ class Runner:
         return {k: v / n for k, v in tot.items()}
 
 
+def dispatch_overhead_us(env, n=8):
+    """Per-launch dispatch + completion time of the env step that its in-kernel stamps do not see: HIP
+    events around n eager launches minus their stamped spans (after the timed region)."""
+    from puffer_phc_amd._native import KernelTimer
+
+    t = KernelTimer(capacity=2 * n)
+    prev, env.env.kernel_timer = env.env.kernel_timer, t
+    act = torch.zeros((env.num_agents, 69), device=env.actions.device)
+    evs = []
+    try:
+        for _ in range(n):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            env.step(act)
+            e1.record()
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        stamped = t.total_ms() / max(t.count, 1)
+        evented = sum(a.elapsed_time(b) for a, b in evs) / n
+    finally:
+        env.env.kernel_timer = prev
+    return max(0.0, (evented - stamped) * 1e3)
+
+
+DP_FIELDS = ("mode", "backend", "allreduce_exposed_ms_per_minibatch_rank0",
+             "allreduce_exposed_ms_per_minibatch_max_rank", "minibatches_timed", "grad_bytes_per_minibatch", "note")
+
+
+def dp_summary(mode, exp_ms, n_bw, grad_bytes, device):
+    """config.dp at N > 1 (collective: every rank calls it): the exposed all-reduce wait per minibatch
+    backward on this rank (rank 0's goes in the line) and on the slowest rank."""
+    e = torch.tensor([exp_ms or 0.0], dtype=torch.float64, device=device)
+    torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
+    return {"mode": mode, "backend": torch.distributed.get_backend(),
+            "allreduce_exposed_ms_per_minibatch_rank0": exp_ms,
+            "allreduce_exposed_ms_per_minibatch_max_rank": float(e[0]), "minibatches_timed": n_bw,
+            "grad_bytes_per_minibatch": grad_bytes,
+            "note": "CUDA events on rank's compute stream around the wait for the backward's all-reduces "
+                    "(FlatGrads.overlap_finish): the stall after the last backward kernel"}
+
+
 def launch_ranks(n):
     """`--gpus N` without a torch.distributed launcher around this process: start N ranks (one per
     GPU) under torch.distributed.run as CHILD processes and return their exit code.  This parent
@@ -488,6 +535,9 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     runner.mark()
+    from puffer_phc_amd import _native as _N
+
+    gemm_launch0, tick0 = _N.GEMM_LAUNCHES[0], env.tick
     t0 = time.perf_counter()
     processed = 0
     for _ in range(args.steps):
@@ -498,10 +548,14 @@ def main():
     elapsed = time.perf_counter() - t0
     skipped = runner.skipped()
     skipped = None if skipped is None else skipped - runner._skip0
-    env_steps = timer.count  # sampled phc_env_step launches of the timed region, timed by their dispatch events
-    env_offered, gemm_offered = timer.offered, gtimer.offered
+    env_steps = timer.count  # sampled env-step launches of the timed region, stamped by the kernel itself
+    # launches the timed region ran (captured graphs replay launches the host does not offer again)
+    env_offered, gemm_offered = env.tick - tick0, _N.GEMM_LAUNCHES[0] - gemm_launch0
     kern_s = timer.total_ms() / max(env_steps, 1) * 1e-3
     env.env.kernel_timer = None
+    # the stamps span first workgroup start -> last workgroup end; HIP events / rocprofv3 also count the
+    # dispatch and completion of the launch: measured here on a few eager steps after the timed region
+    env_dispatch_us = dispatch_overhead_us(env)
     gemm_set_timer(None)
     gemm_launches, gemm_flops = gtimer.count, gtimer.work
     gemm_s = gtimer.total_ms() * 1e-3 if gemm_launches else 0.0
@@ -522,17 +576,9 @@ def main():
     processed_all = whole_job_steps(counts, args.mode == "ppo", world)
     dp = None
     if flat is not None and world > 1:
-        # the exposed all-reduce wait per minibatch backward: rank 0's and the slowest rank's
         exp_ms, n_bw = flat.exposed_ms()
         flat.timing = False
-        e = torch.tensor([exp_ms or 0.0], dtype=torch.float64, device=device)
-        torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
-        dp = {"mode": args.dp_mode, "backend": torch.distributed.get_backend(),
-              "allreduce_exposed_ms_per_minibatch_rank0": exp_ms,
-              "allreduce_exposed_ms_per_minibatch_max_rank": float(e[0]), "minibatches_timed": n_bw,
-              "grad_bytes_per_minibatch": flat.flat.numel() * 4,
-              "note": "CUDA events on rank's compute stream around the wait for the backward's all-reduces "
-                      "(FlatGrads.overlap_finish): the stall after the last backward kernel"}
+        dp = dp_summary(args.dp_mode, exp_ms, n_bw, flat.flat.numel() * 4, device)
 
     if rank == 0:
         fused = bool(getattr(env.env, "fused_env_step", False)) and args.physics == "replay"
@@ -542,7 +588,9 @@ def main():
         opnd = getattr(env.env, "_obs_operand", None)
         opnd_bytes = int(opnd[0].shape[1] * opnd[0].element_size()) if opnd is not None else 0
         env_bytes += opnd_bytes
-        achieved = env_bytes * args.envs / kern_s / 1e9
+        # the launch's duration as HIP events / rocprofv3 count it: the stamped span + the dispatch overhead
+        env_launch_s = kern_s + (env_dispatch_us or 0.0) * 1e-6
+        achieved = env_bytes * args.envs / env_launch_s / 1e9
         traffic = None
         # HBM bytes of the env step from the committed PMC passes: the rollout-context launch (fused
         # operand written) has its own file (tools/r04_final.sh)
@@ -611,7 +659,8 @@ def main():
                               "env phase)" if fused else "phc_env_step",
                     "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "kernel_us": kern_s * 1e6, "launches_timed": env_steps, "launches_in_region": env_offered,
+                    "kernel_us": env_launch_s * 1e6, "kernel_us_stamped": kern_s * 1e6,
+                    "dispatch_us": env_dispatch_us, "launches_timed": env_steps, "launches_in_region": env_offered,
                     "algorithmic_bytes_per_env_step": env_bytes, "obs_operand_bytes_per_env_step": opnd_bytes}
         if gemm_launches:
             # the dominant kernel of the PPO / rollout modes: the trunk GEMMs (MFMA-bound)

@@ -500,7 +500,8 @@ int phc_compact_rows(const phc_row_field *fields, int32_t num_fields, const uint
  * bias corrections.  state lives in device memory (a captured graph can replay the call);
  * norm_out (device, nullable) = [sum of per-parameter norms, total norm, l2]; with param_init
  * (the flat initial parameters, nullable) l2 = sum over parameters of mean((p - p0)^2) before
- * this step's update (the L2-init regulariser the reference logs, core.py:352-359). */
+ * this step's update (the L2-init regulariser the reference logs, core.py:352-359); norm_acc (device
+ * float64 [3], nullable, needs norm_out) += norm_out (a trainer's running sums, no extra launch). */
 typedef struct phc_adam_params {
   float lr, beta1, beta2, eps;
   float max_norm;
@@ -524,7 +525,7 @@ int64_t phc_opt_block_elems(void);
 size_t phc_opt_workspace_bytes(int32_t nblk);
 int phc_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const int64_t *blk_range,
                  int32_t nblk, const int32_t *seg_blk, int32_t nseg, const phc_adam_params *hp, phc_opt_state *state,
-                 float *norm_out, const float *param_init, void *workspace, void *stream);
+                 float *norm_out, const float *param_init, void *workspace, double *norm_acc, void *stream);
 /* The same step with the GEMM-operand copies of the parameters written by the Adam pass itself
  * (what phc_pack_weights would write right after it, from the same fp32 values: f16 / bf16 / fp32
  * copies, row-wise into dst and transposed into dst_t), so no separate operand refresh re-reads the
@@ -547,7 +548,8 @@ int64_t phc_adam_job_blocks(int32_t kind, int64_t rows, int64_t cols);
 int phc_opt_step_operands(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                           const int64_t *blk_range, int32_t nblk, const int32_t *seg_blk, int32_t nseg,
                           const phc_adam_params *hp, phc_opt_state *state, float *norm_out, const float *param_init,
-                          void *workspace, const phc_adam_job *jobs, int32_t njobs, int64_t nblocks, void *stream);
+                          void *workspace, double *norm_acc, const phc_adam_job *jobs, int32_t njobs, int64_t nblocks,
+                          void *stream);
 
 /* R21 gradient plumbing: for each job, dst[r, c] (+= when accumulate) = sum over s < parts of
  * src[s * part_stride + r * src_ld + c] (parts summed in order; dst dense [rows, cols]).  Writes
@@ -585,6 +587,7 @@ int phc_pack_weights(const phc_pack_job *jobs, int32_t num_jobs, void *stream);
  * loss = pg - ent_coef*ent + vf_coef*v + bound_coef*bound, stats[1..7] = pg, v, ent,
  * old_approx_kl, approx_kl, clipfrac, bound (means); row_coef [m,2] saved for the backward;
  * adv_mean_std = {mean, std} of the advantages (device, from the global statistics).
+ * stats_acc (device float64 [7], nullable) += stats[1..7] (a trainer's running sums, no extra launch).
  * Backward: d loss / d mu [m,a] and d loss / d value [m] scaled by grad_loss[0] (device). */
 #define PHC_PPO_STATS 7
 typedef struct phc_ppo_coefs {
@@ -596,7 +599,7 @@ size_t phc_ppo_workspace_bytes(int64_t m);
 int phc_ppo_loss_fwd(const float *mu, const float *log_sigma, const float *actions, const float *old_logprob,
                      const float *adv, const float *adv_mean_std, const float *value, const float *old_value,
                      const float *returns, int64_t m, int32_t a, const phc_ppo_coefs *coefs, float *row_coef,
-                     float *stats, void *workspace, void *stream);
+                     float *stats, double *stats_acc, void *workspace, void *stream);
 int phc_ppo_loss_bwd(const float *mu, const float *log_sigma, const float *actions, const float *row_coef,
                      const float *grad_loss, int64_t m, int32_t a, const phc_ppo_coefs *coefs, float *grad_mu,
                      float *grad_value, void *stream);

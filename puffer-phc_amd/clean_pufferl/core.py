@@ -158,6 +158,8 @@ class RolloutStep:
             pairs.append((env.amp_obs, exp.amp_obs))
         self.store = _native.RowCompactor(pairs, n, exp.batch_size, dev)
         self.graph = None
+        self._blocks = {}  # captured multi-step blocks by length (run_block)
+        self._blocks_key = None  # the env's launch_key() the blocks were captured under
         self.eager_steps = 0
         self._noise_ready = False
         pol = self.policy.policy if hasattr(self.policy, "policy") else self.policy
@@ -191,7 +193,7 @@ class RolloutStep:
             _native.obs_half(self.env.observations, nm.running_mean, nm.running_var, nm.epsilon, nm.clip, self.opnd)
             self.opnd_first = False
 
-    def _body(self):
+    def _body(self, noise=None):
         pol = self.policy.policy if hasattr(self.policy, "policy") else self.policy
         with torch.no_grad(), autocast(self.cfg):
             fused = False
@@ -199,8 +201,8 @@ class RolloutStep:
                 # sample_logits' Normal draw (self.noise, drawn eagerly by run() before every step:
                 # an RNG op inside the captured graph would add the generator's seed / offset
                 # updates to every replay), then the fused policy tail writes the staging buffers
-                fused = pol.act_rollout(self.env.observations, self.noise, self.actions, self.logprob, self.value,
-                                        mu=self.mu, obs_half=self.opnd)
+                fused = pol.act_rollout(self.env.observations, self.noise if noise is None else noise, self.actions,
+                                        self.logprob, self.value, mu=self.mu, obs_half=self.opnd)
             if not fused:
                 actions, logprob, _, value = self.policy(self.env.observations)
                 self.value.copy_(value.flatten())
@@ -208,6 +210,45 @@ class RolloutStep:
                 self.logprob.copy_(logprob)
             self.fused = fused
         self.store(self.env.masks)
+
+    def block_ok(self):
+        """Whether whole blocks of steps (policy, store, env step) can replay from one graph."""
+        return (BLOCK_GRAPH and self.fused_act and getattr(self.env, "block_steppable", False)
+                and hasattr(self.env, "block_step"))
+
+    def run_block(self, steps):
+        """`steps` rollout steps from ONE captured graph (captured on first use of this length, after
+        the single-step graph exists): per step the policy (its Normal draw from noise row k, all rows
+        drawn by one launch before the replay), the experience store and the env step (the fused
+        replay launch with its logging rows in row k: PHCPufferEnv.finish_block does the host's
+        logging for the block).  Returns the block's infos."""
+        if self.twin is not None:
+            refresh_twin(self.twin, _compute_dtype(self.cfg))
+        if self.opnd is not None:
+            self._refresh_operand()
+        shape = (steps,) + tuple(self.noise.shape)
+        if getattr(self, "_noise_block", None) is None or self._noise_block.shape[0] < steps:
+            self._noise_block = torch.zeros(shape, device=self.noise.device)
+        noise = self._noise_block[:steps]
+        noise.normal_()
+        self.env.block_stats(steps)
+        # the captured step launches hold the env / library / step-parameter structs by value: a
+        # resample_motions() (a new packed library) or an eval toggle invalidates every block
+        key = self.env.env.launch_key()
+        if key != self._blocks_key:
+            self._blocks.clear()
+            self._blocks_key = key
+        g = self._blocks.get(steps)
+        if g is None:
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for k in range(steps):
+                    self._body(noise=noise[k])
+                    self.env.block_step(self.actions, k)
+            self._blocks[steps] = g
+        g.replay()
+        return self.env.finish_block(steps)
 
     def run(self, use_graph=True):
         if self.twin is not None:
@@ -288,7 +329,22 @@ def _evaluate_graph(components, info):
         min_steps = max(1, -(-(experience.batch_size - start) // n))
         steps = 0
         step_infos = []  # read after the loop: a mean_and_log info resolves by waiting for its copy
-        while True:
+        done = False
+        if train_cfg.rollout_graph and rs.graph is not None and rs.block_ok() and min_steps >= 2:
+            # the steps that cannot fill the buffer need no host read: one replayed block of them
+            # (the single-step graph exists, so every lazy initialisation has happened)
+            with profile.env:
+                _, _, _, _, env_info, _, _ = vecenv.recv()  # the previous send's info
+            step_infos.extend(env_info)
+            with profile.eval_forward:
+                step_infos.extend(rs.run_block(min_steps))
+            vecenv._pending = (vecenv.observations, vecenv.rewards, vecenv.terminals, vecenv.truncations, [],
+                               vecenv.env_ids, vecenv.masks)
+            steps = min_steps
+            with profile.eval_misc:
+                cursor, n_valid, taken = rs.store.state()
+                done = cursor >= experience.batch_size
+        while not done:
             with profile.env:
                 _, _, _, _, env_info, _, _ = vecenv.recv()
             step_infos.extend(env_info)
@@ -306,6 +362,9 @@ def _evaluate_graph(components, info):
             for i in step_infos:
                 for k, v in i.items():
                     env_infos[k].append(v)
+            flush = getattr(vecenv, "flush", None)
+            if flush is not None:  # infos a caller never reads still count their episodes now
+                flush()
             # data parallel: every rank advances the same whole-job step count (its own mask-true
             # rows differ with the envs' truncation patterns), so loop exits agree across ranks
             info.global_step += _global_count(n_valid, rs.store.counts.device)
@@ -355,6 +414,9 @@ def evaluate(components, info):
                         env_infos[k].append(v)
             with profile.env:
                 components.vecenv.send(actions)
+        flush = getattr(components.vecenv, "flush", None)
+        if flush is not None:
+            flush()
         info.global_step += _global_count(local_steps, experience.obs.device)
         for k, v in env_infos.items():
             info.stats.extend(k, list(np.atleast_1d(v)))
@@ -461,6 +523,10 @@ _PINNED = _PinnedRing()
 ADV_GRAPH = os.environ.get("PHC_ADV_GRAPH", "1") != "0"
 # rollout: draw the next step's action noise right after the policy graph instead of before it
 NOISE_AHEAD = os.environ.get("PHC_NOISE_AHEAD", "0") != "0"
+# rollout: the steps that cannot fill the buffer (all but the last one or two) replay as ONE captured
+# block of policy + store + env-step launches (RolloutStep.run_block); PHC_BLOCK_GRAPH=0: one graph per
+# step with the env step eager
+BLOCK_GRAPH = os.environ.get("PHC_BLOCK_GRAPH", "1") != "0"
 
 
 _ADV_ATTRS = ("b_idxs_obs", "b_idxs", "b_idxs_flat", "b_obs_half", "b_obs", "b_actions", "b_logprobs", "b_dones",
@@ -586,15 +652,12 @@ def _fused_update(components, info, pol):
         for mb in range(exp.num_minibatches):
             obs = exp.b_obs_half[mb * mbs:(mb + 1) * mbs]
             atn = exp.b_actions[mb].reshape(-1, exp.b_actions.shape[-1])
-            with autocast(cfg):
+            with autocast(cfg):  # the logged sums accumulate inside the objective / optimizer launches
                 loss, st = fused_ppo_loss(pol, obs, atn, exp.b_logprobs[mb].reshape(-1), exp.b_advantages[mb],
                                           adv_ms[mb] if cfg.norm_adv else unit, exp.b_values[mb], exp.b_returns[mb],
-                                          coefs, store_grads=True)
+                                          coefs, store_grads=True, stats_acc=acc_ppo)
             opt.backward(loss)
-            opt.fused_step(cfg.max_grad_norm)
-            with torch.no_grad():
-                acc_ppo += st
-                acc_opt += opt.norms
+            opt.fused_step(cfg.max_grad_norm, norm_acc=acc_opt)
     with torch.no_grad():
         acc = torch.zeros(12, dtype=torch.float64, device=dev)
         i7, i67, i02 = _row_index(dev)
@@ -627,6 +690,7 @@ def _train_minibatches_graphed(components, info, pol):
     if st["graph"] is not None and st["key"] == key:
         fresh = opt.fresh_operand_owners() if st["writes_operands"] else []
         st["graph"].replay()
+        _native.GEMM_LAUNCHES[0] += st["gemm_launches"]
         # the replay rewrote the parameters behind every host-side cache key (FlatAdam.fused_step
         # bumps the generation when it runs on the host; a replay does not run it); the operand
         # caches its captured steps rewrote stay current
@@ -638,8 +702,10 @@ def _train_minibatches_graphed(components, info, pol):
     try:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        launches0 = _native.GEMM_LAUNCHES[0]
         with torch.cuda.graph(g):
             row = _fused_update(components, info, pol)
+        st["gemm_launches"] = _native.GEMM_LAUNCHES[0] - launches0
     except Exception:  # noqa: BLE001  (an op that cannot be captured: stay eager)
         st["failed"] = True
         torch.cuda.synchronize()
@@ -725,8 +791,10 @@ def train(components, info, utilization=None):
                         # number), so a store would overwrite their gradient
                         store_grads = (STORE_GRADS and not info.use_amp_obs and cfg.l2_reg_coef == 0
                                        and isinstance(components.optimizer, FlatAdam))
+                        in_kernel_acc = opt_l2 and not info.use_amp_obs
                         loss, st = fused_ppo_loss(pol, obs, atn, log_probs, adv, ms, val, ret, tail_coefs,
-                                                  store_grads=store_grads)
+                                                  store_grads=store_grads,
+                                                  stats_acc=acc_ppo if in_kernel_acc else None)
                     elif fused_obj:
                         mu, newvalue = pol.forward_train(obs)
                     else:
@@ -813,7 +881,9 @@ def train(components, info, utilization=None):
                         flat.overlap_begin()  # data parallel: per-layer all-reduces during the backward
                         opt.backward(loss)  # d(loss * S): S under fp16 loss scaling
                         flat.overlap_finish()
-                        gnorm = opt.fused_step(cfg.max_grad_norm)[0]  # unscale, clip, skip-on-inf, Adam
+                        # unscale, clip, skip-on-inf, Adam (the logged norms summed in the same launch)
+                        acc_in = fused_mb and opt_l2 and not info.use_amp_obs
+                        gnorm = opt.fused_step(cfg.max_grad_norm, norm_acc=acc_opt if acc_in else None)[0]
                     elif scaler is None:
                         loss.backward()
                         flat.allreduce_mean()
@@ -830,8 +900,9 @@ def train(components, info, utilization=None):
                         scaler.update()
                 with profile.train_misc, torch.no_grad():
                     if fused_obj and opt_l2 and not info.use_amp_obs:
-                        acc_ppo += st  # pg, v, ent, old_kl, kl, clipfrac, bound (ppo_loss.py)
-                        acc_opt += components.optimizer.norms  # norm sum, total norm, l2
+                        if not fused_mb:  # (the fused minibatch's launches summed these already)
+                            acc_ppo += st  # pg, v, ent, old_kl, kl, clipfrac, bound (ppo_loss.py)
+                            acc_opt += components.optimizer.norms  # norm sum, total norm, l2
                         continue
                     if l2 is None:
                         l2 = components.optimizer.norms[2]

@@ -128,12 +128,54 @@ class PHCPufferEnv:
             info = self.mean_and_log()
         return self.observations, rew, self.terminals, self.truncations, info
 
-    def mean_and_log(self):
-        """Host reduction of the per-block statistics (clean_pufferl/env.py:145-188).  The sums come
-        back by a non-blocking copy into pinned memory: the returned info resolves (waits for the
-        copy) when first read, so the rollout does not drain the stream every log_interval steps;
-        the trainer reads the step infos after its rollout loop."""
-        s = self.stats.sum(0)
+    # ----------------------------------------------- rollout blocks (captured graphs) --
+    @property
+    def block_steppable(self):
+        """Whether steps can be captured into a rollout block graph: the fused replay launch (no
+        per-step host value) with the env's in-launch auto-reset, no AMP history."""
+        e = self.env
+        return (e.fused_env_step and hasattr(e.physics, "step_fused") and not e.flag_im_eval
+                and not self.cfg.use_amp_obs)
+
+    def block_stats(self, steps):
+        """[steps, blocks, slots] float64 logging rows: step k of a block writes rows k."""
+        buf = getattr(self, "_block_stats", None)
+        if buf is None or buf.shape[0] < steps:
+            buf = self._block_stats = torch.zeros((steps,) + tuple(self.stats.shape), dtype=torch.float64,
+                                                  device=self.stats.device)
+            self._block_env_c = None
+        env_key = bytes(self.env._env_c)
+        if self._block_env_c is None or self._block_env_key != env_key:  # copies of the current env struct
+            self._block_env_c = [self.env.stats_env_struct(buf[k]) for k in range(buf.shape[0])]
+            self._block_env_key = env_key
+        return buf[:steps]
+
+    def block_step(self, actions, k):
+        """Step k of a captured block: step() without the host's tick / logging bookkeeping (done by
+        finish_block for the whole block), the logging rows going to block_stats row k."""
+        self.env.step(actions, auto_reset=True, env_c=self._block_env_c[k])
+
+    def finish_block(self, steps):
+        """After a replayed block of `steps` steps: advance the tick and emit the mean_and_log infos
+        of every log point inside the block, each over exactly the log_interval steps before it (the
+        rows of earlier eager steps in self.stats, then the block's rows up to the point); the rows
+        after the last point carry into self.stats.  Returns the infos (PendingInfo)."""
+        rows = self._block_stats[:steps]
+        L = self.cfg.log_interval
+        infos, a = [], 0
+        first = (L - self.tick % L) % L  # steps until the next log point (0: the block's first step)
+        for k in range(first if first > 0 else L, steps + 1, L):  # log after step index k - 1
+            s = self.stats.sum(0) + rows[a:k].sum((0, 1))
+            infos.append(self._pending_info(s))
+            self.stats.zero_()
+            a = k
+        if a < steps:
+            self.stats[0] += rows[a:steps].sum((0, 1))
+        rows.zero_()  # the next replay adds into zeroed rows
+        self.tick += steps
+        return infos
+
+    def _pending_info(self, s):
         slot = self._info_ring[self._info_i % len(self._info_ring)]
         self._info_i += 1
         if slot[1] is not None:
@@ -142,10 +184,27 @@ class PHCPufferEnv:
         host.copy_(s, non_blocking=True)
         done = torch.cuda.Event()
         done.record()
-        self.stats.zero_()
         info = PendingInfo(self, host, done)
         slot[1] = info
+        return info
+
+    def mean_and_log(self):
+        """Host reduction of the per-block statistics (clean_pufferl/env.py:145-188).  The sums come
+        back by a non-blocking copy into pinned memory: the returned info resolves (waits for the
+        copy) when first read, so the rollout does not drain the stream every log_interval steps;
+        the trainer reads the step infos after its rollout loop."""
+        info = self._pending_info(self.stats.sum(0))
+        self.stats.zero_()
         return [info]
+
+    def flush(self):
+        """Resolve every outstanding mean_and_log info (waits for their copies): afterwards
+        episode_count includes every log point emitted so far, as the reference's mean_and_log
+        counts at call time (clean_pufferl/env.py:145-188).  The trainer calls it after each
+        rollout loop, where it reads the infos anyway."""
+        for slot in self._info_ring:
+            if slot[1] is not None:
+                slot[1].resolve()
 
     def _resolve_info(self, s):
         n_ep = s[7]

@@ -155,8 +155,21 @@ __device__ __forceinline__ void lds_barrier() {
 // wave drains its own DMA (vmcnt), then the barrier.  __syncthreads() is NOT enough: its fence
 // does not count LDS-DMA, and the compiler's own vmcnt for the DMA may land after the barrier
 // (seen in the persistent tile loop: waves read operand tiles other waves' DMA had not written).
+#ifndef PHC_GEMM_WAIT_BUILTIN
+#define PHC_GEMM_WAIT_BUILTIN 1
+#endif
 __device__ __forceinline__ void dma_barrier() {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if constexpr (PHC_GEMM_WAIT_BUILTIN) {
+    // the wait as the compiler's own instruction (s_waitcnt with every counter 0): its wait-insertion
+    // pass then knows every earlier fragment read has completed and does not drain the reads issued
+    // after the barrier before the first MFMA that needs none of them (inline asm is opaque to it)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
 }
 
 template <typename OutT> __device__ __forceinline__ void gemm_store(void *p, int64_t off, float v) {
@@ -356,6 +369,82 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
       __builtin_amdgcn_s_setprio(0);
     }
   }
+}
+
+// ---- K-steps with the last MFMA group deferred across the barrier (PHC_GEMM_DEFER) -----------
+// gemm_step runs a K-step's MFMA groups 0 .. NG-1 after the workgroup barrier that publishes its
+// operand tile, so each K-step starts with every wave waiting for its first fragment reads (the
+// barrier lines the waves up: both waves of a SIMD stall together).  Here the last group's MFMAs of
+// K-step kt (fragments already in registers: fa[1], fb[1]) run after the barrier of K-step kt + 1,
+// behind that step's first fragment reads (fa[0], fb[0]: other registers), so the LDS latency after
+// the barrier hides behind 2 x NI MFMAs.  The operand buffer the deferred group came from may be
+// overwritten by the next DMA as soon as the barrier passes: its fragments were read (lgkmcnt 0)
+// before it.  gemm_flush runs the last deferred group after the final K-step.
+#ifndef PHC_GEMM_DEFER
+#define PHC_GEMM_DEFER 1
+#endif
+template <typename V8, int NI> struct GemmFrags {
+  V8 fa[2][2], fb[2][NI];
+};
+
+template <typename T, typename V8, int NI>
+__device__ __forceinline__ void mfma_group(const V8 (&a)[2], const V8 (&b)[NI], f4 *acc0, f4 *acc1) {
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    if constexpr (std::is_same<T, _Float16>::value) {
+      acc0[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[j], acc0[j], 0, 0, 0);
+      acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[j], acc1[j], 0, 0, 0);
+    } else {
+      acc0[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j], acc0[j], 0, 0, 0);
+      acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j], acc1[j], 0, 0, 0);
+    }
+  }
+}
+
+template <typename T, typename TL, typename Stage, typename V8>
+__device__ __forceinline__ void gemm_step_defer(const char *__restrict__ rd, char *__restrict__ wr, bool issue,
+                                                bool carry, const Stage &stage, int next, int wave, int lane,
+                                                f4 (&acc)[TL::MI][TL::NI], GemmFrags<V8, TL::NI> &f) {
+  constexpr int MI = TL::MI, NI = TL::NI, BK = TL::BK;
+  const int wm = wave / TL::WGN, wn = wave % TL::WGN;
+  constexpr int GP = MI / 2, NS = BK / 32, NG = NS * GP;
+  static_assert(NG % 2 == 0, "the deferred group must use the second fragment set");
+  constexpr int SPLIT = TL::BM >= 256 ? PHC_GEMM_SPLIT_DMA : 0;
+  if (!SPLIT && issue) stage(next, wr, 3);
+  if (SPLIT && issue) stage(next, wr, 1);
+  const char *ta = rd;
+  const char *tb = rd + TL::BM * BK * 2;
+  auto load_b = [&](V8 *fb, int s) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) read_frag<BK>(tb, wn * TL::TN + j * 16 + (lane & 15), s * 4 + (lane >> 4), fb[j]);
+  };
+  auto load_a = [&](V8 *fa, int s, int p) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+      read_frag<BK>(ta, wm * TL::TM + (2 * p + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), fa[ii]);
+  };
+  load_b(f.fb[0], 0);
+  load_a(f.fa[0], 0, 0);
+  if (carry) {  // the previous K-step's last group, behind this step's first reads
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_group<T, V8, NI>(f.fa[1], f.fb[1], acc[MI - 2], acc[MI - 1]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int q = 0; q + 1 < NG; ++q) {  // group NG - 1 is left in f.fa[1] / f.fb[1] for the next call
+    const int s = q / GP, p = q % GP;
+    const int s1 = (q + 1) / GP, p1 = (q + 1) % GP;
+    if (s1 != s) load_b(f.fb[s1 & 1], s1);
+    load_a(f.fa[(q + 1) & 1], s1, p1);
+    if (SPLIT && issue && q == (SPLIT * NG / 8 < NG - 1 ? SPLIT * NG / 8 : NG - 2)) stage(next, wr, 2);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
+    mfma_group<T, V8, NI>(f.fa[q & 1], f.fb[s & 1], acc[2 * p], acc[2 * p + 1]);
+  }
+}
+
+template <typename T, typename TL, typename V8>
+__device__ __forceinline__ void gemm_flush(f4 (&acc)[TL::MI][TL::NI], GemmFrags<V8, TL::NI> &f) {
+  mfma_group<T, V8, TL::NI>(f.fa[1], f.fb[1], acc[TL::MI - 2], acc[TL::MI - 1]);
 }
 
 // ---- 256 x 256 main loop as a ping-pong of two wave groups (PHC_GEMM_8PH) -------------------
@@ -602,6 +691,21 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
                        acc);
     }
     if (!second) phase_barrier();
+  } else if constexpr (TL::STAGES == 2 && PHC_GEMM_DEFER) {
+    using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
+    GemmFrags<V8, NI> fr;
+    stage(0, smem);
+    for (int kt = 0; kt < kt_n; ++kt) {
+      dma_barrier();  // tile kt landed; buffer (kt+1)&1 is no longer read
+      if (stage_aux && kt == kt_n - 1) {  // nothing else to stage: the epilogue's aux rows
+        stage_aux_pass(0, aux_slot(0));
+        stage_aux_pass(1, aux_slot(1));
+        stage_aux_pass(2, aux_slot(2));
+      }
+      gemm_step_defer<T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt + 1 < kt_n,
+                             kt > 0, stage, kt + 1, wave, lane, acc, fr);
+    }
+    gemm_flush<T, TL>(acc, fr);
   } else if constexpr (TL::STAGES == 2) {
     stage(0, smem);
     for (int kt = 0; kt < kt_n; ++kt) {

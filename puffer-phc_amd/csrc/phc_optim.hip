@@ -125,7 +125,8 @@ __global__ __launch_bounds__(kFinThreads) void k_opt_finish(const double *__rest
                                                             const int64_t *__restrict__ blk_range,
                                                             const int32_t *__restrict__ seg_blk, int nseg,
                                                             phc_adam_params hp, phc_opt_state *__restrict__ st,
-                                                            float *__restrict__ norm_out) {
+                                                            float *__restrict__ norm_out,
+                                                            double *__restrict__ norm_acc) {
   __shared__ double s_tot[kFinWaves], s_norm[kFinWaves], s_l2[kFinWaves];
   __shared__ int s_bad[kFinWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -198,6 +199,11 @@ __global__ __launch_bounds__(kFinThreads) void k_opt_finish(const double *__rest
     norm_out[0] = (float)norm_sum;
     norm_out[1] = total_norm;
     if (part_l2) norm_out[2] = (float)l2;
+    if (norm_acc) {  // the trainer's running sums of the logged row, as `acc += norm_out` would add them
+      norm_acc[0] += (double)norm_out[0];
+      norm_acc[1] += (double)norm_out[1];
+      norm_acc[2] += (double)norm_out[2];
+    }
   }
 }
 
@@ -614,9 +620,10 @@ extern "C" int64_t phc_opt_block_elems(void) { return 16384; }
 extern "C" int phc_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                             const int64_t *blk_range, int32_t nblk, const int32_t *seg_blk, int32_t nseg,
                             const phc_adam_params *hp, phc_opt_state *state, float *norm_out,
-                            const float *param_init, void *workspace, void *stream) {
+                            const float *param_init, void *workspace, double *norm_acc, void *stream) {
   PHC_REQUIRE(param && grad && exp_avg && exp_avg_sq && blk_range && seg_blk && hp && state && workspace,
               "opt_step: null argument");
+  PHC_REQUIRE(!norm_acc || norm_out, "opt_step: norm_acc needs norm_out");
   PHC_REQUIRE(n > 0 && nblk > 0 && nseg > 0, "opt_step: empty parameter set");
   PHC_REQUIRE(((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
                 reinterpret_cast<uintptr_t>(exp_avg) | reinterpret_cast<uintptr_t>(exp_avg_sq)) & 15) == 0,
@@ -629,7 +636,7 @@ extern "C" int phc_opt_step(float *param, const float *grad, float *exp_avg, flo
   hipLaunchKernelGGL(k_grad_partials, dim3((unsigned)nblk), dim3(kOptBlock), 0, st, grad, blk_range, part_sq,
                      part_bad, param, param_init, part_l2);
   hipLaunchKernelGGL(k_opt_finish, dim3(1), dim3(kFinThreads), 0, st, part_sq, part_bad, part_l2, blk_range, seg_blk,
-                     (int)nseg, *hp, state, norm_out);
+                     (int)nseg, *hp, state, norm_out, norm_acc);
   const int64_t quads = (n + 3) / 4;
   const int64_t blocks = std::min<int64_t>((quads + kOptBlock - 1) / kOptBlock, 4096);
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptBlock), 0, st, param, grad, exp_avg, exp_avg_sq, n,
@@ -647,8 +654,8 @@ extern "C" int64_t phc_adam_job_blocks(int32_t kind, int64_t rows, int64_t cols)
 extern "C" int phc_opt_step_operands(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                                      const int64_t *blk_range, int32_t nblk, const int32_t *seg_blk, int32_t nseg,
                                      const phc_adam_params *hp, phc_opt_state *state, float *norm_out,
-                                     const float *param_init, void *workspace, const phc_adam_job *jobs, int32_t njobs,
-                                     int64_t nblocks, void *stream) {
+                                     const float *param_init, void *workspace, double *norm_acc,
+                                     const phc_adam_job *jobs, int32_t njobs, int64_t nblocks, void *stream) {
   PHC_REQUIRE(param && grad && exp_avg && exp_avg_sq && blk_range && seg_blk && hp && state && workspace && jobs,
               "opt_step_operands: null argument");
   PHC_REQUIRE(n > 0 && nblk > 0 && nseg > 0, "opt_step_operands: empty parameter set");
@@ -662,7 +669,7 @@ extern "C" int phc_opt_step_operands(float *param, const float *grad, float *exp
   hipLaunchKernelGGL(k_grad_partials, dim3((unsigned)nblk), dim3(kOptBlock), 0, st, grad, blk_range, part_sq,
                      part_bad, param, param_init, part_l2);
   hipLaunchKernelGGL(k_opt_finish, dim3(1), dim3(kFinThreads), 0, st, part_sq, part_bad, part_l2, blk_range, seg_blk,
-                     (int)nseg, *hp, state, norm_out);
+                     (int)nseg, *hp, state, norm_out, norm_acc);
   hipLaunchKernelGGL(k_adam_ops, dim3((unsigned)nblocks), dim3(kPackThreads), 0, st, param, grad, exp_avg, exp_avg_sq,
                      jobs, (int)njobs, *hp, state);
   return check_launch("opt_step_operands");

@@ -161,7 +161,8 @@ __global__ __launch_bounds__(kPpoBlock) void k_ppo_fwd(PpoArgs p, float *__restr
 // stats[0] = loss, then pg, v, ent, old_approx_kl, approx_kl, clipfrac, bound (means): 256
 // threads accumulate strided block partials in double, then one wave adds the 256 sums in order
 __global__ __launch_bounds__(256) void k_ppo_reduce(const float *__restrict__ partial, int blocks, int64_t m, int a,
-                                                    phc_ppo_coefs c, float *__restrict__ stats) {
+                                                    phc_ppo_coefs c, float *__restrict__ stats,
+                                                    double *__restrict__ stats_acc) {
   __shared__ double red[kPpoStats][256];
   double acc[kPpoStats];
 #pragma unroll
@@ -180,6 +181,7 @@ __global__ __launch_bounds__(256) void k_ppo_reduce(const float *__restrict__ pa
     for (int i = 0; i < 256; ++i) t += red[k][i];
     mean = (float)(k == 6 ? t / ((double)m * a) : t / (double)m);
     stats[1 + k] = mean;
+    if (stats_acc) stats_acc[k] += (double)mean;  // the trainer's running sum over minibatches
   }
   const float pg = __shfl(mean, 0, 64), v = __shfl(mean, 1, 64), ent = __shfl(mean, 2, 64),
               bound = __shfl(mean, 6, 64);
@@ -227,7 +229,7 @@ extern "C" int phc_ppo_loss_fwd(const float *mu, const float *log_sigma, const f
                                 const float *old_logprob, const float *adv, const float *adv_mean_std,
                                 const float *value, const float *old_value, const float *returns, int64_t m,
                                 int32_t a, const phc_ppo_coefs *coefs, float *row_coef, float *stats,
-                                void *workspace, void *stream) {
+                                double *stats_acc, void *workspace, void *stream) {
   PHC_REQUIRE(coefs && row_coef && stats && workspace, "ppo_loss_fwd: null output/workspace");
   const PpoArgs p{mu, log_sigma, actions, old_logprob, adv, adv_mean_std, value, old_value, returns, m, a, *coefs};
   if (int rc = check_ppo(p)) return rc;
@@ -235,7 +237,7 @@ extern "C" int phc_ppo_loss_fwd(const float *mu, const float *log_sigma, const f
   float *partial = static_cast<float *>(workspace);
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(k_ppo_fwd, dim3(blocks), dim3(kPpoBlock), 0, st, p, row_coef, partial);
-  hipLaunchKernelGGL(k_ppo_reduce, dim3(1), dim3(256), 0, st, partial, blocks, m, (int)a, *coefs, stats);
+  hipLaunchKernelGGL(k_ppo_reduce, dim3(1), dim3(256), 0, st, partial, blocks, m, (int)a, *coefs, stats, stats_acc);
   return check_launch("ppo_loss_fwd");
 }
 

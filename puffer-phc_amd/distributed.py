@@ -149,6 +149,12 @@ class FlatGrads:
     def zero(self):
         self.flat.zero_()
 
+    def fill_grads_(self, value):
+        """Fill every parameter's gradient view (the alignment gaps between them keep their zeros):
+        tests pre-fill with NaN to prove a backward writes every gradient."""
+        for p in self.params:
+            p.grad.fill_(value)
+
     def allreduce_mean(self):
         if not is_dist():
             return

@@ -45,7 +45,10 @@ class Box:
 
 class ReplayPhysics:
     """Physics stand-in: rigid bodies = reference state at the env's next control time plus
-    gaussian noise (phc_physics_replay).  Not a reference interface."""
+    gaussian noise (phc_physics_replay).  Not a reference interface.  The noise is keyed by the
+    env's own device counters (episode rng counter, progress), so a step launch carries no per-step
+    host value and a captured graph of steps replays fresh noise every time (the kernel's host
+    counter argument stays 0)."""
 
     def __init__(self, pos_sigma=0.02, force_scale=50.0, seed=0):
         self.pos_sigma = pos_sigma
@@ -54,17 +57,16 @@ class ReplayPhysics:
         self.counter = 0
 
     def step(self, env):
-        self.counter += 1
         _native.physics_replay(env._env_c, env._motion_lib.packed.c, env._step_params, self.pos_sigma,
                                self.force_scale, self.seed, self.counter)
 
-    def step_fused(self, env, params, pd, timer=None):
+    def step_fused(self, env, params, pd, timer=None, env_c=None):
         """The stand-in, the action -> PD map and the post-physics env step in one launch
         (phc_env_step_replay): the replayed state is the reference blend the env step reads
-        anyway, so it never makes an HBM round trip."""
-        self.counter += 1
-        _native.env_step_replay(env._env_c, env._motion_lib.packed.c, params, self.pos_sigma, self.force_scale,
-                                self.seed, self.counter, pd=pd, timer=timer)
+        anyway, so it never makes an HBM round trip.  env_c: the env struct to launch with (default
+        the env's own)."""
+        _native.env_step_replay(env._env_c if env_c is None else env_c, env._motion_lib.packed.c, params,
+                                self.pos_sigma, self.force_scale, self.seed, self.counter, pd=pd, timer=timer)
 
 
 class HumanoidPHC:
@@ -303,10 +305,28 @@ class HumanoidPHC:
         self.obs_operand_fresh = False
         self._init_amp_obs()
 
-    def step(self, actions, auto_reset=False):
+    def launch_key(self):
+        """Everything a captured step launch holds by value: the env struct, the packed library's
+        descriptor (replaced by resample_motions / the eval toggles) and both step-parameter blocks.
+        A graph captured under another key replays stale pointers."""
+        parts = [bytes(self._env_c), bytes(self._motion_lib.packed.c), bytes(self._step_params)]
+        auto = getattr(self, "_step_params_auto", None)
+        if auto is not None:
+            parts.append(bytes(auto))
+        return b"".join(parts)
+
+    def stats_env_struct(self, stats):
+        """A copy of the env struct whose per-workgroup logging rows go to `stats` (same shape as
+        PHCPufferEnv.stats): the captured rollout block gives every step its own rows."""
+        c = type(self._env_c).from_buffer_copy(self._env_c)
+        c.stats = _native._ptr(stats, torch.float64, tuple(self._puffer["stats"].shape), "stats")
+        return c
+
+    def step(self, actions, auto_reset=False, env_c=None):
         """humanoid_phc.py:105-172 with the physics stand-in.  With auto_reset (used by
         PHCPufferEnv) the envs that come up for reset are re-initialised inside the same
-        fused kernel, as PHCPufferEnv.step's env.reset(reset_indices) does next."""
+        fused kernel, as PHCPufferEnv.step's env.reset(reset_indices) does next.  env_c: the env
+        struct of the fused replay launch (stats_env_struct), default the env's own."""
         if actions.dtype != torch.float32 or not actions.is_contiguous():
             actions = actions.float().contiguous()
         # eval mode records MPJPE / positions of the step's own outcome before the envs reset
@@ -318,8 +338,10 @@ class HumanoidPHC:
                             clip)
         if self.fused_env_step and hasattr(self.physics, "step_fused"):
             # R13 + the physics stand-in + the env step: one launch
-            self.physics.step_fused(self, params, pd, timer=self.kernel_timer)
+            self.physics.step_fused(self, params, pd, timer=self.kernel_timer, env_c=env_c)
         else:
+            if env_c is not None:
+                raise ValueError("HumanoidPHC.step: env_c needs the fused replay step")
             if hasattr(self.physics, "step_actions"):  # R13 folded into the physics launch
                 self.physics.step_actions(self, pd)
             else:

@@ -13,6 +13,7 @@ packed rows directly.
 """
 
 import glob
+import os
 import os.path as osp
 import random
 from enum import Enum
@@ -107,6 +108,68 @@ class PackedMotions:
         return self.frames[..., 10:13]
 
 
+class ClipPool:
+    """Every clip of an in-memory (file-mode) library resident in HBM back to back, as float64 the way
+    load_motions uploads them: quat [P, 24, 4], trans [P, 3], aa [P, A]; per-clip first frame, length
+    and fps on the host.  Built once, on the first load; each (re)load then gathers the selected clips'
+    cropped frames with one device index gather instead of the reference's per-clip host loop
+    (load_motion_with_skeleton, motion_lib.py:766-800: crop, convert and heading-rotate each clip,
+    fanned out over num_thread processes at motion_lib.py:334-368), which at C3 scale (4,096 clips
+    per resample out of 11,313) is the reload's cost."""
+
+    CHUNK_FRAMES = 1 << 18  # host staging per upload (about 200 MB of float64 rows)
+
+    def __init__(self, clips, device):
+        n = len(clips)
+        self.lens = np.fromiter((c["root_trans_offset"].shape[0] for c in clips), np.int64, n)
+        self.starts = np.concatenate([[0], np.cumsum(self.lens)[:-1]]).astype(np.int64)
+        self.fps = np.fromiter((float(c.get("fps", 30)) for c in clips), np.float64, n)
+        total = int(self.lens.sum())
+        j = int(np.asarray(clips[0]["pose_quat_global"]).shape[1])
+        a = int(np.asarray(clips[0]["pose_aa"]).reshape(self.lens[0], -1).shape[1])
+        self.quat = torch.empty((total, j, 4), dtype=torch.float64, device=device)
+        self.trans = torch.empty((total, 3), dtype=torch.float64, device=device)
+        self.aa = torch.empty((total, a), dtype=torch.float64, device=device)
+        # host staging in chunks of whole clips, one upload per chunk
+        i = 0
+        while i < n:
+            k = i
+            while k < n and (k == i or self.starts[k] + self.lens[k] - self.starts[i] <= self.CHUNK_FRAMES):
+                k += 1
+            f0, f1 = int(self.starts[i]), int(self.starts[k - 1] + self.lens[k - 1])
+            hq = np.empty((f1 - f0, j, 4))
+            ht = np.empty((f1 - f0, 3))
+            ha = np.empty((f1 - f0, a))
+            for c in range(i, k):
+                s, e = int(self.starts[c]) - f0, int(self.starts[c] + self.lens[c]) - f0
+                clip = clips[c]
+                rt = clip["root_trans_offset"]
+                hq[s:e] = np.asarray(clip["pose_quat_global"], np.float64)
+                ht[s:e] = np.asarray(rt.numpy() if isinstance(rt, torch.Tensor) else rt, np.float64)
+                ha[s:e] = np.asarray(clip["pose_aa"], np.float64).reshape(e - s, -1)
+            self.quat[f0:f1].copy_(torch.from_numpy(hq))
+            self.trans[f0:f1].copy_(torch.from_numpy(ht))
+            self.aa[f0:f1].copy_(torch.from_numpy(ha))
+            i = k
+
+    def gather(self, ids, crop_start, counts):
+        """The frames [crop_start, crop_start + count) of clips `ids` (numpy), back to back."""
+        dev = self.quat.device
+        n = len(ids)
+        cnt = torch.from_numpy(np.asarray(counts, np.int64)).to(dev)
+        total = int(np.asarray(counts).sum())
+        src0 = torch.from_numpy(self.starts[ids] + crop_start).to(dev)
+        dst0 = cnt.cumsum(0) - cnt
+        seg = torch.repeat_interleave(torch.arange(n, device=dev), cnt, output_size=total)
+        idx = torch.arange(total, device=dev) - dst0[seg] + src0[seg]
+        return self.quat[idx], self.trans[idx], self.aa[idx]
+
+
+# PHC_MOTION_POOL=0: the per-clip host loop for in-memory libraries too (the directory mode, whose
+# clips load from disk one by one, always takes it)
+MOTION_POOL = os.environ.get("PHC_MOTION_POOL", "1") != "0"
+
+
 class MotionLibBase:
     def __init__(self, motion_lib_cfg):
         self.m_cfg = motion_lib_cfg
@@ -166,6 +229,53 @@ class MotionLibBase:
         return c
 
     # ----------------------------------------------------------- load ---
+    def _gather_clips(self, ids):
+        """The selected clips cropped to max_length (a random window unless deterministic, the
+        reference's random.randint per long clip, motion_lib.py:776-781) with their heading draws
+        (np.random per clip, motion_lib.py:790-793): (quat f64 [F, J, 4], trans f64 [F, 3], aa f64
+        [F, A] on the device, counts, fps, heading).  The draws come from the same generators in the
+        same order as the reference's loop: python `random` for the crops, then numpy for headings."""
+        max_length = self.m_cfg.max_length
+        randomize = not (self.m_cfg.is_deterministic or self.m_cfg.im_eval)
+        dev = self._device
+        if MOTION_POOL and self.mode == MotionlibMode.file and isinstance(self._motion_data_list[0], dict):
+            pool = getattr(self, "_pool", None)
+            if pool is None:
+                pool = self._pool = ClipPool(self._motion_data_list, dev)
+            lens = pool.lens[ids]
+            start = np.zeros(len(ids), np.int64)
+            counts = lens.copy()
+            if max_length != -1:
+                long = lens >= max_length
+                counts[long] = max_length
+                if not self.m_cfg.is_deterministic:
+                    for j in np.flatnonzero(long):
+                        start[j] = random.randint(0, int(lens[j]) - max_length)
+            heading = np.pi * (2 * np.random.random(len(ids)) - 1.0) if randomize else np.zeros(len(ids))
+            q, t, aa = pool.gather(ids, start, counts)
+            return q, t, aa, counts.tolist(), pool.fps[ids].tolist(), heading.tolist()
+        quats, trans, counts, fps, aas, heading = [], [], [], [], [], []
+        for idx in ids.tolist():
+            clip = self._clip(idx)
+            seq_len = clip["root_trans_offset"].shape[0]
+            if max_length == -1 or seq_len < max_length:
+                start, end = 0, seq_len
+            else:
+                start = 0 if self.m_cfg.is_deterministic else random.randint(0, seq_len - max_length)
+                end = start + max_length
+            rt = clip["root_trans_offset"]
+            rt = rt.numpy() if isinstance(rt, torch.Tensor) else np.asarray(rt)
+            quats.append(np.asarray(clip["pose_quat_global"][start:end], np.float64))
+            trans.append(np.asarray(rt[start:end], np.float64))
+            aas.append(np.asarray(clip["pose_aa"][start:end], np.float64).reshape(end - start, -1))
+            counts.append(end - start)
+            fps.append(float(clip.get("fps", 30)))
+            heading.append(np.pi * (2 * np.random.random() - 1.0) if randomize else 0.0)
+        q = torch.from_numpy(np.concatenate(quats)).to(dev)
+        t = torch.from_numpy(np.concatenate(trans)).to(dev)
+        aa = torch.from_numpy(np.concatenate(aas)).to(dev)
+        return q, t, aa, counts, fps, heading
+
     def _load_motions(self, skeleton_trees, gender_betas, limb_weights, random_sample=True, start_idx=0, max_len=-1,
                       sample_idxes=None):
         """motion_lib.py:257-429 with FK on the GPU."""
@@ -183,29 +293,8 @@ class MotionLibBase:
         self.curr_motion_keys = self._motion_data_keys[sample_idxes.cpu().numpy()]
         self._sampling_batch_prob = self._sampling_prob[sample_idxes] / self._sampling_prob[sample_idxes].sum()
 
-        max_length = self.m_cfg.max_length
-        quats, trans, counts, fps, aas, heading = [], [], [], [], [], []
-        for idx in sample_idxes.cpu().tolist():
-            clip = self._clip(idx)
-            seq_len = clip["root_trans_offset"].shape[0]
-            if max_length == -1 or seq_len < max_length:
-                start, end = 0, seq_len
-            else:
-                start = 0 if self.m_cfg.is_deterministic else random.randint(0, seq_len - max_length)
-                end = start + max_length
-            rt = clip["root_trans_offset"]
-            rt = rt.numpy() if isinstance(rt, torch.Tensor) else np.asarray(rt)
-            quats.append(np.asarray(clip["pose_quat_global"][start:end], np.float64))
-            trans.append(np.asarray(rt[start:end], np.float64))
-            aas.append(np.asarray(clip["pose_aa"][start:end], np.float64).reshape(end - start, -1))
-            counts.append(end - start)
-            fps.append(float(clip.get("fps", 30)))
-            randomize = not (self.m_cfg.is_deterministic or self.m_cfg.im_eval)
-            heading.append(np.pi * (2 * np.random.random() - 1.0) if randomize else 0.0)
+        q, t, aa, counts, fps, heading = self._gather_clips(sample_idxes.cpu().numpy())
         dev = self._device
-        q = torch.from_numpy(np.concatenate(quats)).to(dev)
-        t = torch.from_numpy(np.concatenate(trans)).to(dev)
-        aa = torch.from_numpy(np.concatenate(aas)).to(dev)
         cnt = torch.tensor(counts, dtype=torch.int64, device=dev)
         hd = torch.tensor(heading, dtype=torch.float64, device=dev)
         if bool((hd != 0).any()):

@@ -274,11 +274,12 @@ class FlatAdam(torch.optim.Adam):
         for o in owners:
             weight_cache.mark_fresh(o)
 
-    def fused_step(self, max_norm):
+    def fused_step(self, max_norm, norm_acc=None):
         """clip_grad_norm_(max_norm) + Adam (+ loss-scale update); returns the device [3] tensor
         (sum of per-parameter gradient norms as the reference logs, global norm, L2-init
         distance of the parameters before the update when tracked).  The learning rate comes from
-        the device state (sync_lr); under graph capture the caller syncs it before each replay."""
+        the device state (sync_lr); under graph capture the caller syncs it before each replay.
+        norm_acc (device float64 [3], optional) += that tensor in the same launch."""
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         gf, bf, gi = self._hp_scale
@@ -291,7 +292,8 @@ class FlatAdam(torch.optim.Adam):
         args = (self.param_flat.data_ptr(), self.flat_grads.flat.data_ptr(), self.exp_avg.data_ptr(),
                 self.exp_avg_sq.data_ptr(), n, self._blk.data_ptr(), self._blk.shape[0], self._seg.data_ptr(),
                 self._seg.numel() - 1, ctypes.byref(hp), self._state.data_ptr(), self.norms.data_ptr(),
-                self.param_init.data_ptr() if self.param_init is not None else None, self._ws.data_ptr())
+                self.param_init.data_ptr() if self.param_init is not None else None, self._ws.data_ptr(),
+                N._ptr(norm_acc, torch.float64, (3,), "norm_acc", nullable=True))
         if ops is None:
             N._check(N.lib().phc_opt_step(*args, N._stream()), "phc_opt_step")
             # the parameters changed behind torch's version counters: every GEMM-operand cache of

@@ -42,7 +42,7 @@ class FusedPPOLossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weights, cfg, data, n_trunk, *params):
-        eps, log_sigma, coefs, ctx.store_grads = cfg
+        eps, log_sigma, coefs, ctx.store_grads, stats_acc = cfg
         y, saved = mfma_trunk_forward(x, weights, True)
         la_w, la_b, lc_w, lc_b, mu_w, mu_b, v_w, v_b = [p.detach() for p in params[n_trunk:]]
         actions, old_logprob, adv, adv_ms, old_value, returns = data
@@ -54,7 +54,7 @@ class FusedPPOLossFn(torch.autograd.Function):
             else:
                 mu = torch.addmm(mu_b, h_a, mu_w.t())
             stats, row_coef = N.ppo_loss_fwd(mu, log_sigma, actions, old_logprob, adv, adv_ms, value, old_value,
-                                             returns, coefs)
+                                             returns, coefs, stats_acc=stats_acc)
         ctx.saved, ctx.tail, ctx.params, ctx.n_trunk = saved, tail, params, n_trunk
         ctx.ppo = (mu, log_sigma, actions, row_coef, coefs)
         st = stats[1:]
@@ -124,11 +124,12 @@ def fused_ppo_supported(policy, obs):
 
 
 def fused_ppo_loss(policy, obs, actions, old_logprob, adv, adv_mean_std, old_value, returns, coefs,
-                   store_grads=False):
+                   store_grads=False, stats_acc=None):
     """(loss, stats [7]: pg, v, entropy, old_approx_kl, approx_kl, clipfrac, bound) of one
     minibatch; the backward writes every policy gradient.  store_grads: with the gradients bound
     to a flat buffer (direct mode), the backward stores them instead of adding to them, so the
-    buffer need not be zeroed first (every parameter of the policy has exactly one writer)."""
+    buffer need not be zeroed first (every parameter of the policy has exactly one writer).  stats_acc
+    (device float64 [7], optional) += the stats in the objective's own reduce launch."""
     h = policy._head
     la, lc = policy.actor_mlp[h], policy.critic_mlp[h]
     vh, mh = policy.critic_mlp[h + 2], policy.mu[0]
@@ -137,5 +138,5 @@ def fused_ppo_loss(policy, obs, actions, old_logprob, adv, adv_mean_std, old_val
     f = lambda t: t.detach().float().contiguous().reshape(-1)  # noqa: E731
     data = (actions.detach().float().contiguous(), f(old_logprob), f(adv), adv_mean_std.detach().float().contiguous(),
             f(old_value), f(returns))
-    cfg = (la.eps, policy.sigma.detach().float().contiguous().reshape(-1), coefs, bool(store_grads))
+    cfg = (la.eps, policy.sigma.detach().float().contiguous().reshape(-1), coefs, bool(store_grads), stats_acc)
     return FusedPPOLossFn.apply(obs, policy._twin, cfg, data, len(trunk), *trunk, *tail)

@@ -77,6 +77,7 @@ def test_two_rank_gloo_bench_reports_rows_over_wall():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_envs"] == 1024
     dp = out["config"]["dp"]  # the exposed all-reduce wait per minibatch backward
+    assert set(dp) == set(_bench().DP_FIELDS)
     assert dp["mode"] == "split" and dp["minibatches_timed"] >= 4 and dp["backend"] == "gloo"
     assert dp["allreduce_exposed_ms_per_minibatch_max_rank"] >= dp["allreduce_exposed_ms_per_minibatch_rank0"] >= 0
     rows = out["config"]["env_steps_timed"]
@@ -85,3 +86,55 @@ def test_two_rank_gloo_bench_reports_rows_over_wall():
     assert 2 * 8192 <= rows < 2 * 8192 + 2 * 512
     wall_s = out["ms_per_step"] * out["steps"] / 1e3
     assert out["value"] == pytest.approx(rows / wall_s, rel=1e-9)
+
+
+def _dp_worker(rank, world, port, root, out):
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, root)
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank r waited 0.5 + r ms per backward over 8 minibatches (rank 1 reports none: a rank with no
+        # timed backward contributes 0 to the max)
+        exp = 0.5 + rank if rank != 1 else None
+        dp = bench.dp_summary("split", exp, 8, 4 * 1000, "cpu")
+        mine = torch.tensor([131072.0 + 17], dtype=torch.float64)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        total = bench.whole_job_steps([float(c) for c in every], True, world)
+        out.put((rank, dp, total))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_summary_world3_gloo_cpu():
+    """config.dp over three gloo ranks on the CPU: every field present, the slowest rank's exposed
+    wait is the max over ranks, the backend is named, and the ppo count is taken once."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 3, port, ROOT, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    fields = _bench().DP_FIELDS
+    for rank, dp, total in res:
+        assert tuple(dp) == fields
+        assert dp["backend"] == "gloo" and dp["mode"] == "split" and dp["minibatches_timed"] == 8
+        assert dp["allreduce_exposed_ms_per_minibatch_max_rank"] == 2.5
+        assert dp["allreduce_exposed_ms_per_minibatch_rank0"] == (0.5 + rank if rank != 1 else None)
+        assert dp["grad_bytes_per_minibatch"] == 4000
+        assert total == 131072.0 + 17

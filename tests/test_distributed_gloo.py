@@ -106,3 +106,95 @@ def _worker(rank, world, port, root):
 def test_collectives_world2():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     mp.spawn(_worker, args=(2, _free_port(), root), nprocs=2, join=True)
+
+
+L_TRUNK = 5  # twin trunk depth of the test model (PHCPolicy: 6)
+
+
+def _twin_model(seed):
+    """A twin-trunk stand-in with PHCPolicy's parameter grouping: layer l of the trunk owns
+    [actor W, actor b, critic W, critic b]; a tail (value / mu heads) follows."""
+    torch.manual_seed(seed)
+    dims = [12, 24, 20, 16, 16, 8]
+    actor = torch.nn.ModuleList([torch.nn.Linear(dims[i], dims[i + 1]) for i in range(L_TRUNK)])
+    critic = torch.nn.ModuleList([torch.nn.Linear(dims[i], dims[i + 1]) for i in range(L_TRUNK)])
+    mu, value = torch.nn.Linear(dims[-1], 3), torch.nn.Linear(dims[-1], 1)
+    trunk = [p for l in range(L_TRUNK) for p in (actor[l].weight, actor[l].bias, critic[l].weight, critic[l].bias)]
+    tail = [mu.weight, mu.bias, value.weight, value.bias]
+
+    def loss(x, y):
+        a = c = x
+        for l in range(L_TRUNK):
+            a, c = torch.nn.functional.silu(actor[l](a)), torch.nn.functional.silu(critic[l](c))
+        return ((mu(a) - y) ** 2).mean() + ((value(c) - y[:, :1]) ** 2).mean()
+
+    return trunk, tail, loss
+
+
+def _ready_sequence(mode, trunk, tail):
+    """The GRAD_READY calls the fused backward makes in each data-parallel mode (fused_ppo.py:95-98 for
+    the tail; twin_mlp.py mfma_trunk_backward for the trunk): grouped = one call with every trunk
+    layer, last first; per_layer = one call per layer as its gradient lands; split = the last three
+    layers, then (cumulatively) all of them."""
+    L = len(trunk) // 4
+    layers = lambda lo: [p for l in range(L - 1, lo - 1, -1) for p in trunk[4 * l:4 * l + 4]]  # noqa: E731
+    seq = [tail]
+    if mode == "grouped":
+        seq.append(layers(0))
+    elif mode == "per_layer":
+        seq += [trunk[4 * l:4 * l + 4] for l in range(L - 1, -1, -1)]
+    else:
+        seq += [layers(max(L - 3, 0)), layers(0)]
+    return seq
+
+
+def _dp_modes_worker(rank, world, port, root):
+    import sys
+
+    sys.path.insert(0, root)
+    import phc_amd_path
+
+    phc_amd_path.register()
+    from puffer_phc_amd import distributed as D
+    from puffer_phc_amd.policies import twin_mlp
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(7 + rank)
+        x, y = torch.randn(32, 12, generator=g), torch.randn(32, 3, generator=g)
+        xs = [torch.empty_like(x) for _ in range(world)]
+        ys = [torch.empty_like(y) for _ in range(world)]
+        dist.all_gather(xs, x)
+        dist.all_gather(ys, y)
+        rt, rtail, rloss = _twin_model(0)
+        rloss(torch.cat(xs), torch.cat(ys)).backward()  # the mean loss over the union, one process
+        want = [p.grad.clone() for p in rtail + rt]
+        for mode in twin_mlp.DP_MODES:
+            twin_mlp.set_dp_mode(mode)
+            assert twin_mlp.dp_mode() == mode
+            trunk, tail, loss = _twin_model(0)
+            order = tail + [p for l in range(L_TRUNK - 1, -1, -1) for p in trunk[4 * l:4 * l + 4]]
+            fg = D.FlatGrads(trunk + tail, order=order)
+            fg.zero()
+            loss(x, y).backward()  # the per-rank gradient (the mean over this rank's rows)
+            fg.overlap_begin()
+            seq = _ready_sequence(mode, trunk, tail)
+            for group in seq:
+                twin_mlp.GRAD_READY(group)
+            # every group is one contiguous span of the flat buffer (alignment gaps bridged): one
+            # all-reduce per call, none for parameters an earlier call already reduced
+            assert len(fg._works) == len(seq), (mode, len(fg._works))
+            fg.overlap_finish()
+            for p, w in zip(tail + trunk, want):
+                torch.testing.assert_close(p.grad, w, atol=1e-6, rtol=1e-5, msg=mode)
+        twin_mlp.set_dp_mode("grouped")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_modes_world2():
+    """grouped / per_layer / split: each mode's readiness calls all-reduce every gradient exactly once
+    and leave every rank with the gradient of the mean loss over both ranks' rows."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mp.spawn(_dp_modes_worker, args=(2, _free_port(), root), nprocs=2, join=True)

@@ -77,7 +77,7 @@ def _worker(rank, world, port, out_dir, mode):
         def backward(batch, overlap):
             obs, atn, old_lp, adv, val, ret = batch
             if overlap:  # as clean_pufferl.core.train runs it: gradients stored, the buffer not zeroed
-                fg.flat.fill_(float("nan"))
+                fg.fill_grads_(float("nan"))
             else:
                 fg.zero()
             with torch.autocast("cuda", dtype=torch.float16):

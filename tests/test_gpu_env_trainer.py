@@ -282,3 +282,98 @@ def test_rollout_env_written_operand_matches_obs_half():
     for (a, b) in zip(*runs):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+def test_block_rollout_matches_single_step_graphs(monkeypatch):
+    """evaluate() with its first min_steps steps replayed as ONE captured block (policy + store + fused
+    env step per step, core.RolloutStep.run_block) against one graph per step with the env step eager:
+    the same experience rows, the same tick, and the same mean_and_log infos — log points that fall
+    inside a block included (log_interval 5 does not divide the 24-step rollouts)."""
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.clean_pufferl import core
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig, TrainConfig
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    runs = []
+    for block in (False, True):
+        monkeypatch.setattr(core, "BLOCK_GRAPH", block)
+        q, t, c, fps = synthetic_clips(64, 12, 40, seed=21, device=DEV)  # short clips: many resets
+        env = PHCPufferEnv(EnvConfig(num_envs=64, seed=8, log_interval=5),
+                           motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
+        torch.manual_seed(0)
+        policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+        cfg = TrainConfig(batch_size=64 * 24, minibatch_size=64 * 8, bptt_horizon=8, checkpoint_interval=10 ** 9)
+        comps, info, _ = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+        infos = []
+        for it in range(4):
+            torch.manual_seed(10 + it)
+            _, env_infos = clean_pufferl.evaluate(comps, info)
+            infos.append({k: [float(x) for x in v] for k, v in env_infos.items()})
+        e = comps.experience
+        runs.append(dict(step=info.global_step, tick=env.tick, obs=e.obs.clone(), rew=e.rewards.clone(),
+                         done=e.dones.clone(), ids=e.env_ids.clone(), infos=infos,
+                         blocks=len(getattr(comps.rollout, "_blocks", {}))))
+    a, b = runs
+    assert a["blocks"] == 0 and b["blocks"] == 1
+    assert a["step"] == b["step"] and a["tick"] == b["tick"]
+    for k in ("obs", "rew", "done", "ids"):
+        assert torch.equal(a[k], b[k]), k
+    for ia, ib in zip(a["infos"], b["infos"]):
+        assert ia.keys() == ib.keys()
+        for k in ia:
+            np.testing.assert_allclose(ia[k], ib[k], rtol=1e-9, atol=1e-12, err_msg=k)
+
+
+def _dict_clips(n, lo, hi, seed):
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    q, t, c, fps = synthetic_clips(n, lo, hi, seed=seed, device=DEV)
+    qh, th, ch, fh = q.cpu().numpy(), t.cpu().numpy(), c.cpu().numpy(), fps.cpu().numpy()
+    ends = np.cumsum(ch)
+    return {f"clip_{i:04d}": {"pose_quat_global": qh[ends[i] - ch[i]:ends[i]],
+                              "root_trans_offset": torch.from_numpy(th[ends[i] - ch[i]:ends[i]]),
+                              "pose_aa": np.zeros((int(ch[i]), 72)), "fps": float(fh[i])} for i in range(n)}
+
+
+def test_block_rollout_follows_resample(monkeypatch):
+    """resample_motions() replaces the packed library the captured block's env-step launches hold by
+    value: the block graphs are re-captured under the new library (HumanoidPHC.launch_key), and the
+    rollout before and after the resample equals the per-step graphs' bit for bit."""
+    import random
+
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.clean_pufferl import core
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig, TrainConfig
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+
+    clips = _dict_clips(200, 12, 60, seed=5)
+    runs = []
+    for block in (False, True):
+        monkeypatch.setattr(core, "BLOCK_GRAPH", block)
+        env = PHCPufferEnv(EnvConfig(num_envs=64, seed=8, log_interval=5, max_episode_length=40), motion_data=clips)
+        torch.manual_seed(0)
+        policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+        cfg = TrainConfig(batch_size=64 * 24, minibatch_size=64 * 8, bptt_horizon=8, checkpoint_interval=10 ** 9)
+        comps, info, _ = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+        obs, keys = [], []
+        for it in range(5):
+            if it == 3:
+                torch.manual_seed(99)
+                random.seed(98)
+                np.random.seed(97)
+                env.env.resample_motions()
+                env.reset()
+            torch.manual_seed(10 + it)
+            clean_pufferl.evaluate(comps, info)
+            obs.append(comps.experience.obs.clone())
+            keys.append(getattr(comps.rollout, "_blocks_key", None))
+        runs.append(dict(obs=obs, keys=keys, ids=env.env._motion_lib._curr_motion_ids.clone(), step=info.global_step))
+    a, b = runs
+    assert torch.equal(a["ids"], b["ids"]) and a["step"] == b["step"]
+    assert b["keys"][2] is not None and b["keys"][3] != b["keys"][2] and b["keys"][4] == b["keys"][3]
+    for x, y in zip(a["obs"], b["obs"]):
+        assert torch.equal(x, y)

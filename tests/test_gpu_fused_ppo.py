@@ -195,7 +195,7 @@ def test_store_grads_writes_every_gradient(rows):
     out = []
     for store in (False, True):
         if store:
-            fg.flat.fill_(float("nan"))
+            fg.fill_grads_(float("nan"))
         else:
             fg.zero()
         with torch.autocast("cuda", dtype=torch.float16):

@@ -61,11 +61,12 @@ def test_clip_adam_matches_torch(max_norm):
         torch.testing.assert_close(out[2], l2, rtol=1e-4, atol=1e-12)
         for a, b in zip(ours, ref):
             torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-6, atol=1e-8)
-    # the module parameters are views of the flat buffer
-    off = 0
+    # the module parameters are views of the flat buffer, each slice starting 64-B aligned
+    from puffer_phc_amd.distributed import PARAM_ALIGN
+
     for p in ours:
-        assert p.data_ptr() == opt.param_flat[off:].data_ptr()
-        off += p.numel()
+        off = fg._range[id(p)][0]
+        assert off % PARAM_ALIGN == 0 and p.data_ptr() == opt.param_flat[off:].data_ptr()
     assert int(opt._i[2]) == 4
 
 

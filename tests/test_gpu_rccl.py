@@ -104,7 +104,7 @@ def test_rccl_overlapped_backward_bit_equal(rccl, mode):
     coefs = ppo_coefs(TrainConfig(), pol.soft_bound)
 
     def backward(dp):
-        fg.flat.fill_(float("nan"))
+        fg.fill_grads_(float("nan"))
         with torch.autocast("cuda", dtype=torch.float16):
             xh = pol.obs_half_input(obs)
             loss, _ = fused_ppo_loss(pol, xh, atn, old_lp, adv, ms, val, ret, coefs, store_grads=True)

@@ -60,3 +60,21 @@ def test_pending_info_reads_a_snapshot_of_the_buffer():
     first = dict(info)
     buf.zero_()
     assert dict(info) == first
+
+
+def test_flush_counts_unread_infos_once():
+    """PHCPufferEnv.flush resolves every outstanding ring slot: episodes of infos nobody read are
+    counted, each once; a second flush (or a later read) adds nothing."""
+    env = _env()
+    env._info_ring = [[None, None] for _ in range(4)]
+    evs = [_Event() for _ in range(3)]
+    infos = [PendingInfo(env, _sums(float(k + 1)), evs[k]) for k in range(3)]
+    for k, info in enumerate(infos):
+        env._info_ring[k][1] = info
+    dict(infos[1])  # one read already
+    assert env.episode_count == 2
+    PHCPufferEnv.flush(env)
+    assert env.episode_count == 1 + 2 + 3 and [e.waits for e in evs] == [1, 1, 1]
+    PHCPufferEnv.flush(env)
+    dict(infos[0])
+    assert env.episode_count == 6 and [e.waits for e in evs] == [1, 1, 1]

@@ -25,6 +25,9 @@ M = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 DIMS = [960, 2048, 1536, 1024, 1024, 512, 512]  # padded input width, then the six layer widths
 REPS = int(os.environ.get("REPS", "20"))
 PER_TRUNK = os.environ.get("PER_TRUNK", "0") == "1"  # one launch per trunk (batch 1) instead of batched twins
+# YONLY=1: the forward GEMMs store the activation only, not the pre-activation (the upper bound of a
+# y-only forward store whose consumers would recompute what they need)
+AUX = os.environ.get("YONLY", "0") != "1"
 
 
 SUMS = []
@@ -60,7 +63,7 @@ def main():
     b0 = torch.randn(2 * DIMS[1], device=dev, generator=g)
     z = torch.empty((2, M, DIMS[1]), dtype=dt, device=dev)
     pre = torch.empty((M, 2 * DIMS[1]), dtype=dt, device=dev)
-    us = timeit(lambda: N.twin_gemm(x, w0, N.EPI_BIAS_SILU, z, (2, DIMS[1]), bias=b0, aux=pre,
+    us = timeit(lambda: N.twin_gemm(x, w0, N.EPI_BIAS_SILU, z, (2, DIMS[1]), bias=b0, aux=pre if AUX else None,
                                     aux_layout=N.SPLIT, out_layout=N.GROUPED), z)
     rows.append(("fwd L1", M, 2 * DIMS[1], DIMS[0], 1, us))
     for l in range(2, 7):
@@ -72,11 +75,11 @@ def main():
             o = torch.empty((2, M, n), dtype=dt, device=dev)
             p = torch.empty((2, M, n), dtype=dt, device=dev)
             us = timeit(lambda: [N.twin_gemm(a[t], w[t], N.EPI_BIAS_SILU, o[t], (1, n), bias=b[t * n:(t + 1) * n],
-                                             aux=p[t]) for t in range(2)], o)
+                                             aux=p[t] if AUX else None) for t in range(2)], o)
         elif l < 6:
             o = torch.empty((2, M, n), dtype=dt, device=dev)
             p = torch.empty((2, M, n), dtype=dt, device=dev)
-            us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS_SILU, o, (2, n), bias=b, aux=p), o)
+            us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS_SILU, o, (2, n), bias=b, aux=p if AUX else None), o)
         else:
             o = torch.empty((2, M, n), dtype=torch.float32, device=dev)
             us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS, o, (2, n), bias=b), o)
