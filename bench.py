@@ -593,7 +593,7 @@ def main():
         achieved = env_bytes * args.envs / env_launch_s / 1e9
         traffic = None
         # HBM bytes of the env step from the committed PMC passes: the rollout-context launch (fused
-        # operand written) has its own file (tools/r04_final.sh)
+        # operand written) has its own file (tools/gpu_pass.sh, stage pmc)
         kind = ("fused_ppo_" if opnd_bytes else "fused_") if fused else ""
         tf = args.traffic_file or os.path.join(ROOT, "profiles", f"traffic_{kind}{args.envs}.json")
         if os.path.exists(tf):
@@ -665,7 +665,7 @@ def main():
         if gemm_launches:
             # the dominant kernel of the PPO / rollout modes: the trunk GEMMs (MFMA-bound)
             tfs = gemm_flops / gemm_s / 1e12
-            gtraffic = None  # HBM bytes per launch of the same launches (rocprofv3 PMC, tools/profile_round.sh)
+            gtraffic = None  # HBM bytes per launch of the same launches (rocprofv3 PMC, tools/gpu_pass.sh stage pmc)
             gf = os.path.join(ROOT, "profiles", f"traffic_gemm_{args.envs}.json")
             if os.path.exists(gf):
                 with open(gf) as f:

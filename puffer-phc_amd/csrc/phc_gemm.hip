@@ -383,6 +383,33 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
 #ifndef PHC_GEMM_DEFER
 #define PHC_GEMM_DEFER 1
 #endif
+// measurement aid (experiment i of profiles/r05_gemm_experiments.txt): 1 = apply SiLU to every A
+// fragment after its LDS read (f16 only), the cost a consumer pays when the producing forward GEMM
+// stores only the pre-activation.  Results are NOT the product's; never set in a shipped build.
+#ifndef PHC_GEMM_A_SILU
+#define PHC_GEMM_A_SILU 0
+#endif
+template <typename V8> __device__ __forceinline__ void silu_frag(V8 &f) {
+  if constexpr (PHC_GEMM_A_SILU && std::is_same<V8, h8>::value) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = (float)f[e];
+      f[e] = (_Float16)(x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950f * x)));
+    }
+  }
+}
+
+// tuning build: the extra 128 x 128 tile configurations selectable by PHC_GEMM_CFG=3 / 4
+#ifndef PHC_GEMM_TUNE_CFGS
+#define PHC_GEMM_TUNE_CFGS 0
+#endif
+
+// measurement build (experiment ii): the persistent grid overlaps each tile's epilogue with the DMA of
+// its next tile's first K-tile (forward epilogues; the grad epilogues keep their LDS-staged aux rows)
+#ifndef PHC_GEMM_OVL
+#define PHC_GEMM_OVL 0
+#endif
+
 template <typename V8, int NI> struct GemmFrags {
   V8 fa[2][2], fb[2][NI];
 };
@@ -420,10 +447,15 @@ __device__ __forceinline__ void gemm_step_defer(const char *__restrict__ rd, cha
   };
   auto load_a = [&](V8 *fa, int s, int p) {
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
+    for (int ii = 0; ii < 2; ++ii) {
       read_frag<BK>(ta, wm * TL::TM + (2 * p + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), fa[ii]);
+      silu_frag(fa[ii]);
+    }
   };
-  load_b(f.fb[0], 0);
+  // PHC_GEMM_PROBE 3 (measurement): B fragments read from LDS at the first K-step only — the main loop's cost
+  // without B's LDS traffic (the bound of a B operand loaded straight into registers)
+  const bool read_b = !(PHC_GEMM_PROBE == 3 && carry);
+  if (read_b) load_b(f.fb[0], 0);
   load_a(f.fa[0], 0, 0);
   if (carry) {  // the previous K-step's last group, behind this step's first reads
     __builtin_amdgcn_sched_barrier(0);
@@ -434,7 +466,7 @@ __device__ __forceinline__ void gemm_step_defer(const char *__restrict__ rd, cha
   for (int q = 0; q + 1 < NG; ++q) {  // group NG - 1 is left in f.fa[1] / f.fb[1] for the next call
     const int s = q / GP, p = q % GP;
     const int s1 = (q + 1) / GP, p1 = (q + 1) % GP;
-    if (s1 != s) load_b(f.fb[s1 & 1], s1);
+    if (s1 != s && read_b) load_b(f.fb[s1 & 1], s1);
     load_a(f.fa[(q + 1) & 1], s1, p1);
     if (SPLIT && issue && q == (SPLIT * NG / 8 < NG - 1 ? SPLIT * NG / 8 : NG - 2)) stage(next, wr, 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
@@ -592,10 +624,14 @@ __device__ __forceinline__ void ktile_8ph(const char *__restrict__ rd, char *__r
 // last K-step (into the operand buffer that step does not read and the 32 KB above the operand
 // buffers), those of pass 3 during pass 1; the image then takes four 64-KB passes.  The epilogue
 // reads aux from LDS instead of waiting on HBM round trips per row batch.
-template <int EPI, typename TL, typename OutT> struct EpStage {
+template <int EPI, typename TL, typename OutT, bool OVL = false> struct EpStage {
   static constexpr bool kOn = (EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD) && TL::BM == 256 && TL::BN == 256 &&
                               TL::STAGES == 2 && TL::BK == 64 && TL::kWaves == 8 && sizeof(OutT) == 2;
-  static constexpr int kPasses = kOn ? 4 : TL::kEpPasses;
+  // OVL (persistent grid, PHC_GEMM_OVL): the image takes only the last K-step's operand buffer, in
+  // passes of one buffer each, while the other receives the next tile's first K-tile
+  static constexpr bool kOvl = OVL && !kOn && TL::STAGES == 2;
+  static constexpr int kOvlPasses = (TL::BM * TL::BN * 4 + TL::kStageBytes - 1) / TL::kStageBytes;
+  static constexpr int kPasses = kOn ? 4 : (kOvl ? kOvlPasses : TL::kEpPasses);
   static constexpr int kSlotBytes = 64 * 256 * 2;  // one pass's aux rows: 64 x 256 half-precision values
   static constexpr int kLdsBytes = kOn ? TL::kOpBytes + kSlotBytes : TL::kLdsBytes;
   static_assert(!kOn || TL::kOpBytes + kSlotBytes <= 163840, "LDS");
@@ -604,12 +640,17 @@ template <int EPI, typename TL, typename OutT> struct EpStage {
 // One output tile: main loop + fused epilogue.  `wg` is the tile's linear index (n fastest within
 // an A panel, then m, then batch); smem holds the operand stages and, after the main loop, the
 // epilogue image.
-template <typename T, typename OutT, int EPI, typename TL>
-__device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, int wg) {
+template <typename T, typename OutT, int EPI, typename TL, bool OVL = false>
+__device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, int wg, int next_wg = -1, int buf0 = 0,
+                                               bool pre = false) {
   constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
   constexpr bool kGrad = EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD;  // aux read + column sums
   constexpr bool kBiasFwd = EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU || EPI == PHC_EPI_BIAS_RELU;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tid_ = threadIdx.x;
+  // the persistent loop calls this once per tile: an opaque thread index keeps the compiler from
+  // hoisting the per-thread epilogue addressing out of that loop (long-lived registers that spilled)
+  asm volatile("" : "+v"(tid_));
+  const int tid = tid_, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
   const int tn = wg % g.tiles_n;
   const int tm = (wg / g.tiles_n) % g.tiles_m;
@@ -618,8 +659,14 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   const int n0 = tn * BN;
   const char *A = g.a + bt * g.a_bs * 2;
   const char *B = g.b + bt * g.b_bs * 2;
-  using ES = EpStage<EPI, TL, OutT>;
+  using ES = EpStage<EPI, TL, OutT, OVL>;
   constexpr int EP = ES::kPasses, WR = TL::TM / EP;
+  // OVL: this tile's K-tile 0 sits in operand buffer buf0 (already issued when `pre`); K-step kt
+  // reads buffer (kt + buf0) & 1; the last K-step issues next_wg's K-tile 0 into the other one
+  if constexpr (!ES::kOvl) {
+    buf0 = 0;
+    pre = false;
+  }
   const int kt_last = (g.k / TL::BK - 1) & 1;  // the operand buffer the last K-step reads
   const bool stage_aux = ES::kOn && g.aux_half && g.tc % BN == 0 && g.n % BN == 0 && m0 + BM <= g.m;
   // aux slot s: the halves of the buffer the last K-step does not read, then the spare 32 KB
@@ -658,6 +705,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   const int n0_ = n0;
   auto stage = [&](int kt, char *st, int parts = 3) {  // parts: 1 = A tile, 2 = B tile, 4 / 8 = A halves
     if (PHC_GEMM_PROBE == 2 && kt > 0) return;
+    if (PHC_GEMM_PROBE == 3 && kt > 0) parts &= ~2;  // measurement: B staged once, its fragments kept
     const int64_t m0 = PHC_GEMM_PROBE == 1 ? 0 : m0_;
     const int n0 = PHC_GEMM_PROBE == 1 ? 0 : n0_;
     if (parts & 1) stage_tile<BM, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
@@ -694,7 +742,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   } else if constexpr (TL::STAGES == 2 && PHC_GEMM_DEFER) {
     using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
     GemmFrags<V8, NI> fr;
-    stage(0, smem);
+    if (!pre) stage(0, smem + buf0 * TL::kStageBytes);
     for (int kt = 0; kt < kt_n; ++kt) {
       dma_barrier();  // tile kt landed; buffer (kt+1)&1 is no longer read
       if (stage_aux && kt == kt_n - 1) {  // nothing else to stage: the epilogue's aux rows
@@ -702,8 +750,16 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
         stage_aux_pass(1, aux_slot(1));
         stage_aux_pass(2, aux_slot(2));
       }
-      gemm_step_defer<T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt + 1 < kt_n,
-                             kt > 0, stage, kt + 1, wave, lane, acc, fr);
+      if (ES::kOvl && next_wg >= 0 && kt == kt_n - 1) {  // the next tile's K-tile 0, behind the epilogue
+        const int ntn = next_wg % g.tiles_n, ntm = (next_wg / g.tiles_n) % g.tiles_m;
+        const int nbt = next_wg / (g.tiles_n * g.tiles_m);
+        char *st = smem + ((kt + 1 + buf0) & 1) * TL::kStageBytes;
+        stage_tile<BM, TL::kWaves, TL::BK>(g.a + nbt * g.a_bs * 2, g.lda, (int64_t)ntm * BM, g.m, 0, st, wave, lane);
+        stage_tile<BN, TL::kWaves, TL::BK>(g.b + nbt * g.b_bs * 2, g.ldb, ntn * BN, g.n, 0, st + BM * TL::BK * 2, wave,
+                                           lane);
+      }
+      gemm_step_defer<T, TL>(smem + ((kt + buf0) & 1) * TL::kStageBytes, smem + ((kt + 1 + buf0) & 1) * TL::kStageBytes,
+                             kt + 1 < kt_n, kt > 0, stage, kt + 1, wave, lane, acc, fr);
     }
     gemm_flush<T, TL>(acc, fr);
   } else if constexpr (TL::STAGES == 2) {
@@ -762,8 +818,9 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   constexpr int kColThreads = BN / VW, kRowGroups = TL::kThreads / kColThreads;
   constexpr int kEpRows = BM / EP, kEpMI = MI / EP, IT = kEpRows / kRowGroups;
   static_assert(MI % EP == 0 && kEpRows * BN * 4 <= TL::kOpBytes, "epilogue passes");
-  static_assert(!ES::kOn || kEpRows * BN * 4 <= TL::kStageBytes, "a staged-aux image pass fits one operand buffer");
-  float *ep = reinterpret_cast<float *>(smem + (stage_aux ? kt_last * TL::kStageBytes : 0));
+  static_assert(!(ES::kOn || ES::kOvl) || kEpRows * BN * 4 <= TL::kStageBytes, "an image pass fits one operand buffer");
+  float *ep = reinterpret_cast<float *>(
+      smem + (ES::kOvl ? ((kt_last + buf0) & 1) * TL::kStageBytes : stage_aux ? kt_last * TL::kStageBytes : 0));
   const int cv = (tid % kColThreads) * VW, rg = tid / kColThreads;
   const int gcol = n0 + cv;
   const bool vec = gcol + VW - 1 < g.n && g.tc % VW == 0;
@@ -1017,6 +1074,24 @@ __global__ __launch_bounds__(TL::kThreads) __attribute__((amdgpu_waves_per_eu(TL
   launch_clock_begin(g.clk);
   if constexpr (!PERSIST) {
     twin_gemm_tile<T, OutT, EPI, TL>(g, smem, xcd_first(nwg, orig % 8) + orig / 8);
+  } else if constexpr (PHC_GEMM_OVL && TL::STAGES == 2 && PHC_GEMM_DEFER) {
+    // the persistent loop with the next tile's K-tile 0 issued before this tile's epilogue
+    const int total = g.tiles_m * g.tiles_n * g.batch;
+    const int x = orig % 8, l = orig / 8;
+    const int kt_n = g.k / TL::BK;
+    int buf0 = 0;
+    bool pre = false;
+    for (int base = 0; base < total; base += nwg) {
+      const int cnt = total - base < nwg ? total - base : nwg;
+      if (l >= xcd_count(cnt, x)) break;  // later steps hand out no more tiles than this one
+      const int nb = base + nwg;
+      const int ncnt = total - nb < nwg ? total - nb : nwg;
+      const int next = nb < total && l < xcd_count(ncnt, x) ? nb + xcd_first(ncnt, x) + l : -1;
+      twin_gemm_tile<T, OutT, EPI, TL, true>(g, smem, base + xcd_first(cnt, x) + l, next, buf0, pre);
+      buf0 = (kt_n + buf0) & 1;
+      pre = next >= 0;
+      lds_barrier();  // the epilogue image is read out before the buffer is staged again
+    }
   } else {
     const int total = g.tiles_m * g.tiles_n * g.batch;
     const int x = orig % 8, l = orig / 8;
@@ -1305,7 +1380,11 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad_group(WgradGroupArgs ga)
 // tile configurations
 using Tile128x2 = Tile<128, 128, 2, 2, 2>;
 using Tile256sq = Tile<256, 256, 2, 4, 2>;
-enum { kCfg128 = 0, kCfg256sq = 2 };
+// tuning candidates for the rollout's 4096-row GEMMs (PHC_GEMM_CFG, f16 operands only): BK 32 with
+// 32 KB of operand stages and a 3-stage BK-32 pipeline, both at 3 waves per SIMD (3 workgroups per CU)
+using Tile128k32 = Tile<128, 128, 2, 2, 2, 32, 3>;
+using Tile128k32s3 = Tile<128, 128, 2, 2, 3, 32, 3>;
+enum { kCfg128 = 0, kCfg256sq = 2, kCfg128k32 = 3, kCfg128k32s3 = 4 };
 
 // 256 x 256 tiles when they still give every CU a tile (the rollout's 4096-row first layer), else
 // 128 x 128 (the other 4096-row rollout GEMMs: a half- or quarter-filled grid of 256 x 256 tiles is
@@ -1325,8 +1404,8 @@ static int gemm_config(int64_t m, int n, int batch) {
 }
 
 static void gemm_tile_dims(int cfg, int *bm, int *bn) {
-  *bm = cfg == kCfg128 ? 128 : 256;
-  *bn = cfg == kCfg128 ? 128 : 256;
+  *bm = cfg == kCfg256sq ? 256 : 128;
+  *bn = cfg == kCfg256sq ? 256 : 128;
 }
 
 static phc_kernel_timer *g_gemm_timer = nullptr;  // bench.py measurement aid (phc_gemm_set_timer)
@@ -1350,8 +1429,12 @@ static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
 
 template <typename T, typename OutT, int EPI>
 static void launch_cfg(int cfg, const GemmArgs &g, int64_t blocks, hipStream_t st) {
-  if (cfg == kCfg128) launch_one<T, OutT, EPI, Tile128x2>(g, blocks, st);
-  else launch_one<T, OutT, EPI, Tile256sq>(g, blocks, st);
+  if constexpr (std::is_same<T, _Float16>::value && std::is_same<OutT, _Float16>::value && PHC_GEMM_TUNE_CFGS) {
+    if (cfg == kCfg128k32) return launch_one<T, OutT, EPI, Tile128k32>(g, blocks, st);
+    if (cfg == kCfg128k32s3) return launch_one<T, OutT, EPI, Tile128k32s3>(g, blocks, st);
+  }
+  if (cfg == kCfg256sq) launch_one<T, OutT, EPI, Tile256sq>(g, blocks, st);
+  else launch_one<T, OutT, EPI, Tile128x2>(g, blocks, st);
 }
 
 template <typename T, typename OutT>

@@ -354,6 +354,9 @@ def test_block_rollout_follows_resample(monkeypatch):
     runs = []
     for block in (False, True):
         monkeypatch.setattr(core, "BLOCK_GRAPH", block)
+        torch.manual_seed(1)  # the initial load's crops / headings: the same library in both runs
+        random.seed(2)
+        np.random.seed(3)
         env = PHCPufferEnv(EnvConfig(num_envs=64, seed=8, log_interval=5, max_episode_length=40), motion_data=clips)
         torch.manual_seed(0)
         policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)

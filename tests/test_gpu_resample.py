@@ -42,7 +42,7 @@ def env():
     return e
 
 
-def _resample(env, pool, seeds=(5, 6, 7)):
+def _resample(henv, pool, seeds=(5, 6, 7)):
     from puffer_phc_amd import motion_lib as ML
 
     saved = ML.MOTION_POOL
@@ -53,7 +53,7 @@ def _resample(env, pool, seeds=(5, 6, 7)):
         np.random.seed(seeds[2])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        env.env.resample_motions()
+        henv.resample_motions()
         torch.cuda.synchronize()
         return time.perf_counter() - t0
     finally:

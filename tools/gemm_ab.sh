@@ -9,7 +9,7 @@ for r in $(seq 1 ${ROUNDS:-1}); do
   for v in ${VARIANTS}; do
     IFS=+ read -r so settings <<< "$v"
     tag=${v//[+=]/_}
-    env PHC_HIP_LIB=$ROOT/puffer-phc_amd/lib/$so ${settings//+/ } timeout -k 10 120 python tools/gemm_mb_probe.py \
+    env PHC_HIP_LIB=$ROOT/puffer-phc_amd/lib/$so ${settings//+/ } timeout -k 10 120 python tools/gemm_mb_probe.py ${PROBE_ARGS:-} \
       > "$OUT/gemm_${tag}_$r.log" 2>&1 || { tail -5 "$OUT/gemm_${tag}_$r.log"; exit 4; }
   done
 done

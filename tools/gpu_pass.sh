@@ -11,7 +11,14 @@
 #     env     bench --mode env at 4096 and 32768 envs, their kernel stats and HBM counters
 #     phys    the articulated-physics env bench
 #     amp     AMP + bf16 PPO kernel stats (BASELINE C5 on one GPU)
+#     timeline  host-side timeline + cProfile of PPO iterations (tools/host_timeline.py)
+#     hostgap   rocprofv3 kernel + HIP API trace: the host calls inside every GPU idle gap (tools/host_gaps.py)
+#     gemm      the per-minibatch GEMM probe over GEMM_VARIANTS (tools/gemm_ab.sh, GEMM_ROUNDS rounds)
+#     ab        bench lines over AB_VARIANTS (tools/bench_ab.sh, AB_ROUNDS rounds, AB_ARGS bench args)
 #     extra   EXTRA_CMD (a python command line, run under its own limit)
+# The round-2..4 per-pass drivers (tools/r0N_*.sh, profile_round.sh, gpu_check.sh, variants.sh, lib_ab.sh,
+# ppo_ab.sh, ab_time.sh, ...) named in older profiles/ notes are folded into these stages and into
+# gemm_ab.sh / bench_ab.sh (their text stays in the git history).
 # Every GPU step runs under its own time limit; the first failure ends the pass (nothing after a failed
 # or killed GPU step is started).
 set -u
@@ -22,7 +29,7 @@ fail() { echo "FAILED: $1"; tail -8 "$2"; exit 9; }
 stats() { cp "$(find "$1" -name '*kernel_stats.csv' | head -1)" "$2"; }
 
 if has tests; then
-  timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 240 --timeout-method thread \
+  timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -x -q ${PYTEST_ARGS:-} --timeout 240 --timeout-method thread \
     > "$O/pytest_gpu.log" 2>&1 || fail pytest "$O/pytest_gpu.log"
   tail -1 "$O/pytest_gpu.log"
 fi
@@ -82,6 +89,33 @@ if has amp; then
     || fail amp "$O/trace_ppo_amp_bf16.log"
   tail -1 "$O/trace_ppo_amp_bf16.log" | cut -c1-140
   stats "$O/trace_ppo_amp_bf16" "$O/ppo_4096_amp_bf16_kernel_stats.csv"
+fi
+if has timeline; then
+  timeout -k 10 300 python -u tools/host_timeline.py ${BENCH_ARGS:-} > "$O/host_timeline.txt" 2>&1 || fail timeline "$O/host_timeline.txt"
+  head -40 "$O/host_timeline.txt"
+fi
+if has hostgap; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --hip-trace -d "$O/trace_api" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --steps 4 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$O/trace_api.log" 2>&1 \
+    || fail hostgap "$O/trace_api.log"
+  python tools/host_gaps.py "$(find "$O/trace_api" -name '*kernel_trace.csv' | head -1)" \
+    "$(find "$O/trace_api" -name '*hip_api_trace.csv' | head -1)" 15 > "$O/host_gaps.txt" 2>&1 || true
+  head -30 "$O/host_gaps.txt"
+fi
+if has gemm; then
+  VARIANTS="${GEMM_VARIANTS:-libphc_hip.so}" ROUNDS=${GEMM_ROUNDS:-2} bash tools/gemm_ab.sh > "$O/gemm_ab.txt" 2>&1 \
+    || fail gemm "$O/gemm_ab.txt"
+  grep -E "^==|TOTAL" "$O/gemm_ab.txt"
+  if [ -n "${GEMM_ROLLOUT:-}" ]; then  # the rollout's 4096-row forward GEMMs per tile configuration
+    VARIANTS="$GEMM_ROLLOUT" ROUNDS=1 PROBE_ARGS=4096 WGRAD=0 bash tools/gemm_ab.sh > "$O/gemm_rollout.txt" 2>&1 \
+      || fail gemm_rollout "$O/gemm_rollout.txt"
+    grep -E "^==|fwd" "$O/gemm_rollout.txt"
+  fi
+fi
+if has ab; then
+  VARIANTS="${AB_VARIANTS:-libphc_hip.so}" ROUNDS=${AB_ROUNDS:-2} BENCH_ARGS="${AB_ARGS:-}" bash tools/bench_ab.sh \
+    > "$O/bench_ab.txt" 2>&1 || fail ab "$O/bench_ab.txt"
+  cat "$O/bench_ab.txt"
 fi
 if has extra; then
   timeout -k 10 "${EXTRA_LIMIT:-300}" python -u $EXTRA_CMD > "$O/extra.log" 2>&1 || fail extra "$O/extra.log"
