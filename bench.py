@@ -25,11 +25,13 @@ Roofline: with the replay physics the whole env phase is ONE launch, phc_env_ste
 (HBM-bound; R13 + the stand-in + the fused obs / reward / reset step): 11,714 algorithmic bytes per
 env-step (BYTES_PER_ENV_STEP_FUSED); with articulated physics the env step is phc_env_step,
 10,886 B (7,122 read + 3,764 written).  achieved = bytes x envs / average kernel
-time from HIP start/stop events recorded by each launch's own dispatch (hipExtLaunchKernel) for
-a uniform sample of the launches in the timed region: every ENV_TIMER_PERIOD-th env step and
-every GEMM_TIMER_PERIOD-th trunk GEMM (11, coprime to a minibatch's 13 GEMM launches, so every
-layer's launch is sampled in turn).  A timed dispatch leaves the stream idle for 5-10 us around
-it; timing every launch added ~2.5 ms to a 72 ms PPO iteration (rocprofv3 trace, round 3).  `traffic` = HBM bytes per launch from rocprofv3 PMC counters
+time, which the kernels stamp themselves (phc_timer_*: the first workgroup's start and the last
+workgroup's end from the 100 MHz constant clock, plain per-workgroup stores into a slot of the
+timer) for a uniform sample of the launches in the timed region: every ENV_TIMER_PERIOD-th env step
+and every GEMM_TIMER_PERIOD-th trunk GEMM, launches replayed from captured hipGraphs included (HIP
+events cannot be timed inside a graph on ROCm 7.2).  A stamped launch runs as fast as an untimed
+one; rocprofv3's duration of the same launch is ~3 us (env step) / ~1 % (GEMM) longer: it also counts
+the dispatch and the end-of-kernel release (profiles/r05_clock_vs_rocprof.json).  `traffic` = HBM bytes per launch from rocprofv3 PMC counters
 (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) read from profiles/traffic[_fused]_<envs>.json
 when present, else null.
 
@@ -68,6 +70,9 @@ DEFAULTS = {"env": (200, 20), "rollout": (64, 8), "ppo": (3, 1)}
 # launch exactly once per iteration)
 ENV_TIMER_PERIOD = 4
 GEMM_TIMER_PERIOD = 16
+KERNEL_TIMING_NOTE = ("in-kernel stamps (first workgroup start -> last workgroup end, s_memrealtime); rocprofv3 "
+                      "durations of the same launches run ~3 us (env) / ~1 % (GEMM) longer: dispatch + end-of-kernel "
+                      "release (profiles/r05_clock_vs_rocprof.json)")
 
 
 def parse():
@@ -432,30 +437,6 @@ class Runner:
         return {k: v / n for k, v in tot.items()}
 
 
-def dispatch_overhead_us(env, n=8):
-    """Per-launch dispatch + completion time of the env step that its in-kernel stamps do not see: HIP
-    events around n eager launches minus their stamped spans (after the timed region)."""
-    from puffer_phc_amd._native import KernelTimer
-
-    t = KernelTimer(capacity=2 * n)
-    prev, env.env.kernel_timer = env.env.kernel_timer, t
-    act = torch.zeros((env.num_agents, 69), device=env.actions.device)
-    evs = []
-    try:
-        for _ in range(n):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            env.step(act)
-            e1.record()
-            evs.append((e0, e1))
-        torch.cuda.synchronize()
-        stamped = t.total_ms() / max(t.count, 1)
-        evented = sum(a.elapsed_time(b) for a, b in evs) / n
-    finally:
-        env.env.kernel_timer = prev
-    return max(0.0, (evented - stamped) * 1e3)
-
-
 DP_FIELDS = ("mode", "backend", "allreduce_exposed_ms_per_minibatch_rank0",
              "allreduce_exposed_ms_per_minibatch_max_rank", "minibatches_timed", "grad_bytes_per_minibatch", "note")
 
@@ -553,9 +534,6 @@ def main():
     env_offered, gemm_offered = env.tick - tick0, _N.GEMM_LAUNCHES[0] - gemm_launch0
     kern_s = timer.total_ms() / max(env_steps, 1) * 1e-3
     env.env.kernel_timer = None
-    # the stamps span first workgroup start -> last workgroup end; HIP events / rocprofv3 also count the
-    # dispatch and completion of the launch: measured here on a few eager steps after the timed region
-    env_dispatch_us = dispatch_overhead_us(env)
     gemm_set_timer(None)
     gemm_launches, gemm_flops = gtimer.count, gtimer.work
     gemm_s = gtimer.total_ms() * 1e-3 if gemm_launches else 0.0
@@ -588,9 +566,7 @@ def main():
         opnd = getattr(env.env, "_obs_operand", None)
         opnd_bytes = int(opnd[0].shape[1] * opnd[0].element_size()) if opnd is not None else 0
         env_bytes += opnd_bytes
-        # the launch's duration as HIP events / rocprofv3 count it: the stamped span + the dispatch overhead
-        env_launch_s = kern_s + (env_dispatch_us or 0.0) * 1e-6
-        achieved = env_bytes * args.envs / env_launch_s / 1e9
+        achieved = env_bytes * args.envs / kern_s / 1e9 if kern_s > 0 else 0.0
         traffic = None
         # HBM bytes of the env step from the committed PMC passes: the rollout-context launch (fused
         # operand written) has its own file (tools/gpu_pass.sh, stage pmc)
@@ -659,8 +635,8 @@ def main():
                               "env phase)" if fused else "phc_env_step",
                     "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "kernel_us": env_launch_s * 1e6, "kernel_us_stamped": kern_s * 1e6,
-                    "dispatch_us": env_dispatch_us, "launches_timed": env_steps, "launches_in_region": env_offered,
+                    "kernel_us": kern_s * 1e6, "timing": KERNEL_TIMING_NOTE,
+                    "launches_timed": env_steps, "launches_in_region": env_offered,
                     "algorithmic_bytes_per_env_step": env_bytes, "obs_operand_bytes_per_env_step": opnd_bytes}
         if gemm_launches:
             # the dominant kernel of the PPO / rollout modes: the trunk GEMMs (MFMA-bound)
@@ -675,7 +651,7 @@ def main():
                                          "epilogues) + phc_weight_grad_group / phc_weight_grad (weight gradients)",
                                "achieved": tfs, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
                                "frac": tfs / MFMA_F16_PEAK_TFS, "traffic": gtraffic, "traffic_unit": "bytes",
-                               "kernel_us": gemm_s / gemm_launches * 1e6, "launches_timed": gemm_launches,
+                               "kernel_us": gemm_s / gemm_launches * 1e6, "timing": KERNEL_TIMING_NOTE, "launches_timed": gemm_launches,
                                "launches_in_region": gemm_offered,
                                "algorithmic_flops_per_launch": gemm_flops / gemm_launches}
             out["roofline_env_step"] = env_roof
