@@ -474,6 +474,73 @@ __device__ __forceinline__ void gemm_step_defer(const char *__restrict__ rd, cha
   }
 }
 
+// ---- K-steps with the B operand loaded straight into registers (PHC_GEMM_BDIRECT) --------------
+// The B tile's LDS traffic (its LDS-DMA and every wave's fragment reads: a third of the LDS bytes of a
+// K-step) bounds the LDS-staged loop (profiles/r05_gemm_experiments.txt §5: without it the main loop
+// is 7 % shorter).  Here each wave loads its own B fragments from global memory (L2): B is [n][k]
+// with k contiguous, so one 16-B load per lane is exactly an MFMA fragment (8 consecutive k of one
+// column).  Sub-step 1's fragments are issued right after the deferred group frees their registers,
+// the next K-step's sub-step-0 fragments once sub-step 0's MFMAs have been issued; the K-step barrier's
+// vmcnt(0) retires the latter with the next A tile.  The LDS layout is unchanged (B's region unused).
+#ifndef PHC_GEMM_BDIRECT
+#define PHC_GEMM_BDIRECT 0
+#endif
+// The B fragment loads are inline asm: the compiler's wait insertion then never sees a VGPR load mixed
+// with the LDS-DMA on the vmcnt counter (mixed event kinds made it wait vmcnt(0) before sub-step 1,
+// exposing the next K-step's loads); every use is ordered behind vm_wait_frags, a counted wait that
+// names the fragment registers as operands, so no use or copy of them can be scheduled above it.
+template <typename V8> __device__ __forceinline__ void gload_frag(V8 &r, const char *p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+}
+template <int N, typename V8> __device__ __forceinline__ void vm_wait_frags(V8 (&f)[4]) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "n"(N) : "memory");
+}
+
+template <bool ISSUE, typename T, typename TL, typename Stage, typename LoadB, typename V8>
+__device__ __forceinline__ void gemm_step_bdir(const char *__restrict__ rd, char *__restrict__ wr, bool carry,
+                                               const Stage &stage, const LoadB &load_b, int kt, int wave, int lane,
+                                               f4 (&acc)[TL::MI][TL::NI], GemmFrags<V8, TL::NI> &f) {
+  constexpr bool issue = ISSUE;  // a template constant: no branch around the loads, so the compiler's
+                                 // wait counting stays exact (a merge of paths forced vmcnt(0))
+  constexpr int MI = TL::MI, NI = TL::NI, BK = TL::BK;
+  const int wm = wave / TL::WGN;
+  constexpr int GP = MI / 2, NS = BK / 32, NG = NS * GP;
+  static_assert(NS == 2 && NG % 2 == 0, "two 32-deep sub-steps per K-step");
+  const char *ta = rd;
+  auto load_a = [&](V8 *fa, int s, int p) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+      read_frag<BK>(ta, wm * TL::TM + (2 * p + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), fa[ii]);
+  };
+  load_a(f.fa[0], 0, 0);
+  if (carry) {  // the previous K-step's last group (f.fb[1]: its sub-step 1)
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_group<T, V8, NI>(f.fa[1], f.fb[1], acc[MI - 2], acc[MI - 1]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  static_assert(NI == 4, "vm_wait_frags names four fragments");
+  __builtin_amdgcn_sched_barrier(0);
+  load_b(f.fb[1], kt, 1);  // this K-step's sub-step 1
+  // the next A tile's DMA after those loads (loads retire in order): waiting for sub-step 1's B
+  // fragments leaves the DMA (and the next K-step's B loads) in flight
+  if (issue) stage(kt + 1, wr, 1);
+  constexpr int kLoadsA = TL::BM * TL::BK * 2 / 16 / TL::kThreads;  // A-tile DMA instructions per thread
+#pragma unroll
+  for (int q = 0; q + 1 < NG; ++q) {
+    const int s = q / GP, p = q % GP;
+    const int s1 = (q + 1) / GP, p1 = (q + 1) % GP;
+    load_a(f.fa[(q + 1) & 1], s1, p1);
+    if (q == GP) vm_wait_frags<issue ? kLoadsA + NI : 0>(f.fb[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_group<T, V8, NI>(f.fa[q & 1], f.fb[s], acc[2 * p], acc[2 * p + 1]);
+    if (q == GP - 1 && issue) {  // sub-step 0's MFMAs are issued: its registers take the next K-step's
+      __builtin_amdgcn_sched_barrier(0);
+      load_b(f.fb[0], kt + 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 template <typename T, typename TL, typename V8>
 __device__ __forceinline__ void gemm_flush(f4 (&acc)[TL::MI][TL::NI], GemmFrags<V8, TL::NI> &f) {
   mfma_group<T, V8, TL::NI>(f.fa[1], f.fb[1], acc[TL::MI - 2], acc[TL::MI - 1]);
@@ -739,6 +806,41 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
                        acc);
     }
     if (!second) phase_barrier();
+  } else if constexpr (PHC_GEMM_BDIRECT && TL::STAGES == 2 && PHC_GEMM_DEFER && BM == 256 && BN == 256 && TL::BK == 64) {
+    using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
+    GemmFrags<V8, NI> fr;
+    // lane's B rows: column n0 + wn * TN + j * 16 + (lane & 15), clamped inside B (out-of-range columns'
+    // results are never stored); k offset 8 * (lane >> 4) inside each 32-deep sub-step
+    const char *bl[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      int col = n0 + wn * TL::TN + j * 16 + (lane & 15);
+      col = col < g.n ? col : g.n - 1;
+      bl[j] = B + ((int64_t)col * g.ldb + 8 * (lane >> 4)) * 2;
+    }
+    auto load_b = [&](V8 *fb, int kt, int s) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) gload_frag(fb[j], bl[j] + (kt * TL::BK + s * 32) * 2);
+    };
+    stage(0, smem, 1);
+    load_b(fr.fb[0], 0, 0);
+    int kt = 0;
+    for (; kt + 1 < kt_n; ++kt) {
+      dma_barrier();  // A tile kt landed (and this K-step's sub-step-0 B fragments); buffer (kt+1)&1 is free
+      vm_wait_frags<0>(fr.fb[0]);  // (already retired by the barrier's wait: orders the uses behind it)
+      gemm_step_bdir<true, T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt > 0,
+                                  stage, load_b, kt, wave, lane, acc, fr);
+    }
+    dma_barrier();
+    vm_wait_frags<0>(fr.fb[0]);
+    if (stage_aux) {  // nothing else to stage: the epilogue's aux rows
+      stage_aux_pass(0, aux_slot(0));
+      stage_aux_pass(1, aux_slot(1));
+      stage_aux_pass(2, aux_slot(2));
+    }
+    gemm_step_bdir<false, T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt > 0,
+                                 stage, load_b, kt, wave, lane, acc, fr);
+    gemm_flush<T, TL>(acc, fr);
   } else if constexpr (TL::STAGES == 2 && PHC_GEMM_DEFER) {
     using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
     GemmFrags<V8, NI> fr;
