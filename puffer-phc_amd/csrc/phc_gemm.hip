@@ -383,33 +383,6 @@ __device__ __forceinline__ void gemm_step(const char *__restrict__ rd, char *__r
 #ifndef PHC_GEMM_DEFER
 #define PHC_GEMM_DEFER 1
 #endif
-// measurement aid (experiment i of profiles/r05_gemm_experiments.txt): 1 = apply SiLU to every A
-// fragment after its LDS read (f16 only), the cost a consumer pays when the producing forward GEMM
-// stores only the pre-activation.  Results are NOT the product's; never set in a shipped build.
-#ifndef PHC_GEMM_A_SILU
-#define PHC_GEMM_A_SILU 0
-#endif
-template <typename V8> __device__ __forceinline__ void silu_frag(V8 &f) {
-  if constexpr (PHC_GEMM_A_SILU && std::is_same<V8, h8>::value) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float x = (float)f[e];
-      f[e] = (_Float16)(x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950f * x)));
-    }
-  }
-}
-
-// tuning build: the extra 128 x 128 tile configurations selectable by PHC_GEMM_CFG=3 / 4
-#ifndef PHC_GEMM_TUNE_CFGS
-#define PHC_GEMM_TUNE_CFGS 0
-#endif
-
-// measurement build (experiment ii): the persistent grid overlaps each tile's epilogue with the DMA of
-// its next tile's first K-tile (forward epilogues; the grad epilogues keep their LDS-staged aux rows)
-#ifndef PHC_GEMM_OVL
-#define PHC_GEMM_OVL 0
-#endif
-
 template <typename V8, int NI> struct GemmFrags {
   V8 fa[2][2], fb[2][NI];
 };
@@ -449,7 +422,6 @@ __device__ __forceinline__ void gemm_step_defer(const char *__restrict__ rd, cha
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii) {
       read_frag<BK>(ta, wm * TL::TM + (2 * p + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), fa[ii]);
-      silu_frag(fa[ii]);
     }
   };
   // PHC_GEMM_PROBE 3 (measurement): B fragments read from LDS at the first K-step only — the main loop's cost
@@ -471,73 +443,6 @@ __device__ __forceinline__ void gemm_step_defer(const char *__restrict__ rd, cha
     if (SPLIT && issue && q == (SPLIT * NG / 8 < NG - 1 ? SPLIT * NG / 8 : NG - 2)) stage(next, wr, 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
     mfma_group<T, V8, NI>(f.fa[q & 1], f.fb[s & 1], acc[2 * p], acc[2 * p + 1]);
-  }
-}
-
-// ---- K-steps with the B operand loaded straight into registers (PHC_GEMM_BDIRECT) --------------
-// The B tile's LDS traffic (its LDS-DMA and every wave's fragment reads: a third of the LDS bytes of a
-// K-step) bounds the LDS-staged loop (profiles/r05_gemm_experiments.txt §5: without it the main loop
-// is 7 % shorter).  Here each wave loads its own B fragments from global memory (L2): B is [n][k]
-// with k contiguous, so one 16-B load per lane is exactly an MFMA fragment (8 consecutive k of one
-// column).  Sub-step 1's fragments are issued right after the deferred group frees their registers,
-// the next K-step's sub-step-0 fragments once sub-step 0's MFMAs have been issued; the K-step barrier's
-// vmcnt(0) retires the latter with the next A tile.  The LDS layout is unchanged (B's region unused).
-#ifndef PHC_GEMM_BDIRECT
-#define PHC_GEMM_BDIRECT 0
-#endif
-// The B fragment loads are inline asm: the compiler's wait insertion then never sees a VGPR load mixed
-// with the LDS-DMA on the vmcnt counter (mixed event kinds made it wait vmcnt(0) before sub-step 1,
-// exposing the next K-step's loads); every use is ordered behind vm_wait_frags, a counted wait that
-// names the fragment registers as operands, so no use or copy of them can be scheduled above it.
-template <typename V8> __device__ __forceinline__ void gload_frag(V8 &r, const char *p) {
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
-}
-template <int N, typename V8> __device__ __forceinline__ void vm_wait_frags(V8 (&f)[4]) {
-  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "n"(N) : "memory");
-}
-
-template <bool ISSUE, typename T, typename TL, typename Stage, typename LoadB, typename V8>
-__device__ __forceinline__ void gemm_step_bdir(const char *__restrict__ rd, char *__restrict__ wr, bool carry,
-                                               const Stage &stage, const LoadB &load_b, int kt, int wave, int lane,
-                                               f4 (&acc)[TL::MI][TL::NI], GemmFrags<V8, TL::NI> &f) {
-  constexpr bool issue = ISSUE;  // a template constant: no branch around the loads, so the compiler's
-                                 // wait counting stays exact (a merge of paths forced vmcnt(0))
-  constexpr int MI = TL::MI, NI = TL::NI, BK = TL::BK;
-  const int wm = wave / TL::WGN;
-  constexpr int GP = MI / 2, NS = BK / 32, NG = NS * GP;
-  static_assert(NS == 2 && NG % 2 == 0, "two 32-deep sub-steps per K-step");
-  const char *ta = rd;
-  auto load_a = [&](V8 *fa, int s, int p) {
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-      read_frag<BK>(ta, wm * TL::TM + (2 * p + ii) * 16 + (lane & 15), s * 4 + (lane >> 4), fa[ii]);
-  };
-  load_a(f.fa[0], 0, 0);
-  if (carry) {  // the previous K-step's last group (f.fb[1]: its sub-step 1)
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_group<T, V8, NI>(f.fa[1], f.fb[1], acc[MI - 2], acc[MI - 1]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  static_assert(NI == 4, "vm_wait_frags names four fragments");
-  __builtin_amdgcn_sched_barrier(0);
-  load_b(f.fb[1], kt, 1);  // this K-step's sub-step 1
-  // the next A tile's DMA after those loads (loads retire in order): waiting for sub-step 1's B
-  // fragments leaves the DMA (and the next K-step's B loads) in flight
-  if (issue) stage(kt + 1, wr, 1);
-  constexpr int kLoadsA = TL::BM * TL::BK * 2 / 16 / TL::kThreads;  // A-tile DMA instructions per thread
-#pragma unroll
-  for (int q = 0; q + 1 < NG; ++q) {
-    const int s = q / GP, p = q % GP;
-    const int s1 = (q + 1) / GP, p1 = (q + 1) % GP;
-    load_a(f.fa[(q + 1) & 1], s1, p1);
-    if (q == GP) vm_wait_frags<issue ? kLoadsA + NI : 0>(f.fb[1]);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_group<T, V8, NI>(f.fa[q & 1], f.fb[s], acc[2 * p], acc[2 * p + 1]);
-    if (q == GP - 1 && issue) {  // sub-step 0's MFMAs are issued: its registers take the next K-step's
-      __builtin_amdgcn_sched_barrier(0);
-      load_b(f.fb[0], kt + 1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
   }
 }
 
@@ -691,14 +596,10 @@ __device__ __forceinline__ void ktile_8ph(const char *__restrict__ rd, char *__r
 // last K-step (into the operand buffer that step does not read and the 32 KB above the operand
 // buffers), those of pass 3 during pass 1; the image then takes four 64-KB passes.  The epilogue
 // reads aux from LDS instead of waiting on HBM round trips per row batch.
-template <int EPI, typename TL, typename OutT, bool OVL = false> struct EpStage {
+template <int EPI, typename TL, typename OutT> struct EpStage {
   static constexpr bool kOn = (EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD) && TL::BM == 256 && TL::BN == 256 &&
                               TL::STAGES == 2 && TL::BK == 64 && TL::kWaves == 8 && sizeof(OutT) == 2;
-  // OVL (persistent grid, PHC_GEMM_OVL): the image takes only the last K-step's operand buffer, in
-  // passes of one buffer each, while the other receives the next tile's first K-tile
-  static constexpr bool kOvl = OVL && !kOn && TL::STAGES == 2;
-  static constexpr int kOvlPasses = (TL::BM * TL::BN * 4 + TL::kStageBytes - 1) / TL::kStageBytes;
-  static constexpr int kPasses = kOn ? 4 : (kOvl ? kOvlPasses : TL::kEpPasses);
+  static constexpr int kPasses = kOn ? 4 : TL::kEpPasses;
   static constexpr int kSlotBytes = 64 * 256 * 2;  // one pass's aux rows: 64 x 256 half-precision values
   static constexpr int kLdsBytes = kOn ? TL::kOpBytes + kSlotBytes : TL::kLdsBytes;
   static_assert(!kOn || TL::kOpBytes + kSlotBytes <= 163840, "LDS");
@@ -707,9 +608,8 @@ template <int EPI, typename TL, typename OutT, bool OVL = false> struct EpStage 
 // One output tile: main loop + fused epilogue.  `wg` is the tile's linear index (n fastest within
 // an A panel, then m, then batch); smem holds the operand stages and, after the main loop, the
 // epilogue image.
-template <typename T, typename OutT, int EPI, typename TL, bool OVL = false>
-__device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, int wg, int next_wg = -1, int buf0 = 0,
-                                               bool pre = false) {
+template <typename T, typename OutT, int EPI, typename TL>
+__device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, int wg) {
   constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
   constexpr bool kGrad = EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD;  // aux read + column sums
   constexpr bool kBiasFwd = EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU || EPI == PHC_EPI_BIAS_RELU;
@@ -726,14 +626,8 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   const int n0 = tn * BN;
   const char *A = g.a + bt * g.a_bs * 2;
   const char *B = g.b + bt * g.b_bs * 2;
-  using ES = EpStage<EPI, TL, OutT, OVL>;
+  using ES = EpStage<EPI, TL, OutT>;
   constexpr int EP = ES::kPasses, WR = TL::TM / EP;
-  // OVL: this tile's K-tile 0 sits in operand buffer buf0 (already issued when `pre`); K-step kt
-  // reads buffer (kt + buf0) & 1; the last K-step issues next_wg's K-tile 0 into the other one
-  if constexpr (!ES::kOvl) {
-    buf0 = 0;
-    pre = false;
-  }
   const int kt_last = (g.k / TL::BK - 1) & 1;  // the operand buffer the last K-step reads
   const bool stage_aux = ES::kOn && g.aux_half && g.tc % BN == 0 && g.n % BN == 0 && m0 + BM <= g.m;
   // aux slot s: the halves of the buffer the last K-step does not read, then the spare 32 KB
@@ -806,45 +700,10 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
                        acc);
     }
     if (!second) phase_barrier();
-  } else if constexpr (PHC_GEMM_BDIRECT && TL::STAGES == 2 && PHC_GEMM_DEFER && BM == 256 && BN == 256 && TL::BK == 64) {
-    using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
-    GemmFrags<V8, NI> fr;
-    // lane's B rows: column n0 + wn * TN + j * 16 + (lane & 15), clamped inside B (out-of-range columns'
-    // results are never stored); k offset 8 * (lane >> 4) inside each 32-deep sub-step
-    const char *bl[NI];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      int col = n0 + wn * TL::TN + j * 16 + (lane & 15);
-      col = col < g.n ? col : g.n - 1;
-      bl[j] = B + ((int64_t)col * g.ldb + 8 * (lane >> 4)) * 2;
-    }
-    auto load_b = [&](V8 *fb, int kt, int s) {
-#pragma unroll
-      for (int j = 0; j < NI; ++j) gload_frag(fb[j], bl[j] + (kt * TL::BK + s * 32) * 2);
-    };
-    stage(0, smem, 1);
-    load_b(fr.fb[0], 0, 0);
-    int kt = 0;
-    for (; kt + 1 < kt_n; ++kt) {
-      dma_barrier();  // A tile kt landed (and this K-step's sub-step-0 B fragments); buffer (kt+1)&1 is free
-      vm_wait_frags<0>(fr.fb[0]);  // (already retired by the barrier's wait: orders the uses behind it)
-      gemm_step_bdir<true, T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt > 0,
-                                  stage, load_b, kt, wave, lane, acc, fr);
-    }
-    dma_barrier();
-    vm_wait_frags<0>(fr.fb[0]);
-    if (stage_aux) {  // nothing else to stage: the epilogue's aux rows
-      stage_aux_pass(0, aux_slot(0));
-      stage_aux_pass(1, aux_slot(1));
-      stage_aux_pass(2, aux_slot(2));
-    }
-    gemm_step_bdir<false, T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt > 0,
-                                 stage, load_b, kt, wave, lane, acc, fr);
-    gemm_flush<T, TL>(acc, fr);
   } else if constexpr (TL::STAGES == 2 && PHC_GEMM_DEFER) {
     using V8 = typename std::conditional<std::is_same<T, _Float16>::value, h8, b8>::type;
     GemmFrags<V8, NI> fr;
-    if (!pre) stage(0, smem + buf0 * TL::kStageBytes);
+    stage(0, smem);
     for (int kt = 0; kt < kt_n; ++kt) {
       dma_barrier();  // tile kt landed; buffer (kt+1)&1 is no longer read
       if (stage_aux && kt == kt_n - 1) {  // nothing else to stage: the epilogue's aux rows
@@ -852,16 +711,8 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
         stage_aux_pass(1, aux_slot(1));
         stage_aux_pass(2, aux_slot(2));
       }
-      if (ES::kOvl && next_wg >= 0 && kt == kt_n - 1) {  // the next tile's K-tile 0, behind the epilogue
-        const int ntn = next_wg % g.tiles_n, ntm = (next_wg / g.tiles_n) % g.tiles_m;
-        const int nbt = next_wg / (g.tiles_n * g.tiles_m);
-        char *st = smem + ((kt + 1 + buf0) & 1) * TL::kStageBytes;
-        stage_tile<BM, TL::kWaves, TL::BK>(g.a + nbt * g.a_bs * 2, g.lda, (int64_t)ntm * BM, g.m, 0, st, wave, lane);
-        stage_tile<BN, TL::kWaves, TL::BK>(g.b + nbt * g.b_bs * 2, g.ldb, ntn * BN, g.n, 0, st + BM * TL::BK * 2, wave,
-                                           lane);
-      }
-      gemm_step_defer<T, TL>(smem + ((kt + buf0) & 1) * TL::kStageBytes, smem + ((kt + 1 + buf0) & 1) * TL::kStageBytes,
-                             kt + 1 < kt_n, kt > 0, stage, kt + 1, wave, lane, acc, fr);
+      gemm_step_defer<T, TL>(smem + (kt & 1) * TL::kStageBytes, smem + ((kt + 1) & 1) * TL::kStageBytes, kt + 1 < kt_n,
+                             kt > 0, stage, kt + 1, wave, lane, acc, fr);
     }
     gemm_flush<T, TL>(acc, fr);
   } else if constexpr (TL::STAGES == 2) {
@@ -920,9 +771,8 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   constexpr int kColThreads = BN / VW, kRowGroups = TL::kThreads / kColThreads;
   constexpr int kEpRows = BM / EP, kEpMI = MI / EP, IT = kEpRows / kRowGroups;
   static_assert(MI % EP == 0 && kEpRows * BN * 4 <= TL::kOpBytes, "epilogue passes");
-  static_assert(!(ES::kOn || ES::kOvl) || kEpRows * BN * 4 <= TL::kStageBytes, "an image pass fits one operand buffer");
-  float *ep = reinterpret_cast<float *>(
-      smem + (ES::kOvl ? ((kt_last + buf0) & 1) * TL::kStageBytes : stage_aux ? kt_last * TL::kStageBytes : 0));
+  static_assert(!ES::kOn || kEpRows * BN * 4 <= TL::kStageBytes, "a staged-aux image pass fits one operand buffer");
+  float *ep = reinterpret_cast<float *>(smem + (stage_aux ? kt_last * TL::kStageBytes : 0));
   const int cv = (tid % kColThreads) * VW, rg = tid / kColThreads;
   const int gcol = n0 + cv;
   const bool vec = gcol + VW - 1 < g.n && g.tc % VW == 0;
@@ -1176,24 +1026,6 @@ __global__ __launch_bounds__(TL::kThreads) __attribute__((amdgpu_waves_per_eu(TL
   launch_clock_begin(g.clk);
   if constexpr (!PERSIST) {
     twin_gemm_tile<T, OutT, EPI, TL>(g, smem, xcd_first(nwg, orig % 8) + orig / 8);
-  } else if constexpr (PHC_GEMM_OVL && TL::STAGES == 2 && PHC_GEMM_DEFER) {
-    // the persistent loop with the next tile's K-tile 0 issued before this tile's epilogue
-    const int total = g.tiles_m * g.tiles_n * g.batch;
-    const int x = orig % 8, l = orig / 8;
-    const int kt_n = g.k / TL::BK;
-    int buf0 = 0;
-    bool pre = false;
-    for (int base = 0; base < total; base += nwg) {
-      const int cnt = total - base < nwg ? total - base : nwg;
-      if (l >= xcd_count(cnt, x)) break;  // later steps hand out no more tiles than this one
-      const int nb = base + nwg;
-      const int ncnt = total - nb < nwg ? total - nb : nwg;
-      const int next = nb < total && l < xcd_count(ncnt, x) ? nb + xcd_first(ncnt, x) + l : -1;
-      twin_gemm_tile<T, OutT, EPI, TL, true>(g, smem, base + xcd_first(cnt, x) + l, next, buf0, pre);
-      buf0 = (kt_n + buf0) & 1;
-      pre = next >= 0;
-      lds_barrier();  // the epilogue image is read out before the buffer is staged again
-    }
   } else {
     const int total = g.tiles_m * g.tiles_n * g.batch;
     const int x = orig % 8, l = orig / 8;
@@ -1482,11 +1314,7 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad_group(WgradGroupArgs ga)
 // tile configurations
 using Tile128x2 = Tile<128, 128, 2, 2, 2>;
 using Tile256sq = Tile<256, 256, 2, 4, 2>;
-// tuning candidates for the rollout's 4096-row GEMMs (PHC_GEMM_CFG, f16 operands only): BK 32 with
-// 32 KB of operand stages and a 3-stage BK-32 pipeline, both at 3 waves per SIMD (3 workgroups per CU)
-using Tile128k32 = Tile<128, 128, 2, 2, 2, 32, 3>;
-using Tile128k32s3 = Tile<128, 128, 2, 2, 3, 32, 3>;
-enum { kCfg128 = 0, kCfg256sq = 2, kCfg128k32 = 3, kCfg128k32s3 = 4 };
+enum { kCfg128 = 0, kCfg256sq = 2 };
 
 // 256 x 256 tiles when they still give every CU a tile (the rollout's 4096-row first layer), else
 // 128 x 128 (the other 4096-row rollout GEMMs: a half- or quarter-filled grid of 256 x 256 tiles is
@@ -1531,10 +1359,6 @@ static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
 
 template <typename T, typename OutT, int EPI>
 static void launch_cfg(int cfg, const GemmArgs &g, int64_t blocks, hipStream_t st) {
-  if constexpr (std::is_same<T, _Float16>::value && std::is_same<OutT, _Float16>::value && PHC_GEMM_TUNE_CFGS) {
-    if (cfg == kCfg128k32) return launch_one<T, OutT, EPI, Tile128k32>(g, blocks, st);
-    if (cfg == kCfg128k32s3) return launch_one<T, OutT, EPI, Tile128k32s3>(g, blocks, st);
-  }
   if (cfg == kCfg256sq) launch_one<T, OutT, EPI, Tile256sq>(g, blocks, st);
   else launch_one<T, OutT, EPI, Tile128x2>(g, blocks, st);
 }

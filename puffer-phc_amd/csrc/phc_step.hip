@@ -605,6 +605,27 @@ __device__ __forceinline__ void operand_rows_out_wave(const EnvView &e, const fl
   }
 }
 
+// measurement build (PHC_ENV_PHASES=1, never shipped): lane 0 of every wave stamps the constant clock at
+// the phase boundaries of the staged replay step into g_env_phase[wave][8] (read by
+// phc_env_phase_copy; tools/env_phase_probe.py): 0 start, 1 scalars used, 2 frame rows in LDS,
+// 3 replay + reward done, 4 observation row written, 5 rows copied out, 6 stats flushed
+#ifndef PHC_ENV_PHASES
+#define PHC_ENV_PHASES 0
+#endif
+#if PHC_ENV_PHASES
+constexpr int kPhaseWaves = 1 << 15;
+__device__ unsigned long long g_env_phase[kPhaseWaves * 8];
+#define ENV_PHASE(k)                                                                                  \
+  do {                                                                                                \
+    const int gw_ = (int)((blockIdx.x * kBlock + threadIdx.x) >> 6);                                  \
+    if ((threadIdx.x & 63) == 0 && gw_ < kPhaseWaves) g_env_phase[gw_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define ENV_PHASE(k) \
+  do {               \
+  } while (0)
+#endif
+
 template <bool AUTO, bool REPLAY>
 __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
@@ -626,6 +647,7 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
 #endif
 
   launch_clock_begin(c.clk);
+  ENV_PHASE(0);
   const double st_prev = stats_prefetch(e);
   // kStage: R13 for the wave's envs first (elementwise over their contiguous [nv, 69] action span,
   // independent of everything else: its loads join the first memory round)
@@ -678,6 +700,10 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
   const float t1n = (float)(prog + 1) * c.dt + st + so;  // observation time unless the env resets
   const Blend bl0 = frame_blend(t, m);
   Blend bl1 = frame_blend(t1n, m);
+#if PHC_ENV_PHASES
+  if (bl0.f0 == -12345) e.rew[0] = 0.0f;  // a use of the scalars before the stamp
+  ENV_PHASE(1);
+#endif
 
   // one memory round for the sim record and all four reference rows (t and t+dt)
   BodyRec s;
@@ -698,6 +724,7 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
   if constexpr (kStage) {
     const int64_t fr[4] = {bl0.f0, bl0.f1, bl1.f0, bl1.f1};
     stage_frame_rows(l.frames, wreg, fr, threadIdx.x & 63);
+    ENV_PHASE(2);
     const float *rw = wreg + (g & 1) * (4 * kRowF) + b * kRec;
     rows0 = {load_body(rw), load_body(rw + kRowF)};
     rows1 = {load_body(rw + 2 * kRowF), load_body(rw + 3 * kRowF)};
@@ -746,6 +773,10 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
   }
 
   const Outcome o = env_reward(e, c, ei, lane, prog, t, m, s, ref0, pw_reg);
+#if PHC_ENV_PHASES
+  if (o.reset == 7) e.rew[0] = 0.0f;
+  ENV_PHASE(3);
+#endif
   double st_row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (valid && lane == 0) env_bookkeeping(e, ei, o, st_row);
 
@@ -793,6 +824,7 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
     // the wave writes out its envs' rows (LDS operations of one wave complete in order: the lanes'
     // row writes above are visible to the copy once their issue order is pinned)
     wave_lds_handoff();
+    ENV_PHASE(4);
     const int wl = threadIdx.x & 63;
     const int64_t env0 = (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6) * kWaveEnvs;
     const int64_t left = e.n - env0;
@@ -805,7 +837,9 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
         else operand_rows_out_wave<_Float16>(e, wreg, env0, nv, wl);
       }
     }
+    ENV_PHASE(5);
     if (e.stats) flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
+    ENV_PHASE(6);
     launch_clock_end(c.clk);
     return;
   }
@@ -887,6 +921,14 @@ static int check_env(const phc_env_buffers *e) {
 }  // namespace phc
 
 using namespace phc;
+
+#if PHC_ENV_PHASES
+extern "C" int phc_env_phase_copy(unsigned long long *dst, int64_t waves) {
+  const int64_t n = (waves < kPhaseWaves ? waves : kPhaseWaves) * 8;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_env_phase), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int64_t phc_stats_blocks(int64_t num_envs) { return num_envs <= 0 ? 0 : grid_envs(num_envs); }
 
