@@ -64,7 +64,7 @@ BYTES_PER_ENV_STEP = 10886  # phc_env_step (K1+K2) after a separ
 BYTES_PER_ENV_STEP_FUSED = 11714
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16 / bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
-DEFAULTS = {"env": (200, 20), "rollout": (64, 8), "ppo": (3, 1)}
+DEFAULTS = {"env": (200, 20), "rollout": (64, 8), "ppo": (10, 5)}  # ppo: the warmup covers every graph capture
 # kernel-timer sampling (module docstring): every 4th env-step / physics launch, every 16th trunk GEMM
 # (16 is coprime to a minibatch's 13 GEMM launches and divides an iteration's 16 x 13: each layer's
 # launch exactly once per iteration)

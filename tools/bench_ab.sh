@@ -3,7 +3,7 @@
 # per run, each under its own time limit.  A variant is a library file name under puffer-phc_amd/lib/,
 # optionally followed by +VAR=value settings for the run's environment (the same form as gemm_ab.sh):
 #   VARIANTS="libphc_hip.so libphc_hip.so+PHC_BLOCK_GRAPH=0 libphc_hip_x.so" ROUNDS=2 bash tools/bench_ab.sh
-#   BENCH_ARGS="--mode env --envs 32768" ...   (default: the PPO line, --steps ${STEPS:-5} --warmup 2)
+#   BENCH_ARGS="--mode env --envs 32768" ...   (default: the PPO line, --steps ${STEPS:-5} --warmup ${WARMUP:-5})
 # Prints value, ms per step and the dominant kernel's roofline fraction / time per run.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$ROOT"; OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
@@ -13,7 +13,7 @@ for r in $(seq 1 ${ROUNDS:-1}); do
     tag=${v//[+=]/_}
     log="$OUT/bench_${tag}_$r.log"
     env PHC_HIP_LIB=$ROOT/puffer-phc_amd/lib/$so ${settings//+/ } timeout -k 10 300 python bench.py \
-      --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$log" 2>&1 || { tail -5 "$log"; exit 4; }
+      --steps ${STEPS:-5} --warmup ${WARMUP:-5} --no-cpu-baseline ${BENCH_ARGS:-} > "$log" 2>&1 || { tail -5 "$log"; exit 4; }
     python - "$log" "$v" <<'EOF'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
