@@ -18,6 +18,7 @@
 //   of mu over one half of k in fp32, its W_mu row read as float4 straight from L2 (no staging
 //   barriers), the two halves added through LDS.
 #include "phc_common.h"
+#include "phc_x3.h"
 
 #include <cstdlib>
 
@@ -382,6 +383,209 @@ __global__ __launch_bounds__(kActThreads) void k_policy_act(phc_policy_act_args 
   }
 }
 
+// ------------------------------------------------------- policy_act, MFMA form --
+// 16 rows per 512-thread workgroup (256 workgroups at 4096 rows: one per CU).  LayerNorm + SiLU as
+// above (one (trunk, row) task per wave, 4 tasks per wave), the actor's h rows kept in LDS as fp32;
+// then the mu head on the bf16 MFMA with three-way operand splits (phc_x3.h: fp32-class products):
+// wave w takes the K slice [w H/8, (w + 1) H/8) of all 16 rows x 80 action columns (5 blocks of 16;
+// columns past A multiply zeros), its W_mu fragments (lane (g, c): action 16 nb + c, 8 consecutive
+// K) issued right after the trunk rows and LayerNorm parameters so they land during the LayerNorm,
+// and split in registers (no staging of W); the 8 K-slice partials are added through LDS in a fixed
+// order, then the Normal sample and log_prob as above.  Replaces the fp32-FMA head of k_policy_act
+// (per-thread LDS broadcast reads + W row loads): 4096 rows 18.8-21.3 us standalone vs 24.6-29.0,
+// 20.3-22.3 us vs 28.5 us inside the PPO rollout (tools/act_probe.py, profiles/r05r / r05s traces).
+// PHC_ACT_X3=0 selects k_policy_act.
+constexpr int kAx3Rows = 16, kAx3Waves = 8, kAx3Threads = kAx3Waves * 64, kAx3NB = kActMaxA / 16 + 1;
+static_assert(kAx3NB * 16 >= kActMaxA, "action blocks cover every action");
+static_assert(2 * kAx3Rows % kAx3Waves == 0, "LayerNorm tasks split evenly over the waves");
+
+template <int C>
+__global__ __launch_bounds__(kAx3Threads) void k_policy_act_x3(phc_policy_act_args a) {
+  constexpr int H = C * 256, KW = H / kAx3Waves, KS = KW / 32, HP = H + 4, NB = kAx3NB;
+  // K steps whose W fragments load before the LayerNorm
+  constexpr int KPRE = C >= 3 ? 1 : (KS < 2 ? KS : 2);
+  constexpr int kTasks = 2 * kAx3Rows / kAx3Waves;
+  static_assert(KW % 32 == 0, "each wave's K slice is whole 32-deep MFMA steps");
+  __shared__ __attribute__((aligned(16))) float hs[kAx3Rows][HP];  // +4 floats: conflict-free A reads
+  __shared__ __attribute__((aligned(16))) float part[kAx3Waves][kAx3Rows][NB * 16];
+  __shared__ float lpt[kAx3Rows][kActMaxA];
+  __shared__ float red[kAx3Rows];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int64_t r0 = (int64_t)blockIdx.x * kAx3Rows;
+  const int A = a.num_actions;
+  const int kw0 = wave * KW;
+
+  // W_mu fragments: rows clamped to A - 1 (loads stay in bounds), zeroed past A after they land
+  const bool wvec = (reinterpret_cast<uintptr_t>(a.w_mu) & 15) == 0;  // uniform
+  auto load_w = [&](int s, float4 (&wf)[NB][2]) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int act = 16 * nb + c;
+      const float *wp = a.w_mu + (int64_t)(act < A ? act : A - 1) * H + kw0 + 32 * s + 8 * g;
+      if (wvec) {
+        wf[nb][0] = *reinterpret_cast<const float4 *>(wp);
+        wf[nb][1] = *reinterpret_cast<const float4 *>(wp + 4);
+      } else {
+        wf[nb][0] = float4{wp[0], wp[1], wp[2], wp[3]};
+        wf[nb][1] = float4{wp[4], wp[5], wp[6], wp[7]};
+      }
+    }
+  };
+
+  // load order = wait order (vmcnt counts in issue order): the trunk rows first, then the LayerNorm
+  // parameters of both trunks (a wave's tasks span both) and w_value, then what is needed only after
+  // the LayerNorm (W_mu fragments, the sampling inputs).
+  // LayerNorm + SiLU: task q = (trunk, row), q = wave + kAx3Waves t; rows past the end leave zeros
+  float x[kTasks][C][4];
+#pragma unroll
+  for (int t = 0; t < kTasks; ++t) {
+    const int q = wave + kAx3Waves * t;
+    const int grp = q / kAx3Rows;
+    const int64_t row = r0 + q % kAx3Rows;
+    if (row < a.rows) {
+      const float *src = a.trunk_out + ((int64_t)grp * a.rows + row) * H;
+#pragma unroll
+      for (int k = 0; k < C; ++k) {
+        const float4 v = *reinterpret_cast<const float4 *>(src + 4 * (lane + 64 * k));
+        x[t][k][0] = v.x; x[t][k][1] = v.y; x[t][k][2] = v.z; x[t][k][3] = v.w;
+      }
+    }
+  }
+  float gm[2][C][4], bt[2][C][4], wv[C][4];
+#pragma unroll
+  for (int k = 0; k < C; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = 4 * (lane + 64 * k) + e;  // parameter views may be 4-byte aligned only
+      gm[0][k][e] = a.ln_gamma[0][col];
+      gm[1][k][e] = a.ln_gamma[1][col];
+      bt[0][k][e] = a.ln_beta[0][col];
+      bt[1][k][e] = a.ln_beta[1][col];
+      wv[k][e] = a.w_value[col];
+    }
+  const float bv = a.b_value[0];
+  float4 wpre[KPRE][NB][2];
+#pragma unroll
+  for (int s = 0; s < KPRE; ++s) load_w(s, wpre[s]);
+  // the sampling phase's inputs: thread item u = (row, action) i = tid + kAx3Threads u
+  constexpr int kItems = (kAx3Rows * kActMaxA + kAx3Threads - 1) / kAx3Threads;
+  float nz[kItems], lsg[kItems], bmu[kItems];
+#pragma unroll
+  for (int u = 0; u < kItems; ++u) {
+    const int i = tid + kAx3Threads * u, rr = i / A, j = i - rr * A;
+    const int64_t row = r0 + rr;
+    const bool ok = i < kAx3Rows * A && row < a.rows;
+    nz[u] = ok ? a.noise[row * A + j] : 0.0f;
+    lsg[u] = ok ? a.log_sigma[j] : 0.0f;
+    bmu[u] = ok ? a.b_mu[j] : 0.0f;
+  }
+
+#pragma unroll
+  for (int t = 0; t < kTasks; ++t) {
+    const int q = wave + kAx3Waves * t;
+    const int grp = q / kAx3Rows, rr = q % kAx3Rows;  // grp: compile-time per t (kAx3Waves | kAx3Rows)
+    if (r0 + rr >= a.rows) {
+      if (grp == 0) {
+#pragma unroll
+        for (int k = 0; k < C; ++k) *reinterpret_cast<float4 *>(&hs[rr][4 * (lane + 64 * k)]) = float4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+      continue;
+    }
+    // ln_silu_row's arithmetic with the parameters in registers
+    float sm = 0.0f;
+#pragma unroll
+    for (int k = 0; k < C; ++k) sm += (x[t][k][0] + x[t][k][1]) + (x[t][k][2] + x[t][k][3]);
+    const float mean = wave_sum(sm) / (float)H;
+    float vr = 0.0f;
+#pragma unroll
+    for (int k = 0; k < C; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float dd = x[t][k][e] - mean;
+        vr += dd * dd;
+      }
+    const float rstd = rsqrtf(wave_sum(vr) / (float)H + a.ln_eps);
+#pragma unroll
+    for (int k = 0; k < C; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float ln = (x[t][k][e] - mean) * rstd * gm[grp][k][e] + bt[grp][k][e];
+        x[t][k][e] = ln / (1.0f + expf(-ln));
+      }
+    if (grp == 0) {
+#pragma unroll
+      for (int k = 0; k < C; ++k)
+        *reinterpret_cast<float4 *>(&hs[rr][4 * (lane + 64 * k)]) = float4{x[t][k][0], x[t][k][1], x[t][k][2], x[t][k][3]};
+    } else {
+      float sv = 0.0f;
+#pragma unroll
+      for (int k = 0; k < C; ++k)
+        sv += x[t][k][0] * wv[k][0] + x[t][k][1] * wv[k][1] + x[t][k][2] * wv[k][2] + x[t][k][3] * wv[k][3];
+      sv = wave_sum(sv);
+      if (lane == 0) red[rr] = sv + bv;
+    }
+  }
+  __syncthreads();
+
+  // mu partial over this wave's K slice: A = h rows (lane (g, c): row c, K 8 g .. + 7 of the step)
+  x3f4 acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = x3f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    float4 wl[NB][2];
+    if (s >= KPRE) load_w(s, wl);
+    const float4(&wf)[NB][2] = s < KPRE ? wpre[s < KPRE ? s : 0] : wl;
+    X3 xs, ws[NB];
+    const float *hp = &hs[c][kw0 + 32 * s + 8 * g];
+    split3(*reinterpret_cast<const float4 *>(hp), *reinterpret_cast<const float4 *>(hp + 4), xs);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const bool live = 16 * nb + c < A;
+      const float4 z4{0.0f, 0.0f, 0.0f, 0.0f};
+      split3(live ? wf[nb][0] : z4, live ? wf[nb][1] : z4, ws[nb]);
+    }
+    mma_x3_n<NB>(&xs, ws, acc, true);
+  }
+  // lane (g, c) holds rows 4 g + e of action column 16 nb + c
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[wave][4 * g + e][16 * nb + c] = acc[nb][e];
+  __syncthreads();
+
+  // the 8 partials in a fixed order, + b_mu; sample and the Normal's log_prob terms
+  const float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+#pragma unroll
+  for (int u = 0; u < kItems; ++u) {
+    const int i = tid + kAx3Threads * u;
+    if (i >= kAx3Rows * A) break;
+    const int rr = i / A, j = i - rr * A;
+    const int64_t row = r0 + rr;
+    float lp = 0.0f;
+    if (row < a.rows) {
+      const float s = ((part[0][rr][j] + part[1][rr][j]) + (part[2][rr][j] + part[3][rr][j])) +
+                      ((part[4][rr][j] + part[5][rr][j]) + (part[6][rr][j] + part[7][rr][j]));
+      const float mu = s + bmu[u];
+      float sd = expf(lsg[u]);
+      sd = sd > a.std_max ? a.std_max : sd;
+      const float act = mu + sd * nz[u];
+      const float d = act - mu;
+      lp = -(d * d) / (2.0f * (sd * sd)) - logf(sd) - kLogSqrt2Pi;
+      a.actions[row * A + j] = act;
+      if (a.mu) a.mu[row * A + j] = mu;
+    }
+    lpt[rr][j] = lp;
+  }
+  __syncthreads();
+  if (tid < kAx3Rows && r0 + tid < a.rows) {
+    float s = 0.0f;
+    for (int jj = 0; jj < A; ++jj) s += lpt[tid][jj];
+    a.logprob[r0 + tid] = s;
+    a.value[r0 + tid] = red[tid];
+  }
+}
+
 }  // namespace phc
 
 using namespace phc;
@@ -450,8 +654,22 @@ extern "C" int phc_policy_act(const phc_policy_act_args *args, void *stream) {
                             (reinterpret_cast<uintptr_t>(a.w_mu_t) & 15) == 0),
               "policy_act: w_mu_t must be 16-byte aligned with ld_w_mu_t >= num_actions, ld_w_mu_t %% 4 == 0");
   if (a.rows == 0) return PHC_OK;
-  const dim3 grid((unsigned)((a.rows + kActRows - 1) / kActRows));
   hipStream_t st = as_stream(stream);
+  static const bool x3 = [] {  // A/B aid: PHC_ACT_X3=0 selects the fp32-FMA head (k_policy_act)
+    const char *e = getenv("PHC_ACT_X3");
+    return !(e && atoi(e) == 0);
+  }();
+  if (x3) {
+    const dim3 gx((unsigned)((a.rows + kAx3Rows - 1) / kAx3Rows));
+    switch (a.hidden / 256) {
+      case 1: hipLaunchKernelGGL(k_policy_act_x3<1>, gx, dim3(kAx3Threads), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(k_policy_act_x3<2>, gx, dim3(kAx3Threads), 0, st, a); break;
+      case 3: hipLaunchKernelGGL(k_policy_act_x3<3>, gx, dim3(kAx3Threads), 0, st, a); break;
+      default: hipLaunchKernelGGL(k_policy_act_x3<4>, gx, dim3(kAx3Threads), 0, st, a); break;
+    }
+    return check_launch("policy_act");
+  }
+  const dim3 grid((unsigned)((a.rows + kActRows - 1) / kActRows));
   switch (a.hidden / 256) {
     case 1: hipLaunchKernelGGL(k_policy_act<1>, grid, dim3(kActThreads), 0, st, a); break;
     case 2: hipLaunchKernelGGL(k_policy_act<2>, grid, dim3(kActThreads), 0, st, a); break;
@@ -460,3 +678,4 @@ extern "C" int phc_policy_act(const phc_policy_act_args *args, void *stream) {
   }
   return check_launch("policy_act");
 }
+
