@@ -172,6 +172,23 @@ __device__ __forceinline__ void dma_barrier() {
   }
 }
 
+// Wave-specialised persistent tiles (PHC_GEMM_WS): waves 0-3 issue every operand DMA, waves 4-7 every
+// epilogue store, so no wave's vmcnt holds both.  A DMA wave waits for its DMA (vmcnt 0) before the
+// K-step barrier; a store wave waits only for its LDS reads (lgkmcnt 0): the previous tile's
+// epilogue stores keep draining while the next tile's main loop runs (with one counter for loads and
+// stores, a wave that had issued both would have to wait for its stores at the first K-step).
+// `dma_wave` must be wave-uniform in an SGPR (readfirstlane): s_waitcnt ignores the exec mask.
+#ifndef PHC_GEMM_WS
+#define PHC_GEMM_WS 1
+#endif
+__device__ __forceinline__ void ws_barrier(bool dma_wave) {
+  asm volatile("" ::: "memory");
+  if (dma_wave) __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+  else __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0) only (vmcnt 63, expcnt 7)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <typename OutT> __device__ __forceinline__ void gemm_store(void *p, int64_t off, float v) {
   static_cast<OutT *>(p)[off] = (OutT)v;
 }
@@ -250,6 +267,32 @@ __device__ __forceinline__ void stage_tile(const char *base, int64_t ld, int64_t
     const char *src = base + (gr * ld + k0 + (c << 3)) * 2;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                      (lds_void *)(lds_tile + q0 * 16), 16, 0, 0);
+  }
+}
+
+// stage_tile for the wave-specialised tiles: the 4 DMA waves issue a whole R x 64 operand tile
+// (R / 32 wave-instructions each).  Lane l of DMA wave w fills LDS rows w * 8 + (l >> 3) + 32 i; its
+// chunk (l & 7) ^ (row & 7) does not depend on i, so one per-lane byte pointer per operand and tile
+// (`lane_src`) plus wave-uniform offsets (k0, 32 i rows: SGPRs) address every instruction, and the
+// LDS destination (M0) is scalar: the generic form's per-instruction row / pointer registers spilled
+// once the DMA waves carried twice the instructions.  Rows are not clamped: whole tiles only.
+struct WsSrc {
+  const char *p;     // this lane's source byte pointer at k0 = 0, instruction 0
+  int64_t row_step;  // bytes between the rows of instruction i and i + 1 (32 rows)
+};
+__device__ __forceinline__ WsSrc ws_src(const char *base, int64_t ld, int64_t row0, int wsg, int lane) {
+  const int rl = wsg * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ ((lane >> 3) & 7);
+  return {base + ((row0 + rl) * ld + (c << 3)) * 2, 32 * ld * 2};
+}
+template <int R>
+__device__ __forceinline__ void stage_tile_ws(const WsSrc &src, int k0, char *lds_tile, int wsg) {
+  constexpr int kInstr = R * 64 / 512 / 4;  // per DMA wave
+#pragma unroll
+  for (int i = 0; i < kInstr; ++i) {
+    const char *a = src.p + (int64_t)k0 * 2 + (int64_t)i * src.row_step;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)a,
+                                     (lds_void *)(lds_tile + (i * 4 + wsg) * 64 * 16), 16, 0, 0);
   }
 }
 
@@ -596,20 +639,35 @@ __device__ __forceinline__ void ktile_8ph(const char *__restrict__ rd, char *__r
 // last K-step (into the operand buffer that step does not read and the 32 KB above the operand
 // buffers), those of pass 3 during pass 1; the image then takes four 64-KB passes.  The epilogue
 // reads aux from LDS instead of waiting on HBM round trips per row batch.
+// the persistent tile loop's forward (store-only) epilogues on 256 x 256 tiles run wave-specialised;
+// the tile's bias row is staged by the DMA waves into LDS past the operand buffers (kWsBiasBytes), so
+// the store waves issue no global load at all (a load's wait would also wait for their stores)
+template <int EPI, typename TL>
+constexpr bool kWsTile = PHC_GEMM_WS && TL::BM == 256 && TL::BN == 256 && TL::kWaves == 8 && TL::STAGES == 2 &&
+                         PHC_GEMM_DEFER && !PHC_GEMM_8PH && !(EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD);
+
+constexpr int kWsBiasBytes = 1024;  // 256 fp32 bias values
+
 template <int EPI, typename TL, typename OutT> struct EpStage {
   static constexpr bool kOn = (EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD) && TL::BM == 256 && TL::BN == 256 &&
                               TL::STAGES == 2 && TL::BK == 64 && TL::kWaves == 8 && sizeof(OutT) == 2;
   static constexpr int kPasses = kOn ? 4 : TL::kEpPasses;
   static constexpr int kSlotBytes = 64 * 256 * 2;  // one pass's aux rows: 64 x 256 half-precision values
-  static constexpr int kLdsBytes = kOn ? TL::kOpBytes + kSlotBytes : TL::kLdsBytes;
+  static constexpr int kLdsBytes = kOn ? TL::kOpBytes + kSlotBytes : TL::kLdsBytes + (kWsTile<EPI, TL> ? kWsBiasBytes : 0);
   static_assert(!kOn || TL::kOpBytes + kSlotBytes <= 163840, "LDS");
 };
 
 // One output tile: main loop + fused epilogue.  `wg` is the tile's linear index (n fastest within
 // an A panel, then m, then batch); smem holds the operand stages and, after the main loop, the
 // epilogue image.
-template <typename T, typename OutT, int EPI, typename TL>
+// ROLE (wave-specialised persistent tiles, kWsTile): 0 = every wave does everything; 1 = the DMA
+// waves' copy (operand DMA, main loop, image writes); 2 = the store waves' copy (main loop, image
+// writes, image reads + global stores).  Separate instantiations, so the compiler's wait insertion
+// for each role sees only its own memory operations (in one shared body it put vmcnt(0) waits meant
+// for the DMA into the store waves' path as well).
+template <typename T, typename OutT, int EPI, typename TL, int ROLE = 0>
 __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, int wg) {
+  constexpr bool WS = ROLE != 0;
   constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
   constexpr bool kGrad = EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD;  // aux read + column sums
   constexpr bool kBiasFwd = EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU || EPI == PHC_EPI_BIAS_RELU;
@@ -619,6 +677,12 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   asm volatile("" : "+v"(tid_));
   const int tid = tid_, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / TL::WGN, wn = wave % TL::WGN;
+  static_assert(!WS || (TL::kWaves == 8 && TL::STAGES == 2 && PHC_GEMM_DEFER && !PHC_GEMM_8PH &&
+                        !(EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD)),
+                "wave specialisation: 8-wave, 2-stage deferred main loop, store-only epilogues");
+  const int wsg = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform (SGPR)
+  constexpr bool dma_wave = ROLE != 2;
+  constexpr int kDW = WS ? TL::kWaves / 2 : TL::kWaves;  // waves issuing the operand DMA
   const int tn = wg % g.tiles_n;
   const int tm = (wg / g.tiles_n) % g.tiles_m;
   const int bt = wg / (g.tiles_n * g.tiles_m);
@@ -664,16 +728,38 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   const int kt_n = g.k / TL::BK;
   const int64_t m0_ = m0;
   const int n0_ = n0;
+  // WS: whole tiles stage through per-lane pointers (stage_tile_ws); ragged ones (never in the PPO
+  // minibatch) through the clamped generic path
+  const bool ws_full = WS && m0 + BM <= g.m && n0 + BN <= g.n;
+  const WsSrc ws_a = ws_src(A, g.lda, m0, wsg, lane), ws_b = ws_src(B, g.ldb, n0, wsg, lane);
+  if constexpr (ROLE == 1) {
+    if (g.bias && (EPI == PHC_EPI_BIAS || EPI == PHC_EPI_BIAS_SILU || EPI == PHC_EPI_BIAS_RELU)) {
+      // the tile's 256 bias values (4-B granules: a bias view may be 4-byte aligned only), wave w
+      // values 64 w .. 64 w + 63; landed by the first K-step's vmcnt(0) + barrier
+      int c = n0 + wsg * 64 + lane;
+      c = c < g.n ? c : g.n - 1;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(g.bias + bt * g.n + c),
+                                       (lds_void *)(smem + TL::kOpBytes + wsg * 256), 4, 0, 0);
+    }
+  }
   auto stage = [&](int kt, char *st, int parts = 3) {  // parts: 1 = A tile, 2 = B tile, 4 / 8 = A halves
     if (PHC_GEMM_PROBE == 2 && kt > 0) return;
     if (PHC_GEMM_PROBE == 3 && kt > 0) parts &= ~2;  // measurement: B staged once, its fragments kept
+    if (WS && !dma_wave) return;                     // the store waves issue no DMA
+    if constexpr (WS && PHC_GEMM_PROBE == 0) {
+      if (ws_full) {
+        if (parts & 1) stage_tile_ws<BM>(ws_a, kt * TL::BK, st, wsg);
+        if (parts & 2) stage_tile_ws<BN>(ws_b, kt * TL::BK, st + BM * TL::BK * 2, wsg);
+        return;
+      }
+    }
     const int64_t m0 = PHC_GEMM_PROBE == 1 ? 0 : m0_;
     const int n0 = PHC_GEMM_PROBE == 1 ? 0 : n0_;
-    if (parts & 1) stage_tile<BM, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
-    if (parts & 4) stage_tile<BM / 2, TL::kWaves, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
+    if (parts & 1) stage_tile<BM, kDW, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
+    if (parts & 4) stage_tile<BM / 2, kDW, TL::BK>(A, g.lda, m0, g.m, kt * TL::BK, st, wave, lane);
     if (parts & 8)
-      stage_tile<BM / 2, TL::kWaves, TL::BK>(A, g.lda, m0 + BM / 2, g.m, kt * TL::BK, st + BM / 2 * TL::BK * 2, wave, lane);
-    if (parts & 2) stage_tile<BN, TL::kWaves, TL::BK>(B, g.ldb, n0, g.n, kt * TL::BK, st + BM * TL::BK * 2, wave, lane);
+      stage_tile<BM / 2, kDW, TL::BK>(A, g.lda, m0 + BM / 2, g.m, kt * TL::BK, st + BM / 2 * TL::BK * 2, wave, lane);
+    if (parts & 2) stage_tile<BN, kDW, TL::BK>(B, g.ldb, n0, g.n, kt * TL::BK, st + BM * TL::BK * 2, wave, lane);
   };
   if constexpr (PHC_GEMM_8PH && BM == 256 && BN == 256 && TL::kWaves == 8 && TL::STAGES == 2 && TL::BK == 64 &&
                 TL::WGM == 2 && TL::WGN == 4) {
@@ -705,7 +791,8 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
     GemmFrags<V8, NI> fr;
     stage(0, smem);
     for (int kt = 0; kt < kt_n; ++kt) {
-      dma_barrier();  // tile kt landed; buffer (kt+1)&1 is no longer read
+      if constexpr (WS) ws_barrier(dma_wave);  // tile kt landed (every DMA wave drained its own)
+      else dma_barrier();  // tile kt landed; buffer (kt+1)&1 is no longer read
       if (stage_aux && kt == kt_n - 1) {  // nothing else to stage: the epilogue's aux rows
         stage_aux_pass(0, aux_slot(0));
         stage_aux_pass(1, aux_slot(1));
@@ -768,12 +855,15 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
   // BN * sizeof(OutT) contiguous bytes per row.
   constexpr int VW = sizeof(OutT) == 2 ? PHC_GEMM_EPI_VW : 4;
   static_assert(VW == 4 || VW == 8, "4 or 8 columns per thread");
-  constexpr int kColThreads = BN / VW, kRowGroups = TL::kThreads / kColThreads;
+  // WS: only the store waves (the upper half of the workgroup) read the image and store
+  constexpr int kStThreads = WS ? TL::kThreads / 2 : TL::kThreads;
+  constexpr int kColThreads = BN / VW, kRowGroups = kStThreads / kColThreads;
   constexpr int kEpRows = BM / EP, kEpMI = MI / EP, IT = kEpRows / kRowGroups;
   static_assert(MI % EP == 0 && kEpRows * BN * 4 <= TL::kOpBytes, "epilogue passes");
   static_assert(!ES::kOn || kEpRows * BN * 4 <= TL::kStageBytes, "a staged-aux image pass fits one operand buffer");
   float *ep = reinterpret_cast<float *>(smem + (stage_aux ? kt_last * TL::kStageBytes : 0));
-  const int cv = (tid % kColThreads) * VW, rg = tid / kColThreads;
+  const int st_tid = WS ? tid - (TL::kThreads - kStThreads) : tid;  // store role index (WS: waves 4-7)
+  const int cv = (st_tid % kColThreads) * VW, rg = st_tid / kColThreads;
   const int gcol = n0 + cv;
   const bool vec = gcol + VW - 1 < g.n && g.tc % VW == 0;
   const bool full = vec && m0 + BM <= g.m;
@@ -783,7 +873,13 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
     biasv[q] = 0.0f;
     csum[q] = 0.0f;
   }
-  if (EPI != PHC_EPI_STORE && g.bias) {
+  if constexpr (ROLE == 2) {
+    if (EPI != PHC_EPI_STORE && g.bias) {
+      const float *bl = reinterpret_cast<const float *>(smem + TL::kOpBytes);
+#pragma unroll
+      for (int q = 0; q < VW; ++q) biasv[q] = bl[cv + q];  // columns past n: clamped copies, masked
+    }
+  } else if (ROLE == 0 && EPI != PHC_EPI_STORE && g.bias) {
 #pragma unroll
     for (int q = 0; q < VW; ++q)
       if (gcol + q < g.n) biasv[q] = g.bias[bt * g.n + gcol + q];
@@ -852,6 +948,7 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
       else if (pass == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * IT) : "memory");
     }
     lds_barrier();
+    if (WS && dma_wave) continue;  // the DMA waves only write the image
     const char *aux_lds = stage_aux ? aux_slot(pass == 3 ? 0 : pass) : nullptr;
     if (full) {
       // whole tile in range, VW whole columns per thread: offsets are base + row * stride, rows
@@ -1026,6 +1123,19 @@ __global__ __launch_bounds__(TL::kThreads) __attribute__((amdgpu_waves_per_eu(TL
   launch_clock_begin(g.clk);
   if constexpr (!PERSIST) {
     twin_gemm_tile<T, OutT, EPI, TL>(g, smem, xcd_first(nwg, orig % 8) + orig / 8);
+  } else if constexpr (kWsTile<EPI, TL>) {
+    // the same tile sequence in both role copies: their barriers pair up one for one
+    const int total = g.tiles_m * g.tiles_n * g.batch;
+    const int x = orig % 8, l = orig / 8;
+    auto walk = [&](auto role) {
+      for (int base = 0; base < total; base += nwg) {
+        const int cnt = total - base < nwg ? total - base : nwg;
+        if (l < xcd_count(cnt, x)) twin_gemm_tile<T, OutT, EPI, TL, decltype(role)::value>(g, smem, base + xcd_first(cnt, x) + l);
+        lds_barrier();  // the epilogue image is read out before the next tile's operands land
+      }
+    };
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < TL::kWaves / 2) walk(std::integral_constant<int, 1>{});
+    else walk(std::integral_constant<int, 2>{});
   } else {
     const int total = g.tiles_m * g.tiles_n * g.batch;
     const int x = orig % 8, l = orig / 8;
@@ -1463,6 +1573,19 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   PHC_REQUIRE(blocks < (1ll << 31), "twin_gemm: grid too large");
   PHC_REQUIRE(d->max_workgroups >= 0, "twin_gemm: max_workgroups must be >= 0");
   if (d->max_workgroups > 0 && d->max_workgroups < blocks) blocks = d->max_workgroups;
+  // forward (store-only) epilogues on 256 x 256 tiles with more tiles than CUs: one persistent
+  // workgroup per CU, wave-specialised (kWsTile), so each tile's epilogue stores drain under the
+  // next tile's main loop.  PHC_GEMM_WS_GRID=0 keeps one tile per workgroup (A/B aid).
+  static const bool ws_grid = [] {
+    const char *e = getenv("PHC_GEMM_WS_GRID");
+    return PHC_GEMM_WS && !(e && atoi(e) == 0);
+  }();
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  if (ws_grid && d->max_workgroups == 0 && cfg == kCfg256sq && !grad_epi && blocks > cus) blocks = cus;
   GemmArgs g{};
   g.a = static_cast<const char *>(d->a);
   g.b = static_cast<const char *>(d->b);
