@@ -8,7 +8,9 @@ usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <kernel_regex> <out.j
 kernel_regex "train_gemm" selects the launches bench.py's GEMM timer records (the PPO update's
 trunk GEMMs, launched outside the rollout graph): every k_wgrad* dispatch, and k_twin_gemm
 dispatches of the 256 x 256 configuration (512-thread workgroups) with more than 256 workgroups
-(the minibatch's 32768-row GEMMs; the rollout's 4096-row GEMMs have at most 256).
+or of the persistent instantiation (template flag `Lb1E`: the wave-specialised forward GEMMs run
+one workgroup per CU) — the minibatch's 32768-row GEMMs; the rollout's 4096-row GEMMs have at most
+256 workgroups and never run persistent.
 """
 import csv
 import json
@@ -22,7 +24,7 @@ def selected(r, kernel, grid="Grid_Size", wg="Workgroup_Size"):
         return re.search(kernel, name) is not None
     if "k_wgrad" in name:
         return True
-    return "k_twin_gemm" in name and int(r[wg]) == 512 and int(r[grid]) // 512 > 256
+    return "k_twin_gemm" in name and int(r[wg]) == 512 and (int(r[grid]) // 512 > 256 or "Lb1E" in name)
 
 
 def counter(d, kernel):
