@@ -12,6 +12,29 @@
 
 namespace phc {
 
+// The logistic sigmoid of the LayerNorm + SiLU tails (policy tail, PPO-minibatch tail, the module path's
+// twin LayerNorm): PHC_FAST_SILU = 1 evaluates it from the hardware exp2 / reciprocal (1-ulp class, as the
+// trunk GEMMs' fused SiLU epilogues do); 0 = expf and an IEEE division (torch's formula, ~3x the VALU work
+// of these VALU-bound kernels).
+#ifndef PHC_FAST_SILU
+#define PHC_FAST_SILU 1
+#endif
+__device__ __forceinline__ float tail_sigmoid(float x) {
+#if PHC_FAST_SILU
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * 1.44269504088896341f));
+#else
+  return 1.0f / (1.0f + expf(-x));
+#endif
+}
+__device__ __forceinline__ float tail_silu(float x) {
+#if PHC_FAST_SILU
+  return x * tail_sigmoid(x);
+#else
+  return x / (1.0f + expf(-x));
+#endif
+}
+
+
 // thread-local message of the last failing call (phc_last_error)
 void set_error(const char *fmt, ...);
 int check_launch(const char *what);

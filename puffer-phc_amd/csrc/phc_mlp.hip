@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void k_ln_silu_fwd(const T *__restrict__ y, co
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float ln = (x[k][e] - mean) * rstd * gm[e] + bt[e];
-      o4[e] = ln / (1.0f + expf(-ln));
+      o4[e] = tail_silu(ln);
     }
     st4(z + row * n + c, o4);
   }
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void k_ln_silu_bwd(const T *__restrict__ y, co
         for (int e = 0; e < 4; ++e) {
           const float xh = (yv[h][k][e] - mr[h][0]) * mr[h][1];
           const float ln = xh * gm[k][e] + bt[k][e];
-          const float sg = 1.0f / (1.0f + expf(-ln));
+          const float sg = tail_sigmoid(ln);
           const float dln = dv[h][k][e] * sg * (1.0f + ln * (1.0f - sg));
           pg[k][e] += dln * xh;
           pb[k][e] += dln;

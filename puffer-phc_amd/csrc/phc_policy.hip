@@ -187,7 +187,7 @@ __device__ __forceinline__ void ln_silu_row(float x[C][4], const float *__restri
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float ln = (x[k][e] - mean) * rstd * g4[e] + b4[e];
-      x[k][e] = ln / (1.0f + expf(-ln));
+      x[k][e] = tail_silu(ln);
     }
   }
 }
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(kAx3Threads) void k_policy_act_x3(phc_policy_act_ar
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float ln = (x[t][k][e] - mean) * rstd * gm[grp][k][e] + bt[grp][k][e];
-        x[t][k][e] = ln / (1.0f + expf(-ln));
+        x[t][k][e] = tail_silu(ln);
       }
     if (grp == 0) {
 #pragma unroll

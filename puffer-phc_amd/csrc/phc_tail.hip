@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kFwdThreads) void k_tail_ln_fwd(phc_tail_ln_args a)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float ln = (x[t][k][e] - st.mean) * st.rstd * gm[k][e] + bt[k][e];
-        h[k][e] = ln / (1.0f + expf(-ln));
+        h[k][e] = tail_silu(ln);
       }
     if (grp == 0) {
 #pragma unroll
@@ -157,7 +157,7 @@ __device__ __forceinline__ void t_ln_bwd_row(const float x[kTC][4], const float 
     for (int e = 0; e < 4; ++e) {
       const float xv = (x[k][e] - st.mean) * st.rstd;
       const float ln = xv * gm[k][e] + bt[k][e];
-      const float sg = 1.0f / (1.0f + expf(-ln));
+      const float sg = tail_sigmoid(ln);
       float d = dh[k][e];
       if constexpr (CRITIC) {
         pwv[k][e] += dvalue * (ln * sg);
