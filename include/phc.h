@@ -351,9 +351,12 @@ int phc_act_bwd(const void *grad_out, int32_t grad_out_layout, const void *pre, 
  *             puffer_phc/policies/discriminator_policy.py:43-53)
  *   RELU_GRAD out = C * [aux + bias[c] > 0] (aux = the BIAS_RELU output, bias null: torch's
  *             threshold_backward reads the ReLU result), bias_grad as SILU_GRAD
+ *   BIAS_SILU_D  as BIAS_SILU, but aux = silu'(C + bias[c]) = s (1 + z (1 - s)), s = sigmoid(z): the
+ *             one thing the backward needs of the pre-activation z, in the same bytes (round 5)
+ *   DSILU_GRAD   out = C * aux (aux = BIAS_SILU_D's silu'; bias must be null), bias_grad as SILU_GRAD
  * out is fp32 or dtype (out_dtype). */
 enum { PHC_EPI_STORE = 0, PHC_EPI_BIAS = 1, PHC_EPI_BIAS_SILU = 2, PHC_EPI_SILU_GRAD = 3, PHC_EPI_BIAS_RELU = 4,
-       PHC_EPI_RELU_GRAD = 5 };
+       PHC_EPI_RELU_GRAD = 5, PHC_EPI_BIAS_SILU_D = 6, PHC_EPI_DSILU_GRAD = 7 };
 typedef struct phc_gemm_desc {
   const void *a;
   const void *b;

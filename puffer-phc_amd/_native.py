@@ -149,6 +149,8 @@ class GemmDescC(ctypes.Structure):
 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_SILU, EPI_SILU_GRAD, EPI_BIAS_RELU, EPI_RELU_GRAD = 0, 1, 2, 3, 4, 5
+# the silu'-aux pair (phc.h): the forward stores silu'(pre) instead of pre, the input gradient multiplies by it
+EPI_BIAS_SILU_D, EPI_DSILU_GRAD = 6, 7
 
 
 class WgradDescC(ctypes.Structure):

@@ -12,6 +12,10 @@
 //                       pre-activation, as BIAS_SILU writes it); bias_grad = column sums of out
 //   PHC_EPI_BIAS_RELU : out = relu(acc + bias)   (the AMP discriminator's Linear + ReLU,
 //                       policies/discriminator_policy.py:43-53)
+//   PHC_EPI_BIAS_SILU_D : BIAS_SILU with aux = silu'(pre) = s (1 + pre (1 - s)), s = sigmoid(pre)
+//                       (the only thing the backward needs of the pre-activation, in the same bytes)
+//   PHC_EPI_DSILU_GRAD: out = acc * aux (aux = BIAS_SILU_D's silu'(pre), bias null); bias_grad as below:
+//                       the input gradient's epilogue without the sigmoid (it was VALU-bound on it)
 //   PHC_EPI_RELU_GRAD : out = acc * [aux + bias > 0] (aux = the forward's ReLU output, bias null:
 //                       relu' from the output as torch's threshold_backward); bias_grad as above
 // so no fp32 GEMM output makes an HBM round trip through a separate elementwise kernel.
@@ -142,6 +146,12 @@ __device__ __forceinline__ float gemm_sigmoid(float a) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-a * 1.44269504088896341f));
 }
 __device__ __forceinline__ float gemm_silu(float a) { return a * gemm_sigmoid(a); }
+// y = silu(z) (gemm_silu's arithmetic) and d = silu'(z) = s (1 + z (1 - s)) from one sigmoid
+__device__ __forceinline__ void gemm_silu_d(float z, float &y, float &d) {
+  const float s = gemm_sigmoid(z);
+  y = z * s;
+  d = s * (1.0f + z * (1.0f - s));
+}
 
 // workgroup barrier for the epilogue's LDS hand-offs: waits for this wave's LDS operations only
 // (lgkmcnt), not for its global stores (vmcnt), so the stores of one
@@ -642,14 +652,21 @@ __device__ __forceinline__ void ktile_8ph(const char *__restrict__ rd, char *__r
 // the persistent tile loop's forward (store-only) epilogues on 256 x 256 tiles run wave-specialised;
 // the tile's bias row is staged by the DMA waves into LDS past the operand buffers (kWsBiasBytes), so
 // the store waves issue no global load at all (a load's wait would also wait for their stores)
+// the silu'-aux pair instantiates its own kernels (a run-time switch in the shared body spilled the
+// wave-specialised forward): the body sees the base epilogue plus kDeriv
+constexpr int epi_base(int e) {
+  return e == PHC_EPI_BIAS_SILU_D ? PHC_EPI_BIAS_SILU : (e == PHC_EPI_DSILU_GRAD ? PHC_EPI_SILU_GRAD : e);
+}
+
 template <int EPI, typename TL>
 constexpr bool kWsTile = PHC_GEMM_WS && TL::BM == 256 && TL::BN == 256 && TL::kWaves == 8 && TL::STAGES == 2 &&
-                         PHC_GEMM_DEFER && !PHC_GEMM_8PH && !(EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD);
+                         PHC_GEMM_DEFER && !PHC_GEMM_8PH &&
+                         !(epi_base(EPI) == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD);
 
 constexpr int kWsBiasBytes = 1024;  // 256 fp32 bias values
 
 template <int EPI, typename TL, typename OutT> struct EpStage {
-  static constexpr bool kOn = (EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD) && TL::BM == 256 && TL::BN == 256 &&
+  static constexpr bool kOn = (epi_base(EPI) == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD) && TL::BM == 256 && TL::BN == 256 &&
                               TL::STAGES == 2 && TL::BK == 64 && TL::kWaves == 8 && sizeof(OutT) == 2;
   static constexpr int kPasses = kOn ? 4 : TL::kEpPasses;
   static constexpr int kSlotBytes = 64 * 256 * 2;  // one pass's aux rows: 64 x 256 half-precision values
@@ -665,8 +682,10 @@ template <int EPI, typename TL, typename OutT> struct EpStage {
 // writes, image reads + global stores).  Separate instantiations, so the compiler's wait insertion
 // for each role sees only its own memory operations (in one shared body it put vmcnt(0) waits meant
 // for the DMA into the store waves' path as well).
-template <typename T, typename OutT, int EPI, typename TL, int ROLE = 0>
+template <typename T, typename OutT, int EPIX, typename TL, int ROLE = 0>
 __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, int wg) {
+  constexpr int EPI = epi_base(EPIX);
+  constexpr bool kDeriv = EPIX != EPI;  // BIAS_SILU_D / DSILU_GRAD: the aux is silu'(pre)
   constexpr bool WS = ROLE != 0;
   constexpr int BM = TL::BM, BN = TL::BN, MI = TL::MI, NI = TL::NI;
   constexpr bool kGrad = EPI == PHC_EPI_SILU_GRAD || EPI == PHC_EPI_RELU_GRAD;  // aux read + column sums
@@ -994,12 +1013,20 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
           float v[VW];
           read_image(r, v);
           if constexpr (EPI == PHC_EPI_SILU_GRAD) {
+            if constexpr (kDeriv) {  // aux = silu'(pre): one multiply
 #pragma unroll
-            for (int q = 0; q < VW; ++q) {
-              const float x = av[u][q] + biasv[q];
-              const float sg = gemm_sigmoid(x);
-              v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
-              csum[q] += v[q];
+              for (int q = 0; q < VW; ++q) {
+                v[q] = v[q] * av[u][q];
+                csum[q] += v[q];
+              }
+            } else {
+#pragma unroll
+              for (int q = 0; q < VW; ++q) {
+                const float x = av[u][q] + biasv[q];
+                const float sg = gemm_sigmoid(x);
+                v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
+                csum[q] += v[q];
+              }
             }
           } else if constexpr (EPI == PHC_EPI_RELU_GRAD) {
 #pragma unroll
@@ -1011,9 +1038,16 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
 #pragma unroll
             for (int q = 0; q < VW; ++q) v[q] += biasv[q];
             if constexpr (EPI == PHC_EPI_BIAS_SILU) {
-              if (g.aux && g.discard != 2) aux_store_v<T, VW>(g, ab + row * as, v);
+              if constexpr (kDeriv) {
+                float d[VW];
 #pragma unroll
-              for (int q = 0; q < VW; ++q) v[q] = gemm_silu(v[q]);
+                for (int q = 0; q < VW; ++q) gemm_silu_d(v[q], v[q], d[q]);
+                if (g.aux && g.discard != 2) aux_store_v<T, VW>(g, ab + row * as, d);
+              } else {
+                if (g.aux && g.discard != 2) aux_store_v<T, VW>(g, ab + row * as, v);
+#pragma unroll
+                for (int q = 0; q < VW; ++q) v[q] = gemm_silu(v[q]);
+              }
             } else if constexpr (EPI == PHC_EPI_BIAS_RELU) {
 #pragma unroll
               for (int q = 0; q < VW; ++q) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
@@ -1049,12 +1083,19 @@ __device__ __forceinline__ void twin_gemm_tile(const GemmArgs &g, char *smem, in
         if constexpr (kBiasFwd) {
           v[q] += biasv[q];
           a[q] = v[q];
-          if constexpr (EPI == PHC_EPI_BIAS_SILU) v[q] = gemm_silu(v[q]);
+          if constexpr (EPI == PHC_EPI_BIAS_SILU) {
+            if constexpr (kDeriv) gemm_silu_d(a[q], v[q], a[q]);
+            else v[q] = gemm_silu(v[q]);
+          }
           if constexpr (EPI == PHC_EPI_BIAS_RELU) v[q] = v[q] > 0.0f ? v[q] : 0.0f;
         } else if constexpr (EPI == PHC_EPI_SILU_GRAD) {
-          const float x = a[q] + biasv[q];
-          const float sg = gemm_sigmoid(x);
-          v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
+          if constexpr (kDeriv) {
+            v[q] = v[q] * a[q];
+          } else {
+            const float x = a[q] + biasv[q];
+            const float sg = gemm_sigmoid(x);
+            v[q] = v[q] * sg * (1.0f + x * (1.0f - sg));
+          }
           csum[q] += gcol + q < g.n ? v[q] : 0.0f;
         } else if constexpr (EPI == PHC_EPI_RELU_GRAD) {
           v[q] = a[q] + biasv[q] > 0.0f ? v[q] : 0.0f;
@@ -1481,6 +1522,8 @@ static void launch_epi(int epi, int cfg, const GemmArgs &g, int64_t blocks, hipS
     case PHC_EPI_BIAS_SILU: launch_cfg<T, OutT, PHC_EPI_BIAS_SILU>(cfg, g, blocks, st); break;
     case PHC_EPI_SILU_GRAD: launch_cfg<T, OutT, PHC_EPI_SILU_GRAD>(cfg, g, blocks, st); break;
     case PHC_EPI_BIAS_RELU: launch_cfg<T, OutT, PHC_EPI_BIAS_RELU>(cfg, g, blocks, st); break;
+    case PHC_EPI_BIAS_SILU_D: launch_cfg<T, OutT, PHC_EPI_BIAS_SILU_D>(cfg, g, blocks, st); break;
+    case PHC_EPI_DSILU_GRAD: launch_cfg<T, OutT, PHC_EPI_DSILU_GRAD>(cfg, g, blocks, st); break;
     default: launch_cfg<T, OutT, PHC_EPI_RELU_GRAD>(cfg, g, blocks, st); break;
   }
 }
@@ -1551,11 +1594,13 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
               "twin_gemm: operands must be 16-byte aligned");
   PHC_REQUIRE(d->dtype == PHC_DT_F16 || d->dtype == PHC_DT_BF16, "twin_gemm: operands must be f16 or bf16");
   PHC_REQUIRE(d->out_dtype == PHC_DT_F32 || d->out_dtype == d->dtype, "twin_gemm: out must be f32 or the operand type");
-  PHC_REQUIRE(d->epilogue >= PHC_EPI_STORE && d->epilogue <= PHC_EPI_RELU_GRAD, "twin_gemm: bad epilogue");
-  const bool grad_epi = d->epilogue == PHC_EPI_SILU_GRAD || d->epilogue == PHC_EPI_RELU_GRAD;
+  PHC_REQUIRE(d->epilogue >= PHC_EPI_STORE && d->epilogue <= PHC_EPI_DSILU_GRAD, "twin_gemm: bad epilogue");
+  const int epi = epi_base(d->epilogue);
+  PHC_REQUIRE(!(d->epilogue == PHC_EPI_DSILU_GRAD && d->bias), "twin_gemm: DSILU_GRAD takes no bias (aux is silu'(pre))");
+  const bool grad_epi = epi == PHC_EPI_SILU_GRAD || epi == PHC_EPI_RELU_GRAD;
   PHC_REQUIRE(d->twin_groups >= 1 && d->twin_cols >= 1 && d->twin_groups * d->twin_cols == d->batch * d->n,
               "twin_gemm: twin geometry must cover batch * n columns");
-  PHC_REQUIRE(!(d->epilogue == PHC_EPI_BIAS || d->epilogue == PHC_EPI_BIAS_SILU || d->epilogue == PHC_EPI_BIAS_RELU) ||
+  PHC_REQUIRE(!(epi == PHC_EPI_BIAS || epi == PHC_EPI_BIAS_SILU || epi == PHC_EPI_BIAS_RELU) ||
                   d->bias,
               "twin_gemm: epilogue needs the bias");
   PHC_REQUIRE(!grad_epi || d->aux, "twin_gemm: SILU_GRAD / RELU_GRAD need the (pre-)activation (aux)");

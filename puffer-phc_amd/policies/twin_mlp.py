@@ -237,7 +237,14 @@ class MfmaTrunkSaved:
 
     def __init__(self, xc, wt, pres, zs, K0):
         self.xc, self.wt, self.pres, self.zs, self.K0 = xc, wt, pres, zs, K0
+        self.deriv = False  # pres are the pre-activations (True: their silu', PHC_EPI_BIAS_SILU_D)
         self.L = len(wt) + 1
+
+
+# the forward GEMMs keep silu'(pre-activation) for the backward instead of the pre-activation itself
+# (PHC_EPI_BIAS_SILU_D / PHC_EPI_DSILU_GRAD: the same bytes, and the input-gradient epilogues multiply
+# instead of evaluating the sigmoid, which made them VALU-bound); PHC_SILU_DERIV=0 keeps the pre-activation
+SILU_DERIV = os.environ.get("PHC_SILU_DERIV", "1") == "1"
 
 
 def mfma_trunk_forward(x, weights, need_grad):
@@ -263,7 +270,8 @@ def mfma_trunk_forward(x, weights, need_grad):
         z = torch.empty((2, M, n1), dtype=dt, device=x.device)
         pdt = dt if PRE_HALF else torch.float32
         pre = torch.empty((M, 2 * n1), dtype=pdt, device=x.device) if need_grad else None
-        N.twin_gemm(xc, ops.w0, N.EPI_BIAS_SILU, z, (2, n1), bias=B[0], aux=pre, aux_layout=N.SPLIT,
+        epi_fwd = N.EPI_BIAS_SILU_D if (need_grad and SILU_DERIV) else N.EPI_BIAS_SILU
+        N.twin_gemm(xc, ops.w0, epi_fwd, z, (2, n1), bias=B[0], aux=pre, aux_layout=N.SPLIT,
                     out_layout=N.GROUPED)
         pres, zs = [pre], [z]
         L = len(ops.w) + 1
@@ -272,13 +280,15 @@ def mfma_trunk_forward(x, weights, need_grad):
             if l < L - 1:
                 z = torch.empty((2, M, n), dtype=dt, device=x.device)
                 pre = torch.empty((2, M, n), dtype=pdt, device=x.device) if need_grad else None
-                N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS_SILU, z, (2, n), bias=B[l], aux=pre)
+                N.twin_gemm(zs[-1], ops.w[l - 1], epi_fwd, z, (2, n), bias=B[l], aux=pre)
                 pres.append(pre)
                 zs.append(z)
             else:
                 y = torch.empty((2, M, n), dtype=torch.float32, device=x.device)
                 N.twin_gemm(zs[-1], ops.w[l - 1], N.EPI_BIAS, y, (2, n), bias=B[l])
     saved = MfmaTrunkSaved(xc, list(ops.wt), pres, zs, K0) if need_grad else None
+    if saved is not None:
+        saved.deriv = epi_fwd == N.EPI_BIAS_SILU_D  # pres hold silu'(pre-activation)
     return y, saved
 
 
@@ -362,6 +372,7 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None, store=Fal
     grouped tile), so the caller need not zero the gradient buffer first."""
     L, K0 = saved.L, saved.K0
     xc, WT, pres, zs = saved.xc, saved.wt, saved.pres, saved.zs
+    epi_bwd = N.EPI_DSILU_GRAD if saved.deriv else N.EPI_SILU_GRAD
     dt = xc.dtype
     M = xc.shape[0]
     grads = [None] * (2 * L)
@@ -428,10 +439,10 @@ def mfma_trunk_backward(saved, g, db, params, direct, extra_jobs=None, store=Fal
                 bias_out = dict(bias_grad=db)
             if l > 1:
                 gp = torch.empty((2, M, k), dtype=dt, device=g.device)
-                N.twin_gemm(g, WT[l - 1], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[l - 1], **bias_out)
+                N.twin_gemm(g, WT[l - 1], epi_bwd, gp, (2, k), aux=pres[l - 1], **bias_out)
             else:  # into the first layer's SPLIT [M, 2k] layout, the operand of its weight gradient
                 gp = torch.empty((M, 2 * k), dtype=dt, device=g.device)
-                N.twin_gemm(g, WT[0], N.EPI_SILU_GRAD, gp, (2, k), aux=pres[0], aux_layout=N.SPLIT,
+                N.twin_gemm(g, WT[0], epi_bwd, gp, (2, k), aux=pres[0], aux_layout=N.SPLIT,
                             out_layout=N.SPLIT, **bias_out)
                 if grouped:
                     d, W = wdst(0)

@@ -319,3 +319,41 @@ def test_wave_specialised_persistent_matches_one_tile(dtype, epi):
         ref = torch.relu(ref)
     eps = 2.0 ** -8 if dtype == torch.float16 else 2.0 ** -5
     torch.testing.assert_close(outs[0][0].float(), ref, rtol=eps if odt != torch.float32 else 2e-5, atol=2e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("m", [777, 16500])  # 128 x 128 tiles; 256 x 256 tiles (wave-specialised forward grid)
+def test_silu_deriv_aux_pair(dtype, m):
+    """PHC_EPI_BIAS_SILU_D stores silu'(pre) (s (1 + z (1 - s))) as the aux and the same activation as
+    BIAS_SILU (bit for bit); PHC_EPI_DSILU_GRAD multiplies the input gradient by that aux and gives
+    SILU_GRAD's result (from the pre-activation) within the aux's rounding, bias-gradient sums too."""
+    from puffer_phc_amd import _native as N
+
+    g = torch.Generator(device=DEV).manual_seed(12)
+    k, n, nout = 192, 1000, 256
+    a = torch.randn((2, m, k), device=DEV, generator=g).to(dtype)
+    w = (torch.randn((2, n, k), device=DEV, generator=g) / k ** 0.5).to(dtype)
+    b = torch.randn(2 * n, device=DEV, generator=g)
+    y0, pre = torch.empty((2, m, n), dtype=dtype, device=DEV), torch.empty((2, m, n), dtype=dtype, device=DEV)
+    y1, dsl = torch.empty((2, m, n), dtype=dtype, device=DEV), torch.empty((2, m, n), dtype=dtype, device=DEV)
+    N.twin_gemm(a, w, N.EPI_BIAS_SILU, y0, (2, n), bias=b, aux=pre)
+    N.twin_gemm(a, w, N.EPI_BIAS_SILU_D, y1, (2, n), bias=b, aux=dsl)
+    assert torch.equal(y0, y1)
+    z = torch.bmm(a.float(), w.float().transpose(1, 2)) + b.view(2, 1, n)
+    s = torch.sigmoid(z)
+    eps = 2.0 ** -10 if dtype == torch.float16 else 2.0 ** -7
+    torch.testing.assert_close(dsl.float(), s * (1 + z * (1 - s)), rtol=eps, atol=2e-3)
+    # backward: gp = (gout @ W) * silu'(z); W given as [n_in = n, n_out] for gout [2, m, n_out]
+    gout = (torch.randn((2, m, nout), device=DEV, generator=g) * 0.5).to(dtype)
+    wt = (torch.randn((2, n, nout), device=DEV, generator=g) / nout ** 0.5).to(dtype)
+    gp0, gp1 = torch.empty((2, m, n), dtype=dtype, device=DEV), torch.empty((2, m, n), dtype=dtype, device=DEV)
+    db0, db1 = torch.empty(2 * n, device=DEV), torch.empty(2 * n, device=DEV)
+    N.twin_gemm(gout, wt, N.EPI_SILU_GRAD, gp0, (2, n), aux=pre, bias_grad=db0)
+    N.twin_gemm(gout, wt, N.EPI_DSILU_GRAD, gp1, (2, n), aux=dsl, bias_grad=db1)
+    full = torch.bmm(gout.float(), wt.float().transpose(1, 2)) * (s * (1 + z * (1 - s)))
+    tol = 2.0 ** -8 if dtype == torch.float16 else 2.0 ** -5
+    torch.testing.assert_close(gp1.float(), full, rtol=tol, atol=5e-3)
+    torch.testing.assert_close(gp1.float(), gp0.float(), rtol=tol, atol=5e-3)
+    torch.testing.assert_close(db1, full.sum(1).reshape(-1), rtol=2e-2, atol=0.5)
+    with pytest.raises(RuntimeError):  # the derivative aux already holds the bias
+        N.twin_gemm(gout, wt, N.EPI_DSILU_GRAD, gp1, (2, n), bias=b, aux=dsl)

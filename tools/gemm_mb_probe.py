@@ -28,6 +28,8 @@ PER_TRUNK = os.environ.get("PER_TRUNK", "0") == "1"  # one launch per trunk (bat
 # YONLY=1: the forward GEMMs store the activation only, not the pre-activation (the upper bound of a
 # y-only forward store whose consumers would recompute what they need)
 AUX = os.environ.get("YONLY", "0") != "1"
+# DERIV=1: the silu'-aux pair (forward PHC_EPI_BIAS_SILU_D, input gradients PHC_EPI_DSILU_GRAD), as the trunk runs it
+DERIV = os.environ.get("DERIV", "0") == "1"
 
 
 SUMS = []
@@ -63,7 +65,7 @@ def main():
     b0 = torch.randn(2 * DIMS[1], device=dev, generator=g)
     z = torch.empty((2, M, DIMS[1]), dtype=dt, device=dev)
     pre = torch.empty((M, 2 * DIMS[1]), dtype=dt, device=dev)
-    us = timeit(lambda: N.twin_gemm(x, w0, N.EPI_BIAS_SILU, z, (2, DIMS[1]), bias=b0, aux=pre if AUX else None,
+    us = timeit(lambda: N.twin_gemm(x, w0, N.EPI_BIAS_SILU_D if DERIV else N.EPI_BIAS_SILU, z, (2, DIMS[1]), bias=b0, aux=pre if AUX else None,
                                     aux_layout=N.SPLIT, out_layout=N.GROUPED), z)
     rows.append(("fwd L1", M, 2 * DIMS[1], DIMS[0], 1, us))
     for l in range(2, 7):
@@ -79,7 +81,7 @@ def main():
         elif l < 6:
             o = torch.empty((2, M, n), dtype=dt, device=dev)
             p = torch.empty((2, M, n), dtype=dt, device=dev)
-            us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS_SILU, o, (2, n), bias=b, aux=p if AUX else None), o)
+            us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS_SILU_D if DERIV else N.EPI_BIAS_SILU, o, (2, n), bias=b, aux=p if AUX else None), o)
         else:
             o = torch.empty((2, M, n), dtype=torch.float32, device=dev)
             us = timeit(lambda: N.twin_gemm(a, w, N.EPI_BIAS, o, (2, n), bias=b), o)
@@ -97,11 +99,11 @@ def main():
                                              bias_grad=db[t * nin:(t + 1) * nin]) for t in range(2)], o)
         elif l > 2:
             o = torch.empty((2, M, nin), dtype=dt, device=dev)
-            us = timeit(lambda: N.twin_gemm(gg, wt, N.EPI_SILU_GRAD, o, (2, nin), aux=p, bias_grad=db), o)
+            us = timeit(lambda: N.twin_gemm(gg, wt, N.EPI_DSILU_GRAD if DERIV else N.EPI_SILU_GRAD, o, (2, nin), aux=p, bias_grad=db), o)
         else:
             o = torch.empty((M, 2 * nin), dtype=dt, device=dev)
             p = rnd(M, 2 * nin)
-            us = timeit(lambda: N.twin_gemm(gg, wt, N.EPI_SILU_GRAD, o, (2, nin), aux=p, aux_layout=N.SPLIT,
+            us = timeit(lambda: N.twin_gemm(gg, wt, N.EPI_DSILU_GRAD if DERIV else N.EPI_SILU_GRAD, o, (2, nin), aux=p, aux_layout=N.SPLIT,
                                             out_layout=N.SPLIT, bias_grad=db), o)
         rows.append((f"dgrad L{l}", M, nin, nout, 2, us))
     # weight gradients (hipBLASLt, fp32 out): dW[b] = g[b]^T z[b]
