@@ -286,34 +286,41 @@ def test_persistent_grid_matches_one_tile_per_workgroup(epi, max_wg):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("epi", ["store", "bias_f32", "bias_silu", "bias_silu_noaux", "bias_relu"])
-def test_wave_specialised_persistent_matches_one_tile(dtype, epi):
+@pytest.mark.parametrize("epi", ["store", "bias_f32", "bias_silu", "bias_silu_noaux", "bias_relu", "bias_silu_d"])
+@pytest.mark.parametrize("shape", [(4160, 700), (4352, 768)])
+def test_wave_specialised_persistent_matches_one_tile(dtype, epi, shape):
     """The forward epilogues run wave-specialised in a persistent grid (kWsTile: waves 0-3 issue the
     operand DMA and stage the bias row, waves 4-7 store; the default for the training GEMMs, which
     have more 256 x 256 tiles than CUs) and must equal the one-tile-per-workgroup kernel bit for bit:
     every epilogue, both operand types, whole and ragged tiles (rows 4160 = 16.25 tiles, columns 700),
-    fp32 and half outputs, with and without the pre-activation."""
+    fp32 and half outputs, with and without the pre-activation (or its derivative, BIAS_SILU_D); whole
+    tiles only (4352 x 768) as well."""
     from puffer_phc_amd import _native as N
 
     g = torch.Generator(device=DEV).manual_seed(11)
-    m, n, k = 4160, 700, 448
+    (m, n), k = shape, 448
     a = torch.randn((2, m, k), device=DEV, generator=g).to(dtype)
     w = (torch.randn((2, n, k), device=DEV, generator=g) / k ** 0.5).to(dtype)
     bias = torch.randn(2 * n, device=DEV, generator=g)
     ep = {"store": N.EPI_STORE, "bias_f32": N.EPI_BIAS, "bias_silu": N.EPI_BIAS_SILU,
-          "bias_silu_noaux": N.EPI_BIAS_SILU, "bias_relu": N.EPI_BIAS_RELU}[epi]
+          "bias_silu_noaux": N.EPI_BIAS_SILU, "bias_relu": N.EPI_BIAS_RELU, "bias_silu_d": N.EPI_BIAS_SILU_D}[epi]
     odt = torch.float32 if epi == "bias_f32" else dtype
     outs = []
     for mwg in (0, 37):  # 37 workgroups: 48 tiles each loop over several (and a ragged last step)
         out = torch.full((2, m, n), 7.0, dtype=odt, device=DEV)
-        aux = torch.full((2, m, n), 7.0, dtype=dtype, device=DEV) if epi == "bias_silu" else None
+        aux = torch.full((2, m, n), 7.0, dtype=dtype, device=DEV) if epi in ("bias_silu", "bias_silu_d") else None
         N.twin_gemm(a, w, ep, out, (2, n), bias=None if epi == "store" else bias, aux=aux, max_workgroups=mwg)
         outs.append((out, aux))
     assert torch.equal(outs[1][0], outs[0][0])
     if outs[0][1] is not None:
         assert torch.equal(outs[1][1], outs[0][1])
     ref = torch.bmm(a.float(), w.float().transpose(1, 2)) + (0 if epi == "store" else bias.view(2, 1, n))
-    if epi in ("bias_silu", "bias_silu_noaux"):
+    if epi == "bias_silu_d":
+        s = torch.sigmoid(ref)
+        torch.testing.assert_close(outs[0][1].float(), s * (1 + ref * (1 - s)), rtol=2.0 ** -7, atol=2e-3)
+    elif epi == "bias_silu":
+        torch.testing.assert_close(outs[0][1].float(), ref, rtol=2.0 ** -7, atol=2e-3)
+    if epi in ("bias_silu", "bias_silu_noaux", "bias_silu_d"):
         ref = torch.nn.functional.silu(ref)
     elif epi == "bias_relu":
         ref = torch.relu(ref)
