@@ -146,11 +146,12 @@ __device__ __forceinline__ float gemm_sigmoid(float a) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-a * 1.44269504088896341f));
 }
 __device__ __forceinline__ float gemm_silu(float a) { return a * gemm_sigmoid(a); }
-// y = silu(z) (gemm_silu's arithmetic) and d = silu'(z) = s (1 + z (1 - s)) from one sigmoid
+// y = silu(z) (gemm_silu's arithmetic) and d = silu'(z) = s (1 + z (1 - s)) = s + y - y s from one
+// sigmoid: one add and one fma on top of y (the store waves' epilogue is VALU-bound)
 __device__ __forceinline__ void gemm_silu_d(float z, float &y, float &d) {
   const float s = gemm_sigmoid(z);
   y = z * s;
-  d = s * (1.0f + z * (1.0f - s));
+  d = __builtin_fmaf(-y, s, s + y);
 }
 
 // workgroup barrier for the epilogue's LDS hand-offs: waits for this wave's LDS operations only
