@@ -135,19 +135,30 @@ struct FlatFields {
   int32_t n;
 };
 
-template <int IT>
+// RPB rows per workgroup (PHC_COPY_RPB): every row's loads are issued before the first store, so a
+// workgroup's rows share one memory round (one row per workgroup left 4,096 single-round workgroups
+// queued two deep per CU)
+#ifndef PHC_COPY_RPB
+#define PHC_COPY_RPB 4
+#endif
+template <int IT, int RPB>
 __global__ __launch_bounds__(256) void k_copy_rows_flat(FlatFields fs, const uint8_t *__restrict__ mask, int64_t n,
                                                         const int64_t *__restrict__ counts,
                                                         const int64_t *__restrict__ ws) {
-  const int64_t row = blockIdx.x;  // grid = n
+  const int64_t row0 = (int64_t)blockIdx.x * RPB;  // grid = ceil(n / RPB)
   const int t = threadIdx.x;
-  const uint32_t mk = *(mask ? (cu8 *)(mask + row) : (cu8 *)&kOneWord);  // pointer select: one load
-  const int64_t r = reinterpret_cast<const int32_t *>(ws + 1)[row];
-  const int64_t take = counts[1], start = ws[0];
   const int W = fs.woff[fs.n];
-  uint32_t v[IT];
-  const char *sp[IT];
-  int k_of[IT], w_of[IT];
+  uint32_t mk[RPB];
+  int64_t rk[RPB];
+#pragma unroll
+  for (int j = 0; j < RPB; ++j) {
+    const int64_t row = row0 + j < n ? row0 + j : n - 1;  // clamped: the tail rows are skipped below
+    mk[j] = *(mask ? (cu8 *)(mask + row) : (cu8 *)&kOneWord);  // pointer select: one load
+    rk[j] = reinterpret_cast<const int32_t *>(ws + 1)[row];
+  }
+  const int64_t take = counts[1], start = ws[0];
+  uint32_t v[RPB][IT];
+  int k_of[IT], w_of[IT], b_of[IT];  // field, word in the field, byte offset in the source row
 #pragma unroll
   for (int u = 0; u < IT; ++u) {
     int vw = t + 256 * u;
@@ -156,22 +167,35 @@ __global__ __launch_bounds__(256) void k_copy_rows_flat(FlatFields fs, const uin
 #pragma unroll
     for (int q = 1; q < PHC_MAX_ROW_FIELDS; ++q) k = (q < fs.n && vw >= fs.woff[q]) ? q : k;
     const int w = vw - fs.woff[k];
-    const bool b8 = (fs.u8_mask >> k) & 1u;
-    const char *a = fs.src[k] + row * fs.srb[k] + (b8 ? w : 4 * w);
-    sp[u] = a;
     k_of[u] = k;
     w_of[u] = w;
-    v[u] = *(cu32 *)((uintptr_t)a & ~(uintptr_t)3);
+    b_of[u] = ((fs.u8_mask >> k) & 1u) ? w : 4 * w;
   }
-  if (!mk || r >= take) return;
-  const int64_t dst_row = start + r;
 #pragma unroll
-  for (int u = 0; u < IT; ++u) {
-    if (t + 256 * u >= W) break;
-    const int k = k_of[u];
-    uint32_t x = v[u];
-    if ((fs.u8_mask >> k) & 1u) x = ((x >> (8 * ((uintptr_t)sp[u] & 3))) & 0xFFu) ? 0x3F800000u : 0u;
-    *reinterpret_cast<uint32_t *>(fs.dst[k] + dst_row * fs.drb[k] + 4 * w_of[u]) = x;
+  for (int j = 0; j < RPB; ++j) {
+    const int64_t row = row0 + j < n ? row0 + j : n - 1;
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const char *a = fs.src[k_of[u]] + row * fs.srb[k_of[u]] + b_of[u];
+      v[j][u] = *(cu32 *)((uintptr_t)a & ~(uintptr_t)3);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RPB; ++j) {
+    const int64_t row = row0 + j;
+    if (row >= n || !mk[j] || rk[j] >= take) continue;
+    const int64_t dst_row = start + rk[j];
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      if (t + 256 * u >= W) break;
+      const int k = k_of[u];
+      uint32_t x = v[j][u];
+      if ((fs.u8_mask >> k) & 1u) {
+        const uintptr_t src = (uintptr_t)(fs.src[k] + row * fs.srb[k] + b_of[u]);
+        x = ((x >> (8 * (src & 3))) & 0xFFu) ? 0x3F800000u : 0u;
+      }
+      *reinterpret_cast<uint32_t *>(fs.dst[k] + dst_row * fs.drb[k] + 4 * w_of[u]) = x;
+    }
   }
 }
 
@@ -229,11 +253,13 @@ extern "C" int phc_compact_rows(const phc_row_field *fields, int32_t num_fields,
   if (flat) {
     ff.woff[num_fields] = (int32_t)words;
     ff.n = num_fields;
-    const dim3 g((unsigned)n), b(256);
-    if (words <= 256) hipLaunchKernelGGL(k_copy_rows_flat<1>, g, b, 0, st, ff, mask, n, counts, ws);
-    else if (words <= 512) hipLaunchKernelGGL(k_copy_rows_flat<2>, g, b, 0, st, ff, mask, n, counts, ws);
-    else if (words <= 1024) hipLaunchKernelGGL(k_copy_rows_flat<4>, g, b, 0, st, ff, mask, n, counts, ws);
-    else hipLaunchKernelGGL(k_copy_rows_flat<8>, g, b, 0, st, ff, mask, n, counts, ws);
+    constexpr int R = PHC_COPY_RPB, R8 = R > 2 ? 2 : R;  // 8 words per thread: at most 2 rows in flight
+    auto grid = [&](int rpb) { return dim3((unsigned)((n + rpb - 1) / rpb)); };
+    const dim3 b(256);
+    if (words <= 256) hipLaunchKernelGGL((k_copy_rows_flat<1, R>), grid(R), b, 0, st, ff, mask, n, counts, ws);
+    else if (words <= 512) hipLaunchKernelGGL((k_copy_rows_flat<2, R>), grid(R), b, 0, st, ff, mask, n, counts, ws);
+    else if (words <= 1024) hipLaunchKernelGGL((k_copy_rows_flat<4, R>), grid(R), b, 0, st, ff, mask, n, counts, ws);
+    else hipLaunchKernelGGL((k_copy_rows_flat<8, R8>), grid(R8), b, 0, st, ff, mask, n, counts, ws);
   } else {
     hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)n), dim3(256), 0, st, fs, mask, n, counts, ws);
   }
