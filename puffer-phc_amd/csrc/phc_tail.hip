@@ -24,7 +24,10 @@ namespace phc {
 constexpr int kTH = 512;        // hidden width
 constexpr int kTC = kTH / 256;  // float4 chunks per lane in a row
 constexpr int kTA = 72;         // max actions (b_mu sums: two per lane)
-constexpr int kFwdThreads = 256, kFwdRows = 8;  // forward: 4 waves, 8 rows (16 row tasks)
+#ifndef PHC_TAIL_FWD_ROWS
+#define PHC_TAIL_FWD_ROWS 4
+#endif
+constexpr int kFwdThreads = 256, kFwdRows = PHC_TAIL_FWD_ROWS;  // forward: 4 waves, 4 rows (8 row tasks)
 constexpr int kBwdThreads = 512;                // backward: 8 waves, persistent
 
 __device__ __forceinline__ float t_wave_sum(float s) {
