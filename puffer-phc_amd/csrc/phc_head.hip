@@ -412,28 +412,37 @@ __global__ __launch_bounds__(kX3FwdWaves * 64) void k_head_fwd_x3(const float *_
   }
 }
 
-// dh = dmu W.  Workgroup = 4 waves = 256 rows x one 128-column panel (blockIdx.y); the panel's W
+// dh = dmu W.  Workgroup = 8 waves = 512 rows x one 128-column panel (blockIdx.y); the panel's W
 // columns are split once into three bf16 planes in LDS, transposed to [column][K] (K = actions,
 // zero past A, padded to 96 + 8) so a lane's 8 consecutive K values are one 16-B read; wave tile =
 // 64 rows (4 row blocks) x 128 columns (8 column blocks), 32 accumulators.
 constexpr int kX3DgradKP = 104;
+// waves per workgroup (64 rows each): the panel's W split is shared by kX3DgradWaves x 64 rows
+// (8: 33.9 vs 35.8 us per 32768-row minibatch with 4, profiles/r05_round5b_experiments.txt §15)
+#ifndef PHC_HEAD_DGRAD_WAVES
+#define PHC_HEAD_DGRAD_WAVES 8
+#endif
+constexpr int kX3DgradWaves = PHC_HEAD_DGRAD_WAVES, kX3DgradThreads = 64 * kX3DgradWaves;
 
-__global__ __launch_bounds__(256, 2) void k_head_dgrad_x3(const float *__restrict__ dmu, const float *__restrict__ w,
-                                                       float *__restrict__ dh, int64_t M, int H, int A) {
+__global__ __launch_bounds__(kX3DgradThreads, 8 / kX3DgradWaves) void k_head_dgrad_x3(const float *__restrict__ dmu,
+                                                                                     const float *__restrict__ w,
+                                                                                     float *__restrict__ dh, int64_t M,
+                                                                                     int H, int A) {
   __shared__ __attribute__((aligned(16))) __bf16 pl[3][128 * kX3DgradKP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int n0 = blockIdx.y * 128;
   const int nq = (A + 31) / 32;  // 32-deep K steps (uniform)
-  for (int base = threadIdx.x; base < 32 * nq * 128; base += 16 * 256) {  // 16 loads in flight
-    float tmp[16];
+  constexpr int kU = 4096 / kX3DgradThreads;  // loads in flight per thread (16 at 4 waves)
+  for (int base = threadIdx.x; base < 32 * nq * 128; base += kU * kX3DgradThreads) {
+    float tmp[kU];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int i = base + 256 * u, k = i >> 7, n = i & 127;
+    for (int u = 0; u < kU; ++u) {
+      const int i = base + kX3DgradThreads * u, k = i >> 7, n = i & 127;
       tmp[u] = (k < A && n0 + n < H) ? w[(int64_t)k * H + n0 + n] : 0.0f;
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int i = base + 256 * u, k = i >> 7, n = i & 127;
+    for (int u = 0; u < kU; ++u) {
+      const int i = base + kX3DgradThreads * u, k = i >> 7, n = i & 127;
       if (i >= 32 * nq * 128) break;
       const __bf16 hi = (__bf16)tmp[u];
       float r = tmp[u] - (float)hi;
@@ -445,7 +454,7 @@ __global__ __launch_bounds__(256, 2) void k_head_dgrad_x3(const float *__restric
     }
   }
   __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * 256 + wave * 64;
+  const int64_t r0 = (int64_t)blockIdx.x * (64 * kX3DgradWaves) + wave * 64;
   if (r0 >= M) return;  // after the barrier
   const float *ap[4];
 #pragma unroll
@@ -576,9 +585,10 @@ extern "C" int phc_mu_head_dgrad(const float *dmu, const float *w, float *dh, in
     const char *e = getenv("PHC_MU_X3");
     return !(e && atoi(e) == 0);
   }();
-  if (x3) {  // bf16 x3 MFMA, 256 rows x 128 columns per workgroup
-    const dim3 grid((unsigned)((rows + 255) / 256), (unsigned)((hidden + 127) / 128));
-    hipLaunchKernelGGL(k_head_dgrad_x3, grid, dim3(256), 0, as_stream(stream), dmu, w, dh, rows, (int)hidden,
+  if (x3) {  // bf16 x3 MFMA, 512 rows x 128 columns per workgroup
+    const int64_t per = 64 * kX3DgradWaves;
+    const dim3 grid((unsigned)((rows + per - 1) / per), (unsigned)((hidden + 127) / 128));
+    hipLaunchKernelGGL(k_head_dgrad_x3, grid, dim3(kX3DgradThreads), 0, as_stream(stream), dmu, w, dh, rows, (int)hidden,
                        (int)num_actions);
     return check_launch("mu_head_dgrad");
   }
