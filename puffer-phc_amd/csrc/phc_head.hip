@@ -317,7 +317,10 @@ using b8 = x3b8;
 // accumulators across the K chunks.  Lane (g, c): h row / W row c, K = k0 + 8 g .. + 7 of each
 // 32-deep step (the same K order on both operands); kX3FwdDepth steps of h are in flight per wave,
 // the first ones issued before the W staging.  Requires H % 32 == 0.
-constexpr int kX3FwdWaves = 8;
+#ifndef PHC_HEAD_FWD_WAVES
+#define PHC_HEAD_FWD_WAVES 8
+#endif
+constexpr int kX3FwdWaves = PHC_HEAD_FWD_WAVES;
 constexpr int kX3FwdDepth = 4;  // 32-deep steps of h in flight per wave
 constexpr int kX3FwdKC = 128, kX3FwdKP = kX3FwdKC + 8;
 
