@@ -73,6 +73,44 @@ GEMM_TIMER_PERIOD = 16
 KERNEL_TIMING_NOTE = ("in-kernel stamps (first workgroup start -> last workgroup end, s_memrealtime); rocprofv3 "
                       "durations of the same launches run ~3 us (env) / ~1 % (GEMM) longer: dispatch + end-of-kernel "
                       "release (profiles/r05_clock_vs_rocprof.json)")
+ENV_TIMING_NOTE = ("kernel_us / frac: dispatch-inclusive (the rocprofv3 basis) = the stamped mean over the timed region's "
+                   "sampled launches + dispatch_us, the mean (HIP-event-bracketed duration - stamped duration) of "
+                   "DISPATCH_PROBE_STEPS eager launches of the same kernel right after the timed region; "
+                   "kernel_us_stamped / frac_stamped: the in-kernel stamps alone")
+DISPATCH_PROBE_STEPS = 32
+
+
+def env_dispatch_us(env, actions, steps=DISPATCH_PROBE_STEPS):
+    """The env kernel's dispatch + end-of-kernel overhead that its own stamps do not see: `steps` eager
+    HumanoidPHC.step launches (one kernel each with the replay physics), each bracketed by HIP events on
+    the launching stream AND stamped by the kernel; returns mean(event duration - stamped duration) in
+    microseconds (what rocprofv3 adds to the stamped time), or None."""
+    from puffer_phc_amd._native import KernelTimer
+
+    e = env.env
+    # a slot holds 2 words per workgroup; the timer sizes its buffer for 1,024 workgroups per slot and the
+    # replay kernel runs one workgroup per env pair
+    per_slot = -(-((e.num_envs + 1) // 2) // 1024)
+    timer = KernelTimer(capacity=(steps + 8) * per_slot, period=1)
+    old = e.kernel_timer
+    e.kernel_timer = timer
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in evs:  # materialise the events before the measured launches
+        a.record()
+        b.record()
+    torch.cuda.synchronize()
+    timer.reset()
+    for a, b in evs:
+        a.record()
+        e.step(actions, auto_reset=True)
+        b.record()
+    torch.cuda.synchronize()
+    e.kernel_timer = old
+    stamped = timer.durations_ms()
+    if len(stamped) != steps:
+        return None
+    ev = [a.elapsed_time(b) for a, b in evs]
+    return float(np.mean(np.asarray(ev) - np.asarray(stamped)) * 1e3)
 
 
 def parse():
@@ -495,7 +533,9 @@ def main():
     # the kernel timers are attached before the warmup, so launches captured into hipGraphs during it
     # (the train / rollout graphs) carry timer slots; reset() after the warmup keeps only what the
     # timed region stamps (a graph's slots: its last replay)
-    timer = env.env.kernel_timer = KernelTimer(capacity=max(4096, 64 * args.steps), period=ENV_TIMER_PERIOD)
+    # sized for every sampled launch at one slot per launch (2 words per workgroup; 1,024 workgroups per slot)
+    per_slot = -(-((args.envs + 1) // 2) // 1024)
+    timer = env.env.kernel_timer = KernelTimer(capacity=max(4096, 64 * args.steps) * per_slot, period=ENV_TIMER_PERIOD)
     # the PPO update's trunk GEMMs (phc_twin_gemm of more than 4,096 rows + the weight gradients), every
     # GEMM_TIMER_PERIOD-th stamped by the kernel itself, with its 2 m n k FLOPs
     gtimer = KernelTimer(capacity=max(4096, 256 * args.steps), period=GEMM_TIMER_PERIOD)
@@ -542,6 +582,9 @@ def main():
         env.env.physics.timer = None
         phys_launches = ptimer.count
         phys_s = ptimer.total_ms() * 1e-3 / max(phys_launches, 1)
+    # the env kernel's dispatch overhead (for the rocprof-basis roofline), measured on eager launches after
+    # the timed region (replay physics: one launch per step)
+    disp_us = env_dispatch_us(env, runner.actions) if args.physics == "replay" else None
     t = torch.tensor([elapsed, kern_s], dtype=torch.float64, device=device)
     counts = [float(processed)]
     if world > 1:
@@ -566,7 +609,9 @@ def main():
         opnd = getattr(env.env, "_obs_operand", None)
         opnd_bytes = int(opnd[0].shape[1] * opnd[0].element_size()) if opnd is not None else 0
         env_bytes += opnd_bytes
-        achieved = env_bytes * args.envs / kern_s / 1e9 if kern_s > 0 else 0.0
+        achieved_st = env_bytes * args.envs / kern_s / 1e9 if kern_s > 0 else 0.0
+        kern_rp = kern_s + (disp_us or 0.0) * 1e-6  # dispatch-inclusive (rocprofv3 basis)
+        achieved = env_bytes * args.envs / kern_rp / 1e9 if kern_rp > 0 else 0.0
         traffic = None
         # HBM bytes of the env step from the committed PMC passes: the rollout-context launch (fused
         # operand written) has its own file (tools/gpu_pass.sh, stage pmc)
@@ -635,7 +680,9 @@ def main():
                               "env phase)" if fused else "phc_env_step",
                     "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "kernel_us": kern_s * 1e6, "timing": KERNEL_TIMING_NOTE,
+                    "kernel_us": kern_rp * 1e6, "kernel_us_stamped": kern_s * 1e6, "dispatch_us": disp_us,
+                    "frac_stamped": achieved_st / HBM_PEAK_GBS,
+                    "timing": ENV_TIMING_NOTE if disp_us is not None else KERNEL_TIMING_NOTE,
                     "launches_timed": env_steps, "launches_in_region": env_offered,
                     "algorithmic_bytes_per_env_step": env_bytes, "obs_operand_bytes_per_env_step": opnd_bytes}
         if gemm_launches:

@@ -374,6 +374,9 @@ typedef struct phc_gemm_desc {
                         torch.autocast's Linear output and SiLU's saved input are */
   int32_t max_workgroups; /* 0: one workgroup per output tile; else at most this many
                              workgroups, each looping over tiles (persistent) */
+  int32_t k_valid;        /* 0, or the algorithmic depth when the operands' last k - k_valid columns are
+                             zero padding (the first layer's 934 observations padded to 960): only the
+                             kernel timer's FLOP count (phc_gemm_set_timer) uses it */
 } phc_gemm_desc;
 size_t phc_twin_gemm_workspace_bytes(int64_t m, int32_t batch, int32_t n);
 /* SILU_GRAD / RELU_GRAD: with a workspace and bias_grad NULL, the launch leaves the bias gradient

@@ -145,7 +145,8 @@ class GemmDescC(ctypes.Structure):
                 ("batch", ctypes.c_int32), ("dtype", ctypes.c_int32), ("epilogue", ctypes.c_int32),
                 ("out_dtype", ctypes.c_int32), ("bias", c_vp), ("aux", c_vp), ("out", c_vp),
                 ("aux_layout", ctypes.c_int32), ("out_layout", ctypes.c_int32), ("twin_groups", ctypes.c_int32),
-                ("twin_cols", ctypes.c_int32), ("aux_dtype", ctypes.c_int32), ("max_workgroups", ctypes.c_int32)]
+                ("twin_cols", ctypes.c_int32), ("aux_dtype", ctypes.c_int32), ("max_workgroups", ctypes.c_int32),
+                ("k_valid", ctypes.c_int32)]
 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_SILU, EPI_SILU_GRAD, EPI_BIAS_RELU, EPI_RELU_GRAD = 0, 1, 2, 3, 4, 5
@@ -655,12 +656,13 @@ GEMM_LAUNCHES = [0]
 
 
 def twin_gemm(a, b, epilogue, out, twin, bias=None, aux=None, aux_layout=GROUPED, out_layout=GROUPED,
-              bias_grad=None, max_workgroups=0, bias_partial=None):
+              bias_grad=None, max_workgroups=0, bias_partial=None, k_valid=0):
     """out = epilogue(a[b] @ b[b]^T) for a [batch?, m, k], b [batch?, n, k] (phc_twin_gemm).
     twin = (groups, cols) of the output / aux tensors' logical columns.  max_workgroups > 0:
     a persistent grid of that many workgroups looping over the tiles.  Grad epilogues: bias_grad
     [batch * n] receives the column sums; or bias_partial, fp32 [twin_gemm_m_tiles(m, n, batch),
-    batch * n], the per-m-tile column sums for the caller to reduce (no second launch)."""
+    batch * n], the per-m-tile column sums for the caller to reduce (no second launch).  k_valid: the
+    algorithmic depth when a's / b's last columns are zero padding (the kernel timer's FLOP count only)."""
     pa, abs_, lda, ba, m, k = _operand(a, "a")
     pb, bbs, ldb, bb, n, kb = _operand(b, "b")
     if kb != k or (ba != bb and ba != 1 and bb != 1):
@@ -679,7 +681,7 @@ def twin_gemm(a, b, epilogue, out, twin, bias=None, aux=None, aux_layout=GROUPED
     d = GemmDescC(pa, pb, abs_, bbs, lda, ldb, m, n, k, batch, DTYPE_CODE[a.dtype], epilogue, DTYPE_CODE[out.dtype],
                   _ptr(bias, torch.float32, (batch * n,), "bias", nullable=True),
                   aux.data_ptr() if aux is not None else None, out.data_ptr(), aux_layout, out_layout, G, C,
-                  DTYPE_CODE[aux.dtype] if aux is not None else 0, int(max_workgroups))
+                  DTYPE_CODE[aux.dtype] if aux is not None else 0, int(max_workgroups), int(k_valid))
     ws = None
     if bias_grad is not None:
         _ptr(bias_grad, torch.float32, (batch * n,), "bias_grad")

@@ -1676,7 +1676,9 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   const int64_t out_bytes = d->m * (int64_t)d->batch * d->n * (d->out_dtype == PHC_DT_F32 ? 4 : 2);
   g.nt = (out_bytes >= nt_out_min ? 1 : 0) | ((nt_aux & 1) ? 2 : 0) | ((nt_aux & 2) ? 4 : 0);
   // the training GEMMs only: the rollout's (inside its captured graph, 4096 rows) stay untimed
-  if (d->m > kTimedMinRows) g.clk = phc_timer_take(g_gemm_timer, st, blocks, 2.0 * (double)d->m * d->n * d->k * d->batch);
+  // algorithmic FLOPs: the padded depth's zero columns are not counted (k_valid)
+  const int kf = d->k_valid > 0 && d->k_valid < d->k ? d->k_valid : d->k;
+  if (d->m > kTimedMinRows) g.clk = phc_timer_take(g_gemm_timer, st, blocks, 2.0 * (double)d->m * d->n * kf * d->batch);
   launch_gemm(d->dtype, d->out_dtype, d->epilogue, cfg, g, blocks, st);
   if (bias_grad) {
     const int c = d->batch * d->n;
@@ -1768,7 +1770,7 @@ extern "C" int phc_weight_grad_group(const phc_wgrad_problem *probs, int32_t cou
     p.tiles_n = (d.n + 255) / 256;
     p.block0 = (int)blocks;
     blocks += (int64_t)p.tiles_m * p.tiles_n * d.batch;
-    flops += 2.0 * (double)d.m * d.n * rows * d.batch;
+    flops += 2.0 * (double)d.m * d.n_valid * rows * d.batch;  // algorithmic: the padded columns not counted
   }
   PHC_REQUIRE(blocks < (1ll << 31), "weight_grad_group: grid too large");
   ga.count = count;

@@ -9,6 +9,37 @@
 
 namespace phc {
 
+// PHC_FAST_ENV_MATH (default 1): the float divisions and square roots of the per-step env math that no
+// index or flag depends on (slerp's weights, heading quaternions, the replay's quat_unit, the reward's
+// means and termination distance) on the hardware reciprocal / square root (1-ulp class) instead of the
+// correctly rounded IEEE sequences hipcc emits (~10 VALU each): the results stay within the north_star's
+// 1e-5 of the reference (tests/test_gpu_env_sizes.py).  Frame indices, blend weights and times
+// (frame_blend, the reset time draw) keep the IEEE division: they must match the reference bit for bit.
+#ifndef PHC_FAST_ENV_MATH
+#define PHC_FAST_ENV_MATH 1
+#endif
+__device__ __forceinline__ float fdiv_env(float a, float b) {
+#if PHC_FAST_ENV_MATH
+  return a * __builtin_amdgcn_rcpf(b);
+#else
+  return a / b;
+#endif
+}
+__device__ __forceinline__ float fsqrt_env(float x) {
+#if PHC_FAST_ENV_MATH
+  return __builtin_amdgcn_sqrtf(x);
+#else
+  return sqrtf(x);
+#endif
+}
+__device__ __forceinline__ float fexp_env(float x) {
+#if PHC_FAST_ENV_MATH
+  return __expf(x);
+#else
+  return expf(x);
+#endif
+}
+
 template <typename T> struct Q4 { T x, y, z, w; };
 template <typename T> struct V3 { T x, y, z; };
 
@@ -56,6 +87,18 @@ template <typename T> __device__ __forceinline__ Q4<T> quat_unit(Q4<T> q) {
   T n = norm4(q);
   n = n < T(1e-9) ? T(1e-9) : n;
   return {q.x / n, q.y / n, q.z / n, q.w / n};
+}
+
+// quat_unit (above) of a float quaternion on the hardware square root / reciprocal (PHC_FAST_ENV_MATH)
+__device__ __forceinline__ q4 quat_unit_env(q4 q) {
+#if PHC_FAST_ENV_MATH
+  float n = fsqrt_env(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  n = n < 1e-9f ? 1e-9f : n;
+  const float in = __builtin_amdgcn_rcpf(n);
+  return {q.x * in, q.y * in, q.z * in, q.w * in};
+#else
+  return quat_unit(q);
+#endif
 }
 
 // torch_utils.py:154-161 quat_pos (a sign flip by an exact +-1 factor) then quat_unit.
@@ -158,7 +201,7 @@ __device__ __forceinline__ float fold_angle_0_2pi(float a) { return a > 3.141592
 
 // torch_utils.py:86-106 quat_to_angle_axis: NaN lanes masked exactly like torch.where.
 __device__ __forceinline__ float quat_angle_masked(q4 q, float *sin_theta_out) {
-  const float sin_theta = sqrtf(1.0f - q.w * q.w);
+  const float sin_theta = fsqrt_env(1.0f - q.w * q.w);
   *sin_theta_out = sin_theta;
   if (!(fabsf(sin_theta) > 1e-5f)) return 0.0f;
   return fold_angle_0_2pi(2.0f * acosf(q.w));
@@ -178,13 +221,19 @@ __device__ __forceinline__ q4 slerp(q4 q0, q4 q1, float t) {
   if (c < 0.0f) q1 = {-q1.x, -q1.y, -q1.z, -q1.w};
   c = fabsf(c);
   if (fabsf(c) >= 1.0f) return q0;
-  const float sin_half = sqrtf(1.0f - c * c);
+  const float sin_half = fsqrt_env(1.0f - c * c);
   if (fabsf(sin_half) < 0.001f)
     return {0.5f * q0.x + 0.5f * q1.x, 0.5f * q0.y + 0.5f * q1.y, 0.5f * q0.z + 0.5f * q1.z,
             0.5f * q0.w + 0.5f * q1.w};
   const float half = acosf(c);
+#if PHC_FAST_ENV_MATH
+  const float inv = fdiv_env(1.0f, sin_half);
+  const float ra = sinf((1.0f - t) * half) * inv;
+  const float rb = sinf(t * half) * inv;
+#else
   const float ra = sinf((1.0f - t) * half) / sin_half;
   const float rb = sinf(t * half) / sin_half;
+#endif
   return {ra * q0.x + rb * q1.x, ra * q0.y + rb * q1.y, ra * q0.z + rb * q1.z, ra * q0.w + rb * q1.w};
 }
 
@@ -228,24 +277,26 @@ __device__ __forceinline__ void heading_quats(q4 root_rot, Heading *hrot, Headin
   float tn[6];
   tan_norm_fast(root_rot, tn);  // tn[0..2] = my_quat_rotate(root_rot, x-axis)
   const v3 d = {tn[0], tn[1], tn[2]};
-  const float r = sqrtf(d.x * d.x + d.y * d.y);
+  const float r = fsqrt_env(d.x * d.x + d.y * d.y);
   float ch = 1.0f, sh = 0.0f;
   if (r > 0.0f) {
-    ch = d.x / r;
-    sh = d.y / r;
+    const float ir = fdiv_env(1.0f, r);
+    ch = PHC_FAST_ENV_MATH ? d.x * ir : d.x / r;
+    sh = PHC_FAST_ENV_MATH ? d.y * ir : d.y / r;
   }
   float C, S;
   if (ch >= 0.0f) {
-    C = sqrtf((1.0f + ch) * 0.5f);
-    S = sh / (2.0f * C);
+    C = fsqrt_env((1.0f + ch) * 0.5f);
+    S = fdiv_env(sh, 2.0f * C);
   } else {
-    S = copysignf(sqrtf((1.0f - ch) * 0.5f), sh);
-    C = sh / (2.0f * S);
+    S = copysignf(fsqrt_env((1.0f - ch) * 0.5f), sh);
+    C = fdiv_env(sh, 2.0f * S);
   }
   // quat_unit of (0,0,+-S,C): the norm sqrt(S^2 + C^2) is shared and -S/n == -(S/n) exactly
-  float n = sqrtf(S * S + C * C);
+  float n = fsqrt_env(S * S + C * C);
   n = n < 1e-9f ? 1e-9f : n;
-  const float z = S / n, w = C / n;
+  const float in = fdiv_env(1.0f, n);
+  const float z = PHC_FAST_ENV_MATH ? S * in : S / n, w = PHC_FAST_ENV_MATH ? C * in : C / n;
   *hrot = make_heading(z, w);
   *hinv = make_heading(-z, w);
 }
@@ -261,6 +312,12 @@ __device__ __forceinline__ void quat_angle_axis_d(Q4<double> x, double *angle, V
 }
 
 // Counter-based RNG (splitmix64 finaliser): uniform float in [0, 1) with 24 random bits.
+// splitmix64's finaliser without its increment (mix64(z) == mix64_fin(z + 0x9E3779B97F4A7C15))
+__device__ __forceinline__ unsigned long long mix64_fin(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -9,14 +9,12 @@
 // records and the 4 reference frame rows it blends (t and t+dt) straight from HBM and
 // writes its 934-float observation row once.
 #include "phc_common.h"
+#include "phc_measure.h"
 
 #include <hip/hip_ext.h>
 
 #include <vector>
 
-#ifndef PHC_ENV_ABLATE
-#define PHC_ENV_ABLATE 0
-#endif
 // k_env_step's minimum waves per SIMD (its register budget): 4 = at most 128 VGPRs, which with 40 KB of
 // LDS per 8-env workgroup keeps 4 workgroups (16 waves) per CU; 3 let the fused kernel take 129
 #ifndef PHC_ENV_WAVES
@@ -230,11 +228,20 @@ __global__ __launch_bounds__(kBlock) void k_reset_envs(EnvView e, LibView l, Ste
 }
 
 // --------------------------------------------------------- physics stand-in --
-// Triangular noise with standard deviation `sd` from 16 random bits pairs (cheap integer RNG).
-__device__ __forceinline__ float tri_noise(unsigned long long h, int k, float sd) {
-  const unsigned a = (unsigned)(h >> (32 * (k & 1))) & 0xFFFFu;
-  const unsigned b = (unsigned)(h >> (32 * (k & 1) + 16)) & 0xFFFFu;
-  return ((float)a - (float)b) * (sd * 2.4494897f / 65536.0f);
+// Triangular noise with standard deviation `sd` from one 32-bit draw (two 16-bit uniforms).
+__device__ __forceinline__ float tri_noise32(uint32_t h, float sd) {
+  return ((float)(h & 0xFFFFu) - (float)(h >> 16)) * (sd * 2.4494897f / 65536.0f);
+}
+
+// xorshift32 (Marsaglia's 13 / 17 / 5): the replay's per-(env, body) noise stream after one splitmix64
+// seeding hash.  Round 6: the stream replaced one splitmix64 per noise pair — 9 per body, each two 64-bit
+// products of quarter-rate 32-bit multiplies — which made the hashing a large part of the replay's VALU
+// time.  Full-rate shifts and xors only.
+__device__ __forceinline__ uint32_t xs32(uint32_t &x) {
+  x ^= x << 13;
+  x ^= x >> 17;
+  x ^= x << 5;
+  return x;
 }
 
 struct ReplayArgs {
@@ -260,38 +267,31 @@ __device__ __forceinline__ void replay_perturb(const EnvView &e, const ReplayArg
   unsigned long long key = r.seed ^ mix64(r.counter);
   if (e.rng) key ^= mix64(((unsigned long long)rng_val << 20) ^ (unsigned long long)(unsigned)prog ^ 0x5bd1e995ull);
   const unsigned long long base = mix64(key ^ ((unsigned long long)(env * kBodies + b) << 8));
-  unsigned long long h = mix64(base + 1);
-  s.p.x += tri_noise(h, 0, sigma);
-  s.p.y += tri_noise(h, 1, sigma);
-  h = mix64(base + 2);
-  s.p.z += tri_noise(h, 0, sigma);
-  q4 q = {s.r.x + tri_noise(h, 1, sigma), s.r.y, s.r.z, s.r.w};
-  h = mix64(base + 3);
-  q.y += tri_noise(h, 0, sigma);
-  q.z += tri_noise(h, 1, sigma);
-  s.r = quat_unit(q);
-  h = mix64(base + 4);
-  s.v.x += tri_noise(h, 0, 10.0f * sigma);
-  s.v.y += tri_noise(h, 1, 10.0f * sigma);
-  h = mix64(base + 5);
-  s.v.z += tri_noise(h, 0, 10.0f * sigma);
-  s.av.x += tri_noise(h, 1, 20.0f * sigma);
-  h = mix64(base + 6);
-  s.av.y += tri_noise(h, 0, 20.0f * sigma);
-  s.av.z += tri_noise(h, 1, 20.0f * sigma);
+  uint32_t x = (uint32_t)base ^ (uint32_t)(base >> 32);
+  x = x ? x : 0x9E3779B9u;  // xorshift's one fixed point
+  s.p.x += tri_noise32(xs32(x), sigma);
+  s.p.y += tri_noise32(xs32(x), sigma);
+  s.p.z += tri_noise32(xs32(x), sigma);
+  q4 q = {s.r.x + tri_noise32(xs32(x), sigma), s.r.y, s.r.z, s.r.w};
+  q.y += tri_noise32(xs32(x), sigma);
+  q.z += tri_noise32(xs32(x), sigma);
+  s.r = quat_unit_env(q);
+  s.v.x += tri_noise32(xs32(x), 10.0f * sigma);
+  s.v.y += tri_noise32(xs32(x), 10.0f * sigma);
+  s.v.z += tri_noise32(xs32(x), 10.0f * sigma);
+  s.av.x += tri_noise32(xs32(x), 20.0f * sigma);
+  s.av.y += tri_noise32(xs32(x), 20.0f * sigma);
+  s.av.z += tri_noise32(xs32(x), 20.0f * sigma);
   dv = {0.0f, 0.0f, 0.0f};
   f = {0.0f, 0.0f, 0.0f};
   if (b >= 1) {
     dv = dv_ref;
-    h = mix64(base + 7);
-    dv.x = dv.x + tri_noise(h, 0, 10.0f * sigma);
-    dv.y = dv.y + tri_noise(h, 1, 10.0f * sigma);
-    h = mix64(base + 8);
-    dv.z = dv.z + tri_noise(h, 0, 10.0f * sigma);
-    f.x = tri_noise(h, 1, r.force_scale);
-    h = mix64(base + 9);
-    f.y = tri_noise(h, 0, r.force_scale);
-    f.z = tri_noise(h, 1, r.force_scale);
+    dv.x = dv.x + tri_noise32(xs32(x), 10.0f * sigma);
+    dv.y = dv.y + tri_noise32(xs32(x), 10.0f * sigma);
+    dv.z = dv.z + tri_noise32(xs32(x), 10.0f * sigma);
+    f.x = tri_noise32(xs32(x), r.force_scale);
+    f.y = tri_noise32(xs32(x), r.force_scale);
+    f.z = tri_noise32(xs32(x), r.force_scale);
   }
 }
 
@@ -349,23 +349,29 @@ __device__ __forceinline__ Outcome env_reward(const EnvView &e, const StepConsts
                                               const BodyRec &ref0, float pw_reg = -1.0f) {
   const bool active = lane < kBodies;
   const int b = active ? lane : 0;
+  // the means over xyz (/ 3) and over the 24 bodies (/ 24) as products with the reciprocals (1 ulp)
+  // under PHC_FAST_ENV_MATH; the reward's exponentials on the hardware exp2
+  constexpr float kThird = PHC_FAST_ENV_MATH ? 1.0f / 3.0f : 0.0f;
+  constexpr float kInvBodies = PHC_FAST_ENV_MATH ? 1.0f / (float)kBodies : 0.0f;
+  auto mean3 = [](float x) { return PHC_FAST_ENV_MATH ? x * kThird : x / 3.0f; };
   const v3 dp = vsub(ref0.p, s.p);
   float e_pos = dp.x * dp.x;
   e_pos = e_pos + dp.y * dp.y;
-  e_pos = (e_pos + dp.z * dp.z) / 3.0f;
+  e_pos = mean3(e_pos + dp.z * dp.z);
   float sin_t;
   const float ang = quat_angle_masked(quat_mul(ref0.r, quat_conj(s.r)), &sin_t);
   float e_rot = ang * ang;
   const v3 dv = vsub(ref0.v, s.v);
   float e_vel = dv.x * dv.x;
   e_vel = e_vel + dv.y * dv.y;
-  e_vel = (e_vel + dv.z * dv.z) / 3.0f;
+  e_vel = mean3(e_vel + dv.z * dv.z);
   const v3 da = vsub(ref0.av, s.av);
   float e_ang = da.x * da.x;
   e_ang = e_ang + da.y * da.y;
-  e_ang = (e_ang + da.z * da.z) / 3.0f;
+  e_ang = mean3(e_ang + da.z * da.z);
   // termination distance
-  const float dist = norm3(vsub(s.p, ref0.p));
+  const v3 dd = vsub(s.p, ref0.p);
+  const float dist = PHC_FAST_ENV_MATH ? fsqrt_env(dd.x * dd.x + dd.y * dd.y + dd.z * dd.z) : norm3(dd);
   const bool counted = active && ((c.reset_mask >> b) & 1u);
   float fall = (counted && dist > c.td[b]) ? 1.0f : 0.0f;
   float dsum = counted ? dist : 0.0f;
@@ -390,10 +396,11 @@ __device__ __forceinline__ Outcome env_reward(const EnvView &e, const StepConsts
   pw = group_sum(pw);
 
   Outcome o;
-  o.r_pos = expf(-c.k_pos * (e_pos / (float)kBodies));
-  o.r_rot = expf(-c.k_rot * (e_rot / (float)kBodies));
-  o.r_vel = expf(-c.k_vel * (e_vel / (float)kBodies));
-  o.r_ang = expf(-c.k_ang * (e_ang / (float)kBodies));
+  auto mean_b = [](float x) { return PHC_FAST_ENV_MATH ? x * kInvBodies : x / (float)kBodies; };
+  o.r_pos = fexp_env(-c.k_pos * mean_b(e_pos));
+  o.r_rot = fexp_env(-c.k_rot * mean_b(e_rot));
+  o.r_vel = fexp_env(-c.k_vel * mean_b(e_vel));
+  o.r_ang = fexp_env(-c.k_ang * mean_b(e_ang));
   o.rew = c.w_pos * o.r_pos + c.w_rot * o.r_rot + c.w_vel * o.r_vel + c.w_ang * o.r_ang;
   o.pr = 0.0f;
   if (c.use_power) {
@@ -456,18 +463,11 @@ __device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10], 
   }
 }
 
-// Half-wave per env, 8 envs per workgroup: the throughput form (large env counts).
-// REPLAY: HumanoidPHC.step with the physics stand-in in ONE launch — the action -> PD map (R13),
-// the replayed sim state (k_physics_replay: the reference at t plus noise, which is exactly ref0
-// below plus noise, so its frame rows are gathered once) and the post-physics step; the same
-// values as k_actions_to_pd -> k_physics_replay -> k_env_step bit for bit.
+// Half-wave per env, 8 envs per workgroup: the env step after a separate physics launch (k_env_step).
 // The observation rows (the kernel's largest output: 3,736 B per env) are staged in LDS and written
 // out by the whole workgroup as 16-B stores: the workgroup's 8 rows are one contiguous 29,888-B
 // span of obs [N, 934], so ~8 fully coalesced dwordx4 stores per thread replace 39 scattered dword
-// stores per body lane (PHC_ENV_OBS_LDS=0: written in place).
-#ifndef PHC_ENV_OBS_LDS
-#define PHC_ENV_OBS_LDS 1
-#endif
+// stores per body lane.
 
 // copy `nf` floats of LDS staging rows to global `dst` with 16-B stores (dst 16-B aligned), else 4-B
 __device__ __forceinline__ void copy_rows_out(float *__restrict__ dst, const float *__restrict__ src, int nf) {
@@ -507,16 +507,13 @@ __device__ __forceinline__ void operand_rows_out(const EnvView &e, const float *
   }
 }
 
-// Per-wave staging of the fused replay step (REPLAY, PHC_ENV_STAGE): each wave (2 envs) moves its
-// envs' four frame rows (t and t+dt blends; 1,248 B each, 16-B aligned in the packed table) into its
-// own LDS region by LDS-DMA — 10 wave-instructions of 1 KiB, fully used 64-B lines — instead of 52
-// scattered 4-B lane loads per body; the lanes read their body's records from LDS.  The same region
-// then holds the envs' observation rows and replayed rigid-body records, written out by the wave as
-// contiguous 16-B stores (the records were 13 scattered 4-B stores per body lane).  Wave-local: no
-// workgroup barrier until the stats row.  9,984 B per wave keeps 4 workgroups per CU (the VGPR limit).
-#ifndef PHC_ENV_STAGE
-#define PHC_ENV_STAGE 1
-#endif
+// Per-wave staging of the fused replay step (k_env_replay): each wave (2 envs) moves its envs' four
+// frame rows (t and t+dt blends; 1,248 B each, 16-B aligned in the packed table) into its own LDS
+// region by LDS-DMA — 10 wave-instructions of 1 KiB, fully used 64-B lines — instead of 52 scattered
+// 4-B lane loads per body; the lanes read their body's records from LDS.  The same region then holds
+// the envs' observation rows and replayed rigid-body records, written out by the wave as contiguous
+// 16-B stores (the records were 13 scattered 4-B stores per body lane).  Wave-local: no workgroup
+// barrier.  9,984 B per wave.
 constexpr int kWaveEnvs = 64 / kGroup;            // 2
 constexpr int kRowF = kBodies * kRec;             // 312 floats: one frame row = one env's records
 constexpr int kRowChunks = kRowF / 4;             // 78 x 16 B
@@ -524,6 +521,9 @@ constexpr int kStWave = kWaveEnvs * 4 * kRowF;    // 2,496 floats per wave
 constexpr int kStRec = kWaveEnvs * kObs;          // records after the wave's obs rows
 constexpr int kStDma = (kWaveEnvs * 4 * kRowChunks + 63) / 64;  // 10 LDS-DMA wave-instructions
 static_assert(kStRec % 4 == 0 && kStRec + kWaveEnvs * kRowF <= kStWave, "obs rows + records fit the rows region");
+
+typedef const __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
 
 // the wave's 2 x 4 frame rows into `wreg` ([env][row][312]); fr = this lane's env's frame rows
 __device__ __forceinline__ void stage_frame_rows(const float *__restrict__ frames, float *wreg, const int64_t fr[4],
@@ -544,10 +544,78 @@ __device__ __forceinline__ void stage_frame_rows(const float *__restrict__ frame
     const int fa = rr == 0 ? f0[0] : (rr == 1 ? f0[1] : (rr == 2 ? f0[2] : f0[3]));
     const int fb = rr == 0 ? f1[0] : (rr == 1 ? f1[1] : (rr == 2 ? f1[2] : f1[3]));
     const float *src = frames + (int64_t)(hi ? fb : fa) * kRowF + cc * 4;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                     (__attribute__((address_space(3))) void *)(wreg + i * 256), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gvoid *)src, (lvoid *)(wreg + i * 256), 16, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's rows have landed (wave-local region)
+}
+
+// The reset state of the envs of a wave that pass their clip's end in this step (t >= len: they reset
+// whatever their reward says), by LDS-DMA into the wave's region once its frame rows are in registers:
+// for each half-wave with `need`, the two frame rows of its reset blend (-> [env][2][312]), its two
+// local-rotation rows ([F, 24, 4] -> kRstLr + [env][2][96]) and its two dof-velocity rows ([F, 23, 3]
+// -> kRstDv + [env][2][69]): reset_env_state's loads, landing under the replay / reward arithmetic
+// instead of one dependent memory round after it.  No wait (the caller waits before reading).
+constexpr int kRstLr = kWaveEnvs * 2 * kRowF;                  // 1,248
+constexpr int kRstDv = kRstLr + kWaveEnvs * 2 * kBodies * 4;   // 1,632
+static_assert(kRstDv + kWaveEnvs * 2 * PHC_NUM_DOF <= kStWave, "reset words fit the wave's region");
+
+__device__ __forceinline__ void stage_reset_rows(const LibView &l, float *wreg, const Blend &bR, bool need, int wl) {
+  const int r00 = __builtin_amdgcn_readlane((int)bR.f0, 0), r01 = __builtin_amdgcn_readlane((int)bR.f1, 0);
+  const int r10 = __builtin_amdgcn_readlane((int)bR.f0, 32), r11 = __builtin_amdgcn_readlane((int)bR.f1, 32);
+  const bool n0 = __builtin_amdgcn_readlane((int)need, 0) != 0, n1 = __builtin_amdgcn_readlane((int)need, 32) != 0;
+  constexpr int kRows = kWaveEnvs * 2 * kRowChunks;  // 312 chunks of 16 B
+#pragma unroll
+  for (int i = 0; i < (kRows + 63) / 64; ++i) {
+    const int j = i * 64 + wl;
+    const int h = j >= 2 * kRowChunks;
+    const int rem = h ? j - 2 * kRowChunks : j;
+    const int rr = rem >= kRowChunks, cc = rr ? rem - kRowChunks : rem;
+    const int f = h ? (rr ? r11 : r10) : (rr ? r01 : r00);
+    if (j < kRows && (h ? n1 : n0))
+      __builtin_amdgcn_global_load_lds((gvoid *)(l.frames + (int64_t)f * kRowF + cc * 4), (lvoid *)(wreg + i * 256), 16,
+                                       0, 0);
+  }
+  constexpr int kLr = kWaveEnvs * 2 * kBodies;  // 96 chunks of 16 B (one quaternion each)
+#pragma unroll
+  for (int i = 0; i < (kLr + 63) / 64; ++i) {
+    const int j = i * 64 + wl;
+    const int h = j >= 2 * kBodies;
+    const int rem = h ? j - 2 * kBodies : j;
+    const int rr = rem >= kBodies, bb = rr ? rem - kBodies : rem;
+    const int f = h ? (rr ? r11 : r10) : (rr ? r01 : r00);
+    if (j < kLr && (h ? n1 : n0))
+      __builtin_amdgcn_global_load_lds((gvoid *)(l.local_rot + ((int64_t)f * kBodies + bb) * 4),
+                                       (lvoid *)(wreg + kRstLr + i * 256), 16, 0, 0);
+  }
+  constexpr int kDv = kWaveEnvs * 2 * PHC_NUM_DOF;  // 276 dwords
+#pragma unroll
+  for (int i = 0; i < (kDv + 63) / 64; ++i) {
+    const int j = i * 64 + wl;
+    const int h = j >= 2 * PHC_NUM_DOF;
+    const int rem = h ? j - 2 * PHC_NUM_DOF : j;
+    const int rr = rem >= PHC_NUM_DOF, k = rr ? rem - PHC_NUM_DOF : rem;
+    const int f = h ? (rr ? r11 : r10) : (rr ? r01 : r00);
+    if (j < kDv && (h ? n1 : n0))
+      __builtin_amdgcn_global_load_lds((gvoid *)(l.dof_vel + (int64_t)f * PHC_NUM_DOF + k),
+                                       (lvoid *)(wreg + kRstDv + i * 64), 4, 0, 0);
+  }
+}
+
+// reset_env_state's values of this lane's body from the staged words (its arithmetic, bit for bit): the
+// record (offset: the env's previous global offset), dof position and velocity
+__device__ __forceinline__ void staged_reset_values(const float *wreg, int g, int b, float t, v3 go, BodyRec &s,
+                                                    v3 &dp, v3 &dv) {
+  const float *rr = wreg + g * (2 * kRowF) + b * kRec;
+  s = blend_body(load_body(rr), load_body(rr + kRowF), t, &go);
+  if (b >= 1) {
+    const float *la = wreg + kRstLr + g * (2 * kBodies * 4) + b * 4;
+    const float *lc = la + kBodies * 4;
+    dp = quat_to_exp_map(slerp(q4{la[0], la[1], la[2], la[3]}, q4{lc[0], lc[1], lc[2], lc[3]}, t));
+    const float *da = wreg + kRstDv + g * (2 * PHC_NUM_DOF) + 3 * (b - 1);
+    const float *dc = da + PHC_NUM_DOF;
+    const float sb = 1.0f - t;
+    dv = {sb * da[0] + t * dc[0], sb * da[1] + t * dc[1], sb * da[2] + t * dc[2]};
+  }
 }
 
 // `nf` floats from the wave's LDS region to global `dst` by the wave's 64 lanes (16-B stores when
@@ -605,88 +673,19 @@ __device__ __forceinline__ void operand_rows_out_wave(const EnvView &e, const fl
   }
 }
 
-// measurement build (PHC_ENV_PHASES=1, never shipped): lane 0 of every wave stamps the constant clock at
-// the phase boundaries of the staged replay step into g_env_phase[wave][8] (read by
-// phc_env_phase_copy; tools/env_phase_probe.py): 0 start, 1 scalars used, 2 frame rows in LDS,
-// 3 replay + reward done, 4 observation row written, 5 rows copied out, 6 stats flushed
-#ifndef PHC_ENV_PHASES
-#define PHC_ENV_PHASES 0
-#endif
-#if PHC_ENV_PHASES
-constexpr int kPhaseWaves = 1 << 15;
-__device__ unsigned long long g_env_phase[kPhaseWaves * 8];
-#define ENV_PHASE(k)                                                                                  \
-  do {                                                                                                \
-    const int gw_ = (int)((blockIdx.x * kBlock + threadIdx.x) >> 6);                                  \
-    if ((threadIdx.x & 63) == 0 && gw_ < kPhaseWaves) g_env_phase[gw_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define ENV_PHASE(k) \
-  do {               \
-  } while (0)
-#endif
-
-template <bool AUTO, bool REPLAY>
-__global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, LibView l, StepConsts c, ReplayArgs r) {
+template <bool AUTO>
+__global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, LibView l, StepConsts c) {
   __shared__ double sh_stats[kEnvsPerBlock][10];
-  constexpr bool kStage = REPLAY && PHC_ENV_STAGE && PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0;
-#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
-  // kStage: one 2,496-float region per wave (frame rows, then obs rows + records); else the
-  // workgroup's 8 obs rows
-  __shared__ __attribute__((aligned(16))) float sh_obs[kStage ? (kBlock / 64) * kStWave : kEnvsPerBlock * kObs];
-#endif
+  __shared__ __attribute__((aligned(16))) float sh_obs[kEnvsPerBlock * kObs];  // the workgroup's 8 obs rows
   const int g = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kEnvsPerBlock + g;
   const int lane = threadIdx.x % kGroup;
   const bool valid = env < e.n;
   const int b = lane < kBodies ? lane : 0;
   const int64_t ei = valid ? env : 0;
-#if PHC_ENV_ABLATE == 1  // measurement build: launch + dispatch floor
-  if (valid && lane == 0) e.rew[ei] = 0.0f;
-  return;
-#endif
 
   launch_clock_begin(c.clk);
-  ENV_PHASE(0);
   const double st_prev = stats_prefetch(e);
-  // kStage: R13 for the wave's envs first (elementwise over their contiguous [nv, 69] action span,
-  // independent of everything else: its loads join the first memory round)
-#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
-  if constexpr (kStage) {
-    if (r.actions) {
-      const int wl = threadIdx.x & 63;
-      const int64_t env0 = (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6) * kWaveEnvs;
-      const int64_t left = e.n - env0;
-      const int nv = left <= 0 ? 0 : (left < kWaveEnvs ? (int)left : kWaveEnvs);
-      const float *a = r.actions + env0 * PHC_NUM_DOF;
-      float *pd = r.pd + env0 * PHC_NUM_DOF;
-      // every load of the span first (clamped indices, a zero row standing in for a null frozen
-      // mask): loads behind a select or a null check made hipcc wait vmcnt(0) per element
-      constexpr int kPdIt = (kWaveEnvs * PHC_NUM_DOF + 63) / 64;
-      const int cnt = nv * PHC_NUM_DOF;
-      gu8 *fz = r.frozen ? (gu8 *)r.frozen : (gu8 *)kNoFrozen;
-      float av[kPdIt], ov[kPdIt], sv[kPdIt];
-      uint8_t fv[kPdIt];
-#pragma unroll
-      for (int u = 0; u < kPdIt; ++u) {
-        const int i = wl + 64 * u < cnt ? wl + 64 * u : cnt - 1;
-        const int d = i >= PHC_NUM_DOF ? i - PHC_NUM_DOF : i;
-        av[u] = a[i];
-        ov[u] = r.off[d];
-        sv[u] = r.scale[d];
-        fv[u] = fz[d];
-      }
-#pragma unroll
-      for (int u = 0; u < kPdIt; ++u) {
-        const int i = wl + 64 * u;
-        if (i >= cnt) break;
-        float x = av[u];
-        if (r.clip) x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
-        pd[i] = fv[u] ? 0.0f : ov[u] + sv[u] * x;  // action_to_pd's expression
-      }
-    }
-  }
-#endif
   // per-env scalars (broadcast loads: every lane of the half-wave reads the same word); the rng
   // counter through a pointer select, so its load joins this round instead of waiting behind a
   // null check where it is used
@@ -700,83 +699,13 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
   const float t1n = (float)(prog + 1) * c.dt + st + so;  // observation time unless the env resets
   const Blend bl0 = frame_blend(t, m);
   Blend bl1 = frame_blend(t1n, m);
-#if PHC_ENV_PHASES
-  if (bl0.f0 == -12345) e.rew[0] = 0.0f;  // a use of the scalars before the stamp
-  ENV_PHASE(1);
-#endif
 
   // one memory round for the sim record and all four reference rows (t and t+dt)
-  BodyRec s;
-  if (!REPLAY) s = load_body(e.rb + (ei * kBodies + b) * kRec);
-  RowPair rows0, rows1;
-  // the replay's reference dof velocity rows: loaded before the row DMA's wait, in the same memory
-  // round, and blended after it (ref_dof_vel's arithmetic)
-  v3 dva = {0.0f, 0.0f, 0.0f}, dvc = {0.0f, 0.0f, 0.0f};
-  if (REPLAY) {
-    const int bb = b >= 1 ? b : 1;
-    const float *pa = l.dof_vel + (bl0.f0 * (kBodies - 1) + (bb - 1)) * 3;
-    const float *pc = l.dof_vel + (bl0.f1 * (kBodies - 1) + (bb - 1)) * 3;
-    dva = {pa[0], pa[1], pa[2]};
-    dvc = {pc[0], pc[1], pc[2]};
-  }
-#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
-  float *const wreg = sh_obs + (kStage ? (threadIdx.x >> 6) * kStWave : 0);
-  if constexpr (kStage) {
-    const int64_t fr[4] = {bl0.f0, bl0.f1, bl1.f0, bl1.f1};
-    stage_frame_rows(l.frames, wreg, fr, threadIdx.x & 63);
-    ENV_PHASE(2);
-    const float *rw = wreg + (g & 1) * (4 * kRowF) + b * kRec;
-    rows0 = {load_body(rw), load_body(rw + kRowF)};
-    rows1 = {load_body(rw + 2 * kRowF), load_body(rw + 3 * kRowF)};
-    // the region is reused below (replayed records, obs rows) by other lanes of this wave
-    wave_lds_handoff();
-  } else
-#endif
-  {
-    rows0 = load_rows(l.frames, bl0, b);
-    rows1 = load_rows(l.frames, bl1, b);
-  }
+  BodyRec s = load_body(e.rb + (ei * kBodies + b) * kRec);
+  RowPair rows0 = load_rows(l.frames, bl0, b);
+  RowPair rows1 = load_rows(l.frames, bl1, b);
   const BodyRec ref0 = blend_body(rows0.a, rows0.c, bl0.b, &go);
-
-  float pw_reg = -1.0f;
-  if (REPLAY) {
-    v3 dv, f;
-    s = ref0;
-    v3 dv_ref = {0.0f, 0.0f, 0.0f};
-    if (b >= 1) {
-      const float tb = bl0.b, sb = 1.0f - tb;
-      dv_ref = {sb * dva.x + tb * dvc.x, sb * dva.y + tb * dvc.y, sb * dva.z + tb * dvc.z};
-    }
-    replay_perturb(e, r, ei, b, prog, s, dv_ref, dv, f, rng_val);
-    if constexpr (kStage) {
-#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
-      // the record goes out with the wave's rows at the end; dof vel / force and the PD map here
-      if (lane < kBodies) store_body(wreg + kStRec + (g & 1) * kRowF + b * kRec, s);
-      if (valid && b >= 1) {
-        float *d = e.dof_state + (ei * PHC_NUM_DOF + 3 * (b - 1)) * 2;
-        d[1] = dv.x; d[3] = dv.y; d[5] = dv.z;
-        float *fo = const_cast<float *>(e.dof_force) + ei * PHC_NUM_DOF + 3 * (b - 1);
-        fo[0] = f.x; fo[1] = f.y; fo[2] = f.z;
-      }
-#endif
-    } else if (valid && lane < kBodies) {
-      store_replay(e, ei, b, s, dv, f);
-      map_actions(r, ei, b);
-    }
-    // power: k_env_step's lane j sums the |force x dof vel| of dofs 3j..3j+2, i.e. body j+1's
-    float mine = fabsf(f.x * dv.x);
-    mine = mine + fabsf(f.y * dv.y);
-    mine = mine + fabsf(f.z * dv.z);
-    if (lane >= kBodies) mine = 0.0f;
-    pw_reg = __shfl_down(mine, 1, kGroup);
-    if (lane >= kBodies - 1) pw_reg = 0.0f;
-  }
-
-  const Outcome o = env_reward(e, c, ei, lane, prog, t, m, s, ref0, pw_reg);
-#if PHC_ENV_PHASES
-  if (o.reset == 7) e.rew[0] = 0.0f;
-  ENV_PHASE(3);
-#endif
+  const Outcome o = env_reward(e, c, ei, lane, prog, t, m, s, ref0);
   double st_row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (valid && lane == 0) env_bookkeeping(e, ei, o, st_row);
 
@@ -784,12 +713,7 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
   v3 off1 = go;
   if (AUTO && valid && o.reset) {  // uniform per half-wave
     float mt;
-    float *rec_stage = nullptr;
-#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
-    if (kStage) rec_stage = wreg + kStRec + (g & 1) * kRowF + b * kRec;
-#endif
-    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0, rng_val), &mt,
-                        rec_stage);
+    s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0, rng_val), &mt);
     if (lane == 0) {
       reset_env_counters(e, ei, mt);
       if (e.rng) e.rng[ei] = rng_val + 1u;
@@ -803,45 +727,10 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
     e.reset[ei] = o.reset;
     e.term[ei] = o.terminated;
   }
-#if PHC_ENV_ABLATE == 2  // measurement build: no observation math (the rows still feed a store)
-  if (valid && lane < kBodies) {
-    const BodyRec r1 = blend_body(rows1.a, rows1.c, bl1.b, &off1);
-    e.obs[ei * kObs + lane] = r1.p.x + r1.r.w + r1.v.y + r1.av.z + s.p.x;
-  }
-#elif PHC_ENV_OBS_LDS
-  env_obs_row(kStage ? wreg + (g & 1) * kObs : sh_obs + g * kObs, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1),
-              valid);
-#else
-  env_obs_ref(e, ei, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
-#endif
-
+  env_obs_row(sh_obs + g * kObs, lane, s, blend_body(rows1.a, rows1.c, bl1.b, &off1), valid);
   if (e.stats && lane == 0) {
 #pragma unroll
     for (int k = 0; k < 10; ++k) sh_stats[g][k] = st_row[k];
-  }
-#if PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0
-  if constexpr (kStage) {
-    // the wave writes out its envs' rows (LDS operations of one wave complete in order: the lanes'
-    // row writes above are visible to the copy once their issue order is pinned)
-    wave_lds_handoff();
-    ENV_PHASE(4);
-    const int wl = threadIdx.x & 63;
-    const int64_t env0 = (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6) * kWaveEnvs;
-    const int64_t left = e.n - env0;
-    const int nv = left <= 0 ? 0 : (left < kWaveEnvs ? (int)left : kWaveEnvs);
-    if (nv > 0) {
-      wave_copy_out(e.obs + env0 * kObs, wreg, nv * kObs, wl);
-      wave_copy_out(e.rb + env0 * kRowF, wreg + kStRec, nv * kRowF, wl);
-      if (e.opnd) {
-        if (e.opnd_bf16) operand_rows_out_wave<__bf16>(e, wreg, env0, nv, wl);
-        else operand_rows_out_wave<_Float16>(e, wreg, env0, nv, wl);
-      }
-    }
-    ENV_PHASE(5);
-    if (e.stats) flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
-    ENV_PHASE(6);
-    launch_clock_end(c.clk);
-    return;
   }
   __syncthreads();  // the staged rows and the stats rows are complete
   {
@@ -855,9 +744,212 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
     }
   }
   if (e.stats) flush_stats<kEnvsPerBlock, false>(e, sh_stats, st_prev);
-#else
-  if (e.stats) flush_stats<kEnvsPerBlock>(e, sh_stats, st_prev);
-#endif
+  launch_clock_end(c.clk);
+}
+
+// The fused replay step (HumanoidPHC.step with the physics stand-in, ONE launch): the action -> PD map
+// (R13), the replayed sim state (k_physics_replay: the reference at t plus noise, which is exactly ref0
+// below plus noise, so its frame rows are gathered once) and the post-physics step; the same values as
+// k_actions_to_pd -> k_physics_replay -> k_env_step bit for bit.  kWaves waves per workgroup, each wave
+// with its own LDS region (per-wave staging above) and its own stats row.
+// A passing env (t >= len; it resets in this launch whatever its reward) is known from the scalars: its
+// reset time is drawn before the frame rows are fetched, so the observation rows fetched are already
+// those of the re-initialised env, and its reset-state words are staged while the replay and reward
+// compute.  Before round 6 a resetting env fetched both after its reward, two dependent memory rounds on
+// the waves that hold the launch's tail.  Only a terminated env (rare) still does.
+template <bool AUTO, int kWaves>
+__global__ __launch_bounds__(64 * kWaves, PHC_ENV_WAVES) void k_env_replay(EnvView e, LibView l, StepConsts c,
+                                                                           ReplayArgs r) {
+  constexpr int kEnvs = kWaves * kWaveEnvs;
+  __shared__ double sh_stats[kEnvs][10];
+  __shared__ __attribute__((aligned(16))) float sh_reg[kWaves * kStWave];  // one 2,496-float region per wave
+  const int w = threadIdx.x >> 6, wl = threadIdx.x & 63;
+  const int g = threadIdx.x / kGroup;
+  const int gh = g & 1;  // the env's half of its wave
+  const int64_t env = (int64_t)blockIdx.x * kEnvs + g;
+  const int lane = threadIdx.x % kGroup;
+  const bool valid = env < e.n;
+  const int b = lane < kBodies ? lane : 0;
+  const int64_t ei = valid ? env : 0;
+  float *const wreg = sh_reg + w * kStWave;
+  const int64_t env0 = (int64_t)blockIdx.x * kEnvs + w * kWaveEnvs;  // the wave's first env
+  const int64_t left = e.n - env0;
+  const int nv = left <= 0 ? 0 : (left < kWaveEnvs ? (int)left : kWaveEnvs);
+
+  launch_clock_begin(c.clk);
+  ENV_PHASE(0);
+  const double st_prev = stats_prefetch(e);
+  // R13 for the wave's envs first (elementwise over their contiguous [nv, 69] action span, independent
+  // of everything else: its loads join the first memory round)
+  if (r.actions) {
+    const float *a = r.actions + env0 * PHC_NUM_DOF;
+    float *pd = r.pd + env0 * PHC_NUM_DOF;
+    // every load of the span first (clamped indices, a zero row standing in for a null frozen mask):
+    // loads behind a select or a null check made hipcc wait vmcnt(0) per element
+    constexpr int kPdIt = (kWaveEnvs * PHC_NUM_DOF + 63) / 64;
+    const int cnt = nv * PHC_NUM_DOF;
+    gu8 *fz = r.frozen ? (gu8 *)r.frozen : (gu8 *)kNoFrozen;
+    float av[kPdIt], ov[kPdIt], sv[kPdIt];
+    uint8_t fv[kPdIt];
+#pragma unroll
+    for (int u = 0; u < kPdIt; ++u) {
+      const int i = wl + 64 * u < cnt ? wl + 64 * u : (cnt > 0 ? cnt - 1 : 0);
+      const int d = i >= PHC_NUM_DOF ? i - PHC_NUM_DOF : i;
+      av[u] = a[cnt > 0 ? i : 0];
+      ov[u] = r.off[d];
+      sv[u] = r.scale[d];
+      fv[u] = fz[d];
+    }
+#pragma unroll
+    for (int u = 0; u < kPdIt; ++u) {
+      const int i = wl + 64 * u;
+      if (i >= cnt) break;
+      float x = av[u];
+      if (r.clip) x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+      pd[i] = fv[u] ? 0.0f : ov[u] + sv[u] * x;  // action_to_pd's expression
+    }
+  }
+  // per-env scalars (broadcast loads); the rng counter through a pointer select, so its load joins this
+  // round instead of waiting behind a null check where it is used
+  const uint32_t rng_val = *(e.rng ? (gu32 *)(e.rng + ei) : (gu32 *)&kZeroU32);
+  const int prog = (int)e.progress[ei] + 1;
+  const float st = e.start[ei];
+  const float so = e.start_off[ei];
+  const v3 go = {e.goff[3 * ei], e.goff[3 * ei + 1], e.goff[3 * ei + 2]};
+  const MotionScalars m = load_motion(l, e.motion_ids[ei]);
+  const float t = (float)prog * c.dt + st + so;
+  const Blend bl0 = frame_blend(t, m);
+  // a passing env: reset_env_state's time draw now, its observation at dt + mt (humanoid_phc.py:1061-1065)
+  const bool pass = AUTO && valid && t >= m.len;  // env_reward's pass_time; uniform per half-wave
+  float mt = 0.0f;
+  float tobs = (float)(prog + 1) * c.dt + st + so;  // observation time unless the env resets
+  if (pass) {
+    const float fps_step = 1.0f / 30.0f;  // motion_lib.py:532 curr_fps
+    mt = (float)(int64_t)((reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0, rng_val) * m.len) / fps_step) *
+         fps_step;
+    tobs = (float)(0 + 1) * c.dt + mt + 0.0f;
+  }
+  Blend bl1 = frame_blend(tobs, m);
+  ENV_PHASE_USE(bl1.f0);
+  ENV_PHASE(1);
+
+  // the replay's reference dof velocity rows: loaded before the row DMA's wait, in the same memory
+  // round, and blended after it (ref_dof_vel's arithmetic)
+  v3 dva, dvc;
+  {
+    const int bb = b >= 1 ? b : 1;
+    const float *pa = l.dof_vel + (bl0.f0 * (kBodies - 1) + (bb - 1)) * 3;
+    const float *pc = l.dof_vel + (bl0.f1 * (kBodies - 1) + (bb - 1)) * 3;
+    dva = {pa[0], pa[1], pa[2]};
+    dvc = {pc[0], pc[1], pc[2]};
+  }
+  const int64_t fr[4] = {bl0.f0, bl0.f1, bl1.f0, bl1.f1};
+  stage_frame_rows(l.frames, wreg, fr, wl);
+  ENV_PHASE(2);
+  const float *rw = wreg + gh * (4 * kRowF) + b * kRec;
+  const BodyRec ref0 = blend_body(load_body(rw), load_body(rw + kRowF), bl0.b, &go);
+  // the observation's reference now (13 registers instead of the two rows' 26): offset 0 for a passing
+  // env (a value select: a select of two addresses would put the offsets in scratch)
+  const v3 off1 = {pass ? 0.0f : go.x, pass ? 0.0f : go.y, pass ? 0.0f : go.z};
+  BodyRec ref1 = blend_body(load_body(rw + 2 * kRowF), load_body(rw + 3 * kRowF), bl1.b, &off1);
+  // the region is reused below (reset words, replayed records, obs rows) by other lanes of this wave
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  wave_lds_handoff();
+  Blend blR = {0, 0, 0.0f};
+  const bool any_pass = AUTO && __builtin_amdgcn_ballot_w64(pass) != 0;  // wave-uniform
+  if (any_pass) {
+    if (pass) blR = frame_blend(mt, m);
+    stage_reset_rows(l, wreg, blR, pass, wl);
+  }
+
+  BodyRec s = ref0;
+  v3 dv, f;
+  {
+    v3 dv_ref = {0.0f, 0.0f, 0.0f};
+    if (b >= 1) {
+      const float tb = bl0.b, sb = 1.0f - tb;
+      dv_ref = {sb * dva.x + tb * dvc.x, sb * dva.y + tb * dvc.y, sb * dva.z + tb * dvc.z};
+    }
+    replay_perturb(e, r, ei, b, prog, s, dv_ref, dv, f, rng_val);
+  }
+  // dof vel / force here; the record goes out with the wave's rows at the end
+  if (valid && b >= 1) {
+    float *d = e.dof_state + (ei * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+    d[1] = dv.x; d[3] = dv.y; d[5] = dv.z;
+    float *fo = const_cast<float *>(e.dof_force) + ei * PHC_NUM_DOF + 3 * (b - 1);
+    fo[0] = f.x; fo[1] = f.y; fo[2] = f.z;
+  }
+  // power: k_env_step's lane j sums the |force x dof vel| of dofs 3j..3j+2, i.e. body j+1's
+  float pw_reg;
+  {
+    float mine = fabsf(f.x * dv.x);
+    mine = mine + fabsf(f.y * dv.y);
+    mine = mine + fabsf(f.z * dv.z);
+    if (lane >= kBodies) mine = 0.0f;
+    pw_reg = __shfl_down(mine, 1, kGroup);
+    if (lane >= kBodies - 1) pw_reg = 0.0f;
+  }
+
+  const Outcome o = env_reward(e, c, ei, lane, prog, t, m, s, ref0, pw_reg);
+  ENV_PHASE_USE(o.reset);
+  ENV_PHASE(3);
+  if (lane == 0) {  // the env's log row straight into LDS (not 20 registers held to the end)
+    double st_row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (valid) env_bookkeeping(e, ei, o, st_row);
+    if (e.stats) {
+#pragma unroll
+      for (int k = 0; k < 10; ++k) sh_stats[g][k] = st_row[k];
+    }
+  }
+
+  // ---- in-launch reset (reset_env_state + reset_env_counters) and the observation ----
+  if (any_pass) {  // the passing envs' staged words
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pass) {
+      v3 dp = {0.0f, 0.0f, 0.0f}, dvr = {0.0f, 0.0f, 0.0f};
+      staged_reset_values(wreg, gh, b, blR.b, go, s, dp, dvr);
+      if (b >= 1 && lane < kBodies) {
+        float *d = e.dof_state + (ei * PHC_NUM_DOF + 3 * (b - 1)) * 2;
+        d[0] = dp.x; d[1] = dvr.x; d[2] = dp.y; d[3] = dvr.y; d[4] = dp.z; d[5] = dvr.z;
+      }
+      if (lane == 0 && e.root) store_body(e.root + ei * kRec, s);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the obs rows / records overwrite them
+    wave_lds_handoff();
+  }
+  if (AUTO && valid && o.reset) {  // uniform per half-wave
+    if (!pass) {  // terminated (rare): drawn and loaded now (its record is staged and written out below)
+      s = reset_env_state(e, l, ei, lane, m, reset_draw(e, ei, c.seed, 0ull, c.reset_at_start != 0, rng_val), &mt,
+                          wreg + kStRec + gh * kRowF + b * kRec);
+      const v3 zero = {0.0f, 0.0f, 0.0f};
+      ref1 = ref_body(l.frames, frame_blend((float)(0 + 1) * c.dt + mt + 0.0f, m), b, &zero);
+    }
+    if (lane == 0) {
+      reset_env_counters(e, ei, mt);
+      if (e.rng) e.rng[ei] = rng_val + 1u;
+    }
+  } else if (valid && lane == 0) {
+    e.progress[ei] = (int16_t)prog;
+    e.reset[ei] = o.reset;
+    e.term[ei] = o.terminated;
+  }
+  if (lane < kBodies) store_body(wreg + kStRec + gh * kRowF + b * kRec, s);  // the record, written out below
+  env_obs_row(wreg + gh * kObs, lane, s, ref1, valid);
+  // the wave writes out its envs' rows (LDS operations of one wave complete in order: the lanes' row
+  // writes above are visible to the copy once their issue order is pinned)
+  wave_lds_handoff();
+  ENV_PHASE(4);
+  if (nv > 0) {
+    wave_copy_out(e.obs + env0 * kObs, wreg, nv * kObs, wl);
+    wave_copy_out(e.rb + env0 * kRowF, wreg + kStRec, nv * kRowF, wl);
+    if (e.opnd) {
+      if (e.opnd_bf16) operand_rows_out_wave<__bf16>(e, wreg, env0, nv, wl);
+      else operand_rows_out_wave<_Float16>(e, wreg, env0, nv, wl);
+    }
+  }
+  ENV_PHASE(5);
+  if (e.stats) flush_stats<kEnvs, (kWaves > 1)>(e, sh_stats, st_prev);
+  ENV_PHASE(6);
   launch_clock_end(c.clk);
 }
 
@@ -907,7 +999,6 @@ static int check_env(const phc_env_buffers *e) {
   PHC_REQUIRE((e->episode_return == nullptr) == (e->episode_length == nullptr),
               "env: episode_return and episode_length must both be set or both null");
   if (e->obs_operand) {
-    PHC_REQUIRE(PHC_ENV_OBS_LDS && PHC_ENV_ABLATE == 0, "env: obs_operand needs the LDS-staged obs rows (PHC_ENV_OBS_LDS)");
     PHC_REQUIRE(e->obs_norm_mean && e->obs_norm_var, "env: obs_operand needs the RunningNorm mean and var");
     PHC_REQUIRE(e->obs_operand_ld >= PHC_OBS_DIM && e->obs_operand_ld % 8 == 0 &&
                     (reinterpret_cast<uintptr_t>(e->obs_operand) & 15) == 0,
@@ -922,15 +1013,23 @@ static int check_env(const phc_env_buffers *e) {
 
 using namespace phc;
 
-#if PHC_ENV_PHASES
-extern "C" int phc_env_phase_copy(unsigned long long *dst, int64_t waves) {
-  const int64_t n = (waves < kPhaseWaves ? waves : kPhaseWaves) * 8;
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_env_phase), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) ==
-                 hipSuccess ? 0 : -1;
-}
-#endif
+PHC_ENV_PHASE_COPY
 
-extern "C" int64_t phc_stats_blocks(int64_t num_envs) { return num_envs <= 0 ? 0 : grid_envs(num_envs); }
+// the fused replay step's workgroup shape: kReplayWaves waves (2 envs each) per workgroup, one stats row
+// per workgroup
+#ifndef PHC_REPLAY_WAVES
+#define PHC_REPLAY_WAVES 1
+#endif
+constexpr int kReplayWaves = PHC_REPLAY_WAVES;
+constexpr int kReplayEnvs = kReplayWaves * kWaveEnvs;
+
+// stats rows: one per workgroup of whichever env kernel writes the most (k_env_replay's workgroups hold
+// kReplayEnvs envs, k_env_step's 8)
+extern "C" int64_t phc_stats_blocks(int64_t num_envs) {
+  if (num_envs <= 0) return 0;
+  const int64_t a = grid_envs(num_envs), b = (num_envs + kReplayEnvs - 1) / kReplayEnvs;
+  return a > b ? a : b;
+}
 
 extern "C" int phc_motion_state(const phc_motion_lib *lib, const int64_t *ids, const float *times,
                                 const float *offset, int64_t n, phc_ref_state *out, void *stream) {
@@ -1064,13 +1163,12 @@ extern "C" int phc_env_step_timed(const phc_env_buffers *env, const phc_motion_l
   const LibView lv = lib_view(lib);
   StepConsts cs = make_consts(p);
   cs.clk = phc_timer_take(timer, st, grid.x, (double)env->num_envs);  // work: env-steps
-  const ReplayArgs none{};
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot && lib->dof_vel, "env_step: auto_reset needs local_rot and dof_vel");
     PHC_REQUIRE(env->rng_counter, "env_step: auto_reset needs rng_counter");
-    phc_launch(k_env_step<true, false>, grid, block, 0, st, ev, lv, cs, none);
+    phc_launch(k_env_step<true>, grid, block, 0, st, ev, lv, cs);
   } else {
-    phc_launch(k_env_step<false, false>, grid, block, 0, st, ev, lv, cs, none);
+    phc_launch(k_env_step<false>, grid, block, 0, st, ev, lv, cs);
   }
   return check_launch("env_step");
 }
@@ -1086,7 +1184,7 @@ extern "C" int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_
   ReplayArgs ra{rp->pos_sigma, rp->force_scale, (unsigned long long)rp->seed, (unsigned long long)rp->counter,
                 pd ? pd->actions : nullptr, pd ? pd->pd_target : nullptr, pd ? pd->offset : nullptr,
                 pd ? pd->scale : nullptr, pd ? pd->frozen : nullptr, pd ? pd->clip : 1};
-  const dim3 block(kBlock), grid(grid_envs(env->num_envs));
+  const dim3 block(64 * kReplayWaves), grid((unsigned)((env->num_envs + kReplayEnvs - 1) / kReplayEnvs));
   hipStream_t st = as_stream(stream);
   const EnvView ev = env_view(env);
   const LibView lv = lib_view(lib);
@@ -1095,9 +1193,9 @@ extern "C" int phc_env_step_replay(const phc_env_buffers *env, const phc_motion_
   if (p->auto_reset) {
     PHC_REQUIRE(lib->local_rot, "env_step_replay: auto_reset needs local_rot");
     PHC_REQUIRE(env->rng_counter, "env_step_replay: auto_reset needs rng_counter");
-    phc_launch(k_env_step<true, true>, grid, block, 0, st, ev, lv, cs, ra);
+    phc_launch(k_env_replay<true, kReplayWaves>, grid, block, 0, st, ev, lv, cs, ra);
   } else {
-    phc_launch(k_env_step<false, true>, grid, block, 0, st, ev, lv, cs, ra);
+    phc_launch(k_env_replay<false, kReplayWaves>, grid, block, 0, st, ev, lv, cs, ra);
   }
   return check_launch("env_step_replay");
 }

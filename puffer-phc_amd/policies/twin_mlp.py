@@ -272,7 +272,7 @@ def mfma_trunk_forward(x, weights, need_grad):
         pre = torch.empty((M, 2 * n1), dtype=pdt, device=x.device) if need_grad else None
         epi_fwd = N.EPI_BIAS_SILU_D if (need_grad and SILU_DERIV) else N.EPI_BIAS_SILU
         N.twin_gemm(xc, ops.w0, epi_fwd, z, (2, n1), bias=B[0], aux=pre, aux_layout=N.SPLIT,
-                    out_layout=N.GROUPED)
+                    out_layout=N.GROUPED, k_valid=K0)
         pres, zs = [pre], [z]
         L = len(ops.w) + 1
         for l in range(1, L):

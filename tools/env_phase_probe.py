@@ -1,7 +1,8 @@
-"""Where one fused env step's time goes, per wave (measurement build PHC_ENV_PHASES=1: lane 0 of every wave
-stamps the 100 MHz constant clock at the phase boundaries of k_env_step; phc_env_phase_copy reads them).
+"""Where one fused env step's time goes, per wave (measurement build, csrc/phc_measure.h: lane 0 of every wave
+stamps the 100 MHz constant clock at the phase boundaries of k_env_replay; phc_env_phase_copy reads them).
 
-usage: PHC_HIP_LIB=.../libphc_hip_phases.so python tools/env_phase_probe.py [envs ...]
+usage: tools/build_variants.sh phases "-DPHC_MEASURE_ENV_PHASES=1"
+       PHC_HIP_LIB=.../libphc_hip_phases.so python tools/env_phase_probe.py [envs ...]
 Prints, per env count, the launch span and the median / p90 of each phase's duration over the waves, and
 when the waves start relative to the first one (waves that start late queued behind earlier ones).
 """
@@ -52,6 +53,11 @@ def main():
             print(f"envs {envs}: span {span:.2f} us over {waves} waves; wave start offset median {np.median(start):.2f} "
                   f"p90 {np.percentile(start, 90):.2f} max {start.max():.2f} us; wave life median "
                   f"{np.median((r[:, 6] - r[:, 0]) / 100.0):.2f} us")
+            life = (r[:, 6] - r[:, 0]) / 100.0
+            end = (r[:, 6] - t0) / 100.0
+            print(f"   wave life p90 {np.percentile(life, 90):.2f} p99 {np.percentile(life, 99):.2f} max {life.max():.2f} us; "
+                  f"wave end median {np.median(end):.2f} p90 {np.percentile(end, 90):.2f} p99 {np.percentile(end, 99):.2f} "
+                  f"max {end.max():.2f} us")
             for k, name in enumerate(NAMES):
                 print(f"   {name:14s} median {np.median(d[:, k]):6.2f}  p90 {np.percentile(d[:, k], 90):6.2f} us")
 
