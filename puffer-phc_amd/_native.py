@@ -8,6 +8,7 @@ any op raises.
 """
 
 import ctypes
+import itertools
 import os
 
 import numpy as np
@@ -487,7 +488,11 @@ class KernelTimer:
     and wave ends from the device's constant-rate clock): no event is recorded around the dispatch,
     and launches inside a captured hipGraph are timed too (a graph's slots hold its last replay)."""
 
+    _serials = itertools.count(1)
+
     def __init__(self, capacity=4096, period=1):
+        # never reused (unlike id() or the handle's address): the key of graphs whose launches stamp into it
+        self.serial = next(KernelTimer._serials)
         self.handle = lib().phc_timer_create(int(capacity))
         if not self.handle:
             _check(-1, "phc_timer_create")
@@ -545,7 +550,7 @@ def gemm_set_timer(timer):
 def gemm_timer_id():
     """Identity of the timer set by gemm_set_timer (a captured graph's key: its launches carry
     that timer's slots, or none)."""
-    return id(_GEMM_TIMER[0]) if _GEMM_TIMER[0] is not None else None
+    return _GEMM_TIMER[0].serial if _GEMM_TIMER[0] is not None else None
 
 
 def reset_envs(env_c, mlib, params, mask=None, phase=None, seed=0, counter=0, num_envs=None):

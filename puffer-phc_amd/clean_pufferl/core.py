@@ -231,10 +231,12 @@ class RolloutStep:
             self._noise_block = torch.zeros(shape, device=self.noise.device)
         noise = self._noise_block[:steps]
         noise.normal_()
-        self.env.block_stats(steps)
+        stats_buf = self.env.block_stats(steps)
         # the captured step launches hold the env / library / step-parameter structs by value: a
-        # resample_motions() (a new packed library) or an eval toggle invalidates every block
-        key = self.env.env.launch_key()
+        # resample_motions() (a new packed library) or an eval toggle invalidates every block; so does a
+        # reallocated noise or logging buffer (the graphs hold their addresses) and another kernel timer
+        # (each captured env-step launch stamps into its timer's buffer)
+        key = (self.env.env.launch_key(), self._noise_block.data_ptr(), stats_buf.data_ptr())
         if key != self._blocks_key:
             self._blocks.clear()
             self._blocks_key = key
@@ -675,7 +677,10 @@ def _train_graph_key(components, info, pol):
             cfg.update_epochs, cfg.norm_adv, float(cfg.max_grad_norm), float(cfg.clip_coef), float(cfg.vf_clip_coef),
             float(cfg.vf_coef), float(cfg.ent_coef), float(cfg.bound_coef), bool(cfg.clip_vloss), cfg.precision,
             id(components.optimizer), components.optimizer.use_loss_scale, _native.gemm_timer_id(),
-            weight_cache.layout_key(None, list(pol.parameters())), weight_cache.plans_version())
+            weight_cache.layout_key(None, list(pol.parameters())), weight_cache.plans_version(),
+            # the step kernel receives betas / eps / the hyper-parameter scales by value (lr is device state)
+            tuple(components.optimizer.param_groups[0]["betas"]), float(components.optimizer.param_groups[0]["eps"]),
+            tuple(components.optimizer._hp_scale))
 
 
 def _train_minibatches_graphed(components, info, pol):
@@ -689,6 +694,15 @@ def _train_minibatches_graphed(components, info, pol):
     opt.sync_lr()
     if st["graph"] is not None and st["key"] == key:
         fresh = opt.fresh_operand_owners() if st["writes_operands"] else []
+        if st["writes_operands"]:
+            # the graph's first minibatch reads the GEMM operand copies as they are (its capture saw them
+            # current, so it holds no refresh launch): re-pack any a parameter write outside the captured
+            # Adam steps left stale (load_state_dict, a parameter broadcast, a manual copy)
+            for o in opt._ops_owners:
+                if not any(o is f for f in fresh):
+                    o.plan.run()
+                    weight_cache.mark_fresh(o)
+                    fresh.append(o)
         st["graph"].replay()
         _native.GEMM_LAUNCHES[0] += st["gemm_launches"]
         # the replay rewrote the parameters behind every host-side cache key (FlatAdam.fused_step

@@ -308,11 +308,16 @@ class HumanoidPHC:
     def launch_key(self):
         """Everything a captured step launch holds by value: the env struct, the packed library's
         descriptor (replaced by resample_motions / the eval toggles) and both step-parameter blocks.
-        A graph captured under another key replays stale pointers."""
+        A graph captured under another key replays stale pointers.  The kernel timer (by its never-reused
+        serial) is part of the key: a graph must not stamp into a timer that was replaced or freed."""
         parts = [bytes(self._env_c), bytes(self._motion_lib.packed.c), bytes(self._step_params)]
         auto = getattr(self, "_step_params_auto", None)
         if auto is not None:
             parts.append(bytes(auto))
+        # a captured step launch stamps into its kernel timer's buffer (or into none): another timer, or
+        # none, needs other launches
+        timer = self.kernel_timer
+        parts.append(str(timer.serial if timer is not None else 0).encode())
         return b"".join(parts)
 
     def stats_env_struct(self, stats):

@@ -119,6 +119,15 @@ class ClipPool:
 
     CHUNK_FRAMES = 1 << 18  # host staging per upload (about 200 MB of float64 rows)
 
+    @staticmethod
+    def footprint(clips):
+        """Device bytes the pool of `clips` takes: float64 quat [24, 4] + trans [3] + aa [A] per frame."""
+        frames = sum(int(c["root_trans_offset"].shape[0]) for c in clips)
+        j = int(np.asarray(clips[0]["pose_quat_global"]).shape[1])
+        n0 = int(clips[0]["root_trans_offset"].shape[0])
+        a = int(np.asarray(clips[0]["pose_aa"]).reshape(n0, -1).shape[1])
+        return 8 * frames * (4 * j + 3 + a)
+
     def __init__(self, clips, device):
         n = len(clips)
         self.lens = np.fromiter((c["root_trans_offset"].shape[0] for c in clips), np.int64, n)
@@ -168,6 +177,11 @@ class ClipPool:
 # PHC_MOTION_POOL=0: the per-clip host loop for in-memory libraries too (the directory mode, whose
 # clips load from disk one by one, always takes it)
 MOTION_POOL = os.environ.get("PHC_MOTION_POOL", "1") != "0"
+# the pool is built only when it takes at most this share of the device memory free at the first load
+# (else the per-clip loop): float64 rows, 8 * (24 * 4 + 3 + A) bytes per frame (~1.4 KB for A = 72); the
+# 11,313-clip AMASS library (~40 M frames) would be ~55 GB, well inside 288 GB, which an 8-rank node pays
+# once per rank
+POOL_MAX_FREE_FRACTION = float(os.environ.get("PHC_MOTION_POOL_MAX_FREE_FRACTION", "0.5"))
 
 
 class MotionLibBase:
@@ -238,10 +252,20 @@ class MotionLibBase:
         max_length = self.m_cfg.max_length
         randomize = not (self.m_cfg.is_deterministic or self.m_cfg.im_eval)
         dev = self._device
+        pool = None
         if MOTION_POOL and self.mode == MotionlibMode.file and isinstance(self._motion_data_list[0], dict):
             pool = getattr(self, "_pool", None)
-            if pool is None:
-                pool = self._pool = ClipPool(self._motion_data_list, dev)
+            if pool is None:  # first load: build it when it fits (else False: the per-clip loop from now on)
+                need = ClipPool.footprint(self._motion_data_list)
+                if str(dev).startswith("cuda"):
+                    free = torch.cuda.mem_get_info(dev)[0]
+                else:  # a host-memory pool (tests)
+                    import psutil
+
+                    free = psutil.virtual_memory().available
+                pool = self._pool = ClipPool(self._motion_data_list, dev) if need <= POOL_MAX_FREE_FRACTION * free \
+                    else False
+        if pool:
             lens = pool.lens[ids]
             start = np.zeros(len(ids), np.int64)
             counts = lens.copy()

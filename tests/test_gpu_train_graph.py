@@ -64,3 +64,39 @@ def test_graphed_train_matches_eager(monkeypatch):
     st = graphed[1].__dict__.get("_train_graph")
     assert st is not None and st["graph"] is not None and not st["failed"]
     assert eager[1].__dict__.get("_train_graph") is None
+
+
+def test_graphed_train_follows_parameter_writes_between_replays(monkeypatch):
+    """A parameter write outside the captured Adam steps between two replays (here a policy
+    load_state_dict of perturbed weights, as a checkpoint restore does; also a changed Adam eps and
+    betas) must reach the replayed update: the graph's first minibatch reads the GEMM operand copies,
+    which the replay path re-packs when they went stale, and the optimizer's by-value
+    hyper-parameters are part of the graph key.  Bit-equal to the eager trainer after the write."""
+    from puffer_phc_amd.clean_pufferl import core
+
+    eager = _trainer()
+    graphed = _trainer()
+    for it in range(7):
+        if it == 4:  # after the graph has been captured (call 2) and replayed (call 3)
+            st = graphed[1].__dict__.get("_train_graph")
+            assert st is not None and st["graph"] is not None
+            g = torch.Generator(device=DEV).manual_seed(11)
+            sd = {k: v.clone() for k, v in eager[3].state_dict().items()}
+            for k, v in sd.items():
+                if v.is_floating_point() and "running" not in k and "weight" in k:
+                    v.add_(torch.randn(v.shape, generator=g, device=DEV) * 1e-3)
+            for tr in (eager, graphed):
+                tr[3].load_state_dict(sd)
+        if it == 5:
+            for tr in (eager, graphed):
+                pg = tr[1].optimizer.param_groups[0]
+                pg["eps"], pg["betas"] = 1e-6, (0.85, 0.99)
+        monkeypatch.setattr(core, "TRAIN_GRAPH", False)
+        la = _iterate(*eager, seed=200 + it)
+        monkeypatch.setattr(core, "TRAIN_GRAPH", True)
+        lb = _iterate(*graphed, seed=200 + it)
+        for k in la:
+            assert (la[k] == lb[k]) or (la[k] != la[k] and lb[k] != lb[k]), (it, k, la[k], lb[k])
+        pa = dict(eager[3].named_parameters())
+        for n, p in graphed[3].named_parameters():
+            assert torch.equal(p, pa[n]), (it, n)

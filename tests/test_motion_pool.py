@@ -77,3 +77,21 @@ def test_pool_chunked_upload(monkeypatch):
         np.testing.assert_array_equal(pool.quat[s:s + n].numpy(), c["pose_quat_global"])
         np.testing.assert_array_equal(pool.trans[s:s + n].numpy(), c["root_trans_offset"].numpy())
         np.testing.assert_array_equal(pool.aa[s:s + n].numpy(), c["pose_aa"].reshape(n, -1))
+
+
+def test_pool_falls_back_to_the_loop_when_it_does_not_fit(monkeypatch):
+    """the pool is built only when it fits the free-memory budget; else the per-clip loop
+    (same values) and no pool."""
+    clips = _clips(9)
+    ids = np.array([0, 3, 8, 8])
+    monkeypatch.setattr(ML, "MOTION_POOL", True)
+    monkeypatch.setattr(ML, "POOL_MAX_FREE_FRACTION", 0.0)
+    lib = _lib(clips, -1, True)
+    out = lib._gather_clips(ids)
+    assert lib._pool is False
+    monkeypatch.setattr(ML, "MOTION_POOL", False)
+    ref = _lib(clips, -1, True)._gather_clips(ids)
+    for x, y in zip(out[:3], ref[:3]):
+        assert torch.equal(x, y)
+    frames = sum(c["root_trans_offset"].shape[0] for c in clips.values())
+    assert ML.ClipPool.footprint(list(clips.values())) == 8 * frames * (24 * 4 + 3 + 72)
