@@ -136,6 +136,9 @@ def parse():
     ap.add_argument("--traffic-file", default=None)
     ap.add_argument("--dp-mode", choices=["grouped", "per_layer", "split"], default="grouped",
                     help="data-parallel weight-gradient / all-reduce schedule at N > 1 (twin_mlp.set_dp_mode)")
+    ap.add_argument("--dist-1rank", action="store_true",
+                    help="run the data-parallel path on ONE GPU: a 1-rank RCCL group (every gradient / advantage "
+                         "all-reduce of an N-GPU rank, on one process), to time the DP path beside the headline")
     a = ap.parse_args()
     k, w = DEFAULTS[a.mode]
     a.steps = k if a.steps is None else a.steps
@@ -143,12 +146,23 @@ def parse():
     return a
 
 
-def setup_dist():
+def setup_dist(dist_1rank=False):
     from puffer_phc_amd import distributed as D
 
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # RCCL over xGMI; PHC_DIST_BACKEND=gloo rehearses several ranks on one GPU
         D.init_from_env(os.environ.get("PHC_DIST_BACKEND", "nccl"))
+    elif dist_1rank:
+        # a 1-rank RCCL group, initialised before any other GPU call (the rendezvous on the loopback)
+        import socket
+
+        if "MASTER_PORT" not in os.environ:
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0")):
+            os.environ.setdefault(k, v)
+        D.init_from_env("nccl", force=True)
     else:
         torch.cuda.set_device(0)
     return D.world_size(), D.rank()
@@ -476,10 +490,11 @@ class Runner:
 
 
 DP_FIELDS = ("mode", "backend", "allreduce_exposed_ms_per_minibatch_rank0",
-             "allreduce_exposed_ms_per_minibatch_max_rank", "minibatches_timed", "grad_bytes_per_minibatch", "note")
+             "allreduce_exposed_ms_per_minibatch_max_rank", "minibatches_timed", "grad_bytes_per_minibatch",
+             "train_graph", "dist_1rank", "note")
 
 
-def dp_summary(mode, exp_ms, n_bw, grad_bytes, device):
+def dp_summary(mode, exp_ms, n_bw, grad_bytes, device, train_graph=False, dist_1rank=False):
     """config.dp at N > 1 (collective: every rank calls it): the exposed all-reduce wait per minibatch
     backward on this rank (rank 0's goes in the line) and on the slowest rank."""
     e = torch.tensor([exp_ms or 0.0], dtype=torch.float64, device=device)
@@ -487,7 +502,7 @@ def dp_summary(mode, exp_ms, n_bw, grad_bytes, device):
     return {"mode": mode, "backend": torch.distributed.get_backend(),
             "allreduce_exposed_ms_per_minibatch_rank0": exp_ms,
             "allreduce_exposed_ms_per_minibatch_max_rank": float(e[0]), "minibatches_timed": n_bw,
-            "grad_bytes_per_minibatch": grad_bytes,
+            "grad_bytes_per_minibatch": grad_bytes, "train_graph": bool(train_graph), "dist_1rank": bool(dist_1rank),
             "note": "CUDA events on rank's compute stream around the wait for the backward's all-reduces "
                     "(FlatGrads.overlap_finish): the stall after the last backward kernel"}
 
@@ -519,7 +534,10 @@ def main():
         import faulthandler
 
         faulthandler.dump_traceback_later(float(os.environ["PHC_WATCHDOG_S"]), repeat=True)
-    world, rank = setup_dist()
+    world, rank = setup_dist(args.dist_1rank)
+    from puffer_phc_amd import distributed as D
+
+    dp_on = D.is_dist()  # the data-parallel path runs (N > 1, or --dist-1rank)
     from puffer_phc_amd.policies import twin_mlp
 
     twin_mlp.set_dp_mode(args.dp_mode)
@@ -550,7 +568,7 @@ def main():
         if tm is not None:
             tm.reset()
     flat = getattr(getattr(runner, "components", None), "flat_grads", None)
-    if flat is not None and world > 1:
+    if flat is not None and dp_on:
         flat.timing, flat.exposed = True, []
     if world > 1:
         torch.distributed.barrier()
@@ -596,10 +614,13 @@ def main():
     elapsed, kern_s = float(t[0]), float(t[1])
     processed_all = whole_job_steps(counts, args.mode == "ppo", world)
     dp = None
-    if flat is not None and world > 1:
+    if flat is not None and dp_on:
         exp_ms, n_bw = flat.exposed_ms()
         flat.timing = False
-        dp = dp_summary(args.dp_mode, exp_ms, n_bw, flat.flat.numel() * 4, device)
+        st = getattr(runner.components, "_train_graph", None)
+        dp = dp_summary(args.dp_mode, exp_ms, n_bw, flat.flat.numel() * 4, device,
+                        train_graph=bool(st and st.get("graph") is not None and not st.get("failed")),
+                        dist_1rank=args.dist_1rank)
 
     if rank == 0:
         fused = bool(getattr(env.env, "fused_env_step", False)) and args.physics == "replay"
@@ -705,7 +726,7 @@ def main():
         else:
             out["roofline"] = env_roof
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dp_on:
         torch.distributed.destroy_process_group()
 
 

@@ -244,7 +244,7 @@ class RolloutStep:
         if g is None:
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with _capture(g):
                 for k in range(steps):
                     self._body(noise=noise[k])
                     self.env.block_step(self.actions, k)
@@ -268,7 +268,7 @@ class RolloutStep:
         else:
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with _capture(g):
                 self._body()
             self.graph = g
             g.replay()
@@ -277,6 +277,15 @@ class RolloutStep:
             # (the buffer is read only by the next replay, stream-ordered after this draw)
             self.noise.normal_()
             self._noise_ready = True
+
+
+def _capture(g):
+    """torch.cuda.graph(g); under data parallelism in relaxed capture mode: RCCL's watchdog thread
+    queries its (pre-capture) works' events while a capture runs, which the default global mode turns
+    into hipErrorStreamCaptureUnsupported and an abort of the process.  (Thread-local mode does not
+    serve: the backward's kernels are launched into the capturing stream by autograd's device thread.)
+    Every capture here was validated in global mode, which rejects unsafe calls of any thread."""
+    return torch.cuda.graph(g, capture_error_mode="relaxed" if D.is_dist() else "global")
 
 
 def _global_count(n, device):
@@ -577,7 +586,7 @@ def _compute_advantages_train(components, info):
     try:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _capture(g):
             out = compute_advantages(components, info)
     except Exception:  # noqa: BLE001  (an op that cannot be captured: stay eager)
         st["failed"] = True
@@ -608,17 +617,23 @@ def _fill_losses(losses, a):
 
 # train()'s minibatch loop (update_epochs x num_minibatches fused minibatches: trunks, tail, PPO
 # objective, backward, clip + Adam) and the logged loss row replayed from ONE captured hipGraph: the
-# ~40 launches per minibatch run back to back with no host in between.  Eligible: the single-process
-# fused path with FlatAdam and the reference's defaults (no AMP, no recurrent policy, no target-KL early
-# stop, no L2-init loss, the bound term a no-grad constant), once train()'s advantage pass itself
-# replays from its graph (fixed input addresses).  PHC_TRAIN_GRAPH=0: eager.
+# ~40 launches per minibatch run back to back with no host in between.  Eligible: the fused path with
+# FlatAdam and the reference's defaults (no AMP, no recurrent policy, no target-KL early stop, no
+# L2-init loss, the bound term a no-grad constant), once train()'s advantage pass itself replays from
+# its graph (fixed input addresses).  Data parallel (round 6): the graph holds the RCCL collectives too
+# -- the per-train() advantage statistics all-reduce and every minibatch's gradient-span all-reduces,
+# forked onto RCCL's stream by the backward's readiness hook and joined before the optimizer step
+# (FlatGrads.overlap_begin / overlap_finish) -- so every rank replays the same collective sequence.
+# PHC_TRAIN_GRAPH=0: eager; PHC_DP_TRAIN_GRAPH=0: eager under data parallelism only.
 TRAIN_GRAPH = os.environ.get("PHC_TRAIN_GRAPH", "1") != "0"
+DP_TRAIN_GRAPH = os.environ.get("PHC_DP_TRAIN_GRAPH", "1") != "0"
 
 
 def _train_graph_eligible(components, info, pol):
     cfg, exp, opt = info.config, components.experience, components.optimizer
     adv = getattr(components, "_adv_graph", None)
-    if not (TRAIN_GRAPH and exp.obs.is_cuda and not info.use_amp_obs and exp.lstm_h is None and not D.is_dist()
+    if not (TRAIN_GRAPH and exp.obs.is_cuda and not info.use_amp_obs and exp.lstm_h is None
+            and (not D.is_dist() or (DP_TRAIN_GRAPH and D.backend() == "nccl"))
             and isinstance(opt, FlatAdam) and opt.param_init is not None and cfg.l2_reg_coef == 0
             and cfg.target_kl is None and not cfg.bound_loss_grad and STORE_GRADS and cfg.fused_loss
             and adv is not None and adv.get("replayed") and getattr(exp, "b_obs_half", None) is not None
@@ -636,6 +651,7 @@ def _fused_update(components, info, pol):
     fused_mb and opt_l2) and the loss row; returns the row (device float64 [14]).  Captured into the
     train graph, or run eagerly (first sight of a configuration)."""
     cfg, exp, opt = info.config, components.experience, components.optimizer
+    flat = components.flat_grads
     dev = exp.obs.device
     acc_ppo = torch.zeros(7, dtype=torch.float64, device=dev)
     acc_opt = torch.zeros(3, dtype=torch.float64, device=dev)
@@ -658,7 +674,9 @@ def _fused_update(components, info, pol):
                 loss, st = fused_ppo_loss(pol, obs, atn, exp.b_logprobs[mb].reshape(-1), exp.b_advantages[mb],
                                           adv_ms[mb] if cfg.norm_adv else unit, exp.b_values[mb], exp.b_returns[mb],
                                           coefs, store_grads=True, stats_acc=acc_ppo)
+            flat.overlap_begin()  # data parallel: the gradient spans' all-reduces as the backward finishes them
             opt.backward(loss)
+            flat.overlap_finish()
             opt.fused_step(cfg.max_grad_norm, norm_acc=acc_opt)
     with torch.no_grad():
         acc = torch.zeros(12, dtype=torch.float64, device=dev)
@@ -668,6 +686,12 @@ def _fused_update(components, info, pol):
         if mbl_ref is not None:
             acc[9] = mbl_ref.double()
         return torch.cat([acc, exp.ev_pair])
+
+
+def _dp_mode_key():
+    from ..policies import twin_mlp
+
+    return twin_mlp.dp_mode()
 
 
 def _train_graph_key(components, info, pol):
@@ -680,7 +704,9 @@ def _train_graph_key(components, info, pol):
             weight_cache.layout_key(None, list(pol.parameters())), weight_cache.plans_version(),
             # the step kernel receives betas / eps / the hyper-parameter scales by value (lr is device state)
             tuple(components.optimizer.param_groups[0]["betas"]), float(components.optimizer.param_groups[0]["eps"]),
-            tuple(components.optimizer._hp_scale))
+            tuple(components.optimizer._hp_scale),
+            # data parallel: the collectives are captured too (the readiness schedule of the DP mode)
+            D.is_dist(), D.world_size(), _dp_mode_key())
 
 
 def _train_minibatches_graphed(components, info, pol):
@@ -717,7 +743,7 @@ def _train_minibatches_graphed(components, info, pol):
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         launches0 = _native.GEMM_LAUNCHES[0]
-        with torch.cuda.graph(g):
+        with _capture(g):
             row = _fused_update(components, info, pol)
         st["gemm_launches"] = _native.GEMM_LAUNCHES[0] - launches0
     except Exception:  # noqa: BLE001  (an op that cannot be captured: stay eager)

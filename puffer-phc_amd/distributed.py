@@ -24,6 +24,11 @@ def is_dist():
     return dist.is_available() and dist.is_initialized()
 
 
+def backend():
+    """The process group's backend ("nccl" = RCCL on ROCm, "gloo"), None without a group."""
+    return dist.get_backend() if is_dist() else None
+
+
 def world_size():
     return dist.get_world_size() if is_dist() else 1
 
@@ -128,7 +133,8 @@ class FlatGrads:
         if rest:
             self._on_ready(rest)
         ev = None
-        if self.timing and self.flat.is_cuda:
+        # (timing events cannot be recorded inside a captured graph: a captured backward is not timed)
+        if self.timing and self.flat.is_cuda and not torch.cuda.is_current_stream_capturing():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         for w in self._works:

@@ -191,3 +191,39 @@ def test_rccl_ppo_iteration_matches_single_gpu(rccl, monkeypatch):
     diff = (p_dp - p_1).abs()
     assert float(diff.max()) <= 2.5e-4
     assert float((diff > 1e-6).float().mean()) < 1e-3
+
+
+@pytest.mark.parametrize("mode", ["grouped", "split"])
+def test_rccl_graphed_dp_train_matches_eager_dp(rccl, monkeypatch, mode):
+    """train()'s minibatch loop captured WITH its RCCL collectives (the per-train()
+    advantage-statistics all-reduce, every minibatch's gradient-span all-reduces forked onto RCCL's
+    stream by the backward and joined before the optimizer step) replays bit for bit like the eager
+    data-parallel loop of the same launches, over several iterations (eager, capture, replays) — at
+    world size 1 over RCCL, the data-parallel path of every rank of a node.  The graph is really
+    used (the train graph state records a captured graph, not a fallback)."""
+    from puffer_phc_amd.clean_pufferl import core
+    from puffer_phc_amd.policies import twin_mlp
+
+    from test_gpu_train_graph import _iterate, _trainer
+
+    old = twin_mlp.dp_mode()
+    twin_mlp.set_dp_mode(mode)
+    try:
+        eager = _trainer()
+        graphed = _trainer()
+        for it in range(5):
+            monkeypatch.setattr(core, "TRAIN_GRAPH", False)
+            la = _iterate(*eager, seed=300 + it)
+            monkeypatch.setattr(core, "TRAIN_GRAPH", True)
+            lb = _iterate(*graphed, seed=300 + it)
+            for k in la:
+                assert (la[k] == lb[k]) or (la[k] != la[k] and lb[k] != lb[k]), (it, k, la[k], lb[k])
+            pa = dict(eager[3].named_parameters())
+            for n, p in graphed[3].named_parameters():
+                assert torch.equal(p, pa[n]), (it, n)
+            oa, ob = eager[1].optimizer, graphed[1].optimizer
+            assert torch.equal(oa.exp_avg, ob.exp_avg) and torch.equal(oa.exp_avg_sq, ob.exp_avg_sq), it
+        st = graphed[1].__dict__.get("_train_graph")
+        assert st is not None and st["graph"] is not None and not st["failed"], "the DP train graph was not captured"
+    finally:
+        twin_mlp.set_dp_mode(old)
