@@ -30,6 +30,8 @@
 // XCD's L2 walk the column tiles of the same A row panel.  m and n may be ragged (loads clamp
 // to the last row, stores are masked); k must be a multiple of 64.
 #include "phc_common.h"
+#define PHC_MEASURE_GEMM_ONLY
+#include "phc_measure.h"  // PHC_GEMM_PROBE / phc_gemm_discard(): measurement builds only
 
 #include <hip/hip_ext.h>
 
@@ -58,12 +60,6 @@ constexpr int kGBK = 64;
 #endif
 #ifndef PHC_GEMM_SPLIT_DMA
 #define PHC_GEMM_SPLIT_DMA 2
-#endif
-// measurement builds only (tools/build_variants.sh): 1 = every tile stages the operand panels of
-// tile (0, 0) (L2-hot operands, same instruction stream); 2 = only the first K-tile is staged (LDS
-// fragment reads + MFMA, no operand traffic)
-#ifndef PHC_GEMM_PROBE
-#define PHC_GEMM_PROBE 0
 #endif
 // 256 x 256 tiles: the second wave of every SIMD (waves 4-7) issues its share of the next K-tile's
 // DMA at MFMA groups PHC_GEMM_STG_A / _B instead of with waves 0-3, so one wave of each SIMD keeps
@@ -1654,12 +1650,7 @@ extern "C" int phc_twin_gemm(const phc_gemm_desc *d, float *bias_grad, void *wor
   g.partial = static_cast<float *>(workspace);  // per-m-tile bias-gradient column sums (grad epilogues)
   g.tiles_m = (int)tiles_m;
   g.tiles_n = (int)tiles_n;
-  // measurement aid: 1 = main loop only, 2 = the whole epilogue but no global stores
-  static const int discard = [] {
-    const char *e = getenv("PHC_GEMM_DISCARD");
-    return e ? (atoi(e) == 2 ? 2 : 1) : 0;
-  }();
-  g.discard = discard;
+  g.discard = phc_gemm_discard();  // 0 in a product build (phc_measure.h)
   // Non-temporal epilogue traffic: an output of a whole PPO minibatch (tens to hundreds of MB,
   // far past the 4 MB per-XCD L2) streams out without evicting the operand panels the other CUs
   // are still re-reading; the pre-activation (written by the forward, read back once by the backward) always does.  Small
@@ -1719,8 +1710,7 @@ extern "C" int phc_weight_grad(const phc_wgrad_desc *d, void *stream) {
   g.tiles_m = (int)tiles_m;
   g.tiles_n = (int)tiles_n;
   g.out = d->out;
-  static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
-  g.discard = discard ? 1 : 0;
+  g.discard = phc_gemm_discard() ? 1 : 0;
   hipStream_t st = as_stream(stream);
   g.clk = phc_timer_take(g_gemm_timer, st, blocks, 2.0 * (double)d->m * d->n * d->rows * d->batch);
   if (d->dtype == PHC_DT_F16) launch_wgrad<_Float16>(g, blocks, st);
@@ -1776,8 +1766,7 @@ extern "C" int phc_weight_grad_group(const phc_wgrad_problem *probs, int32_t cou
   ga.count = count;
   ga.accumulate = accumulate ? 1 : 0;
   ga.rows = rows;
-  static const bool discard = getenv("PHC_GEMM_DISCARD") != nullptr;  // measurement aid
-  ga.discard = discard ? 1 : 0;
+  ga.discard = phc_gemm_discard() ? 1 : 0;
   hipStream_t st = as_stream(stream);
   ga.clk = phc_timer_take(g_gemm_timer, st, blocks, flops);
   if (dtype == PHC_DT_F16) launch_wgrad_group<_Float16>(ga, blocks, st);

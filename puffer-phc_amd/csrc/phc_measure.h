@@ -1,5 +1,6 @@
-// phc_measure.h — measurement-only instrumentation of the env kernels (never part of a product build).
-// A product build (Makefile default) defines nothing here: ENV_PHASE / ENV_PHASE_USE expand to nothing
+// phc_measure.h — measurement-only instrumentation of the env and GEMM kernels (never part of a product
+// build).
+// Env kernels.  A product build (Makefile default) defines nothing here: ENV_PHASE / ENV_PHASE_USE expand to nothing
 // and phc_env_phase_copy is absent from the library.  tools/build_variants.sh builds the measurement
 // library with -DPHC_MEASURE_ENV_PHASES=1: lane 0 of every wave of k_env_replay stamps the constant clock
 // at its phase boundaries into g_env_phase[wave][8] (tools/env_phase_probe.py reads them):
@@ -7,6 +8,7 @@
 // 5 rows copied out, 6 stats flushed.
 #pragma once
 
+#ifndef PHC_MEASURE_GEMM_ONLY  // the GEMM translation unit takes only the GEMM section below
 #if defined(PHC_MEASURE_ENV_PHASES) && PHC_MEASURE_ENV_PHASES
 namespace phc {
 constexpr int kPhaseWaves = 1 << 15;
@@ -36,4 +38,34 @@ __device__ unsigned long long g_env_phase[kPhaseWaves * 8];
   do {                   \
   } while (0)
 #define PHC_ENV_PHASE_COPY
+#endif
+#endif  // PHC_MEASURE_GEMM_ONLY
+
+// GEMM kernels.  A product build defines neither PHC_MEASURE_GEMM nor PHC_GEMM_PROBE: the probes compile to
+// nothing and phc_gemm_discard() is the constant 0.  tools/build_variants.sh builds the measurement library
+// with -DPHC_MEASURE_GEMM=1 (and optionally -DPHC_GEMM_PROBE=n):
+//   PHC_GEMM_PROBE 1 = every tile stages the operand panels of tile (0, 0) (L2-hot operands, same
+//     instruction stream); 2 = only the first K-tile is staged (LDS fragment reads + MFMA, no operand
+//     traffic); 3 = B staged once and its fragments kept;
+//   PHC_GEMM_DISCARD=1 in the environment (read at library load) = main loop only, =2 = the whole
+//     epilogue but no global stores.
+#if defined(PHC_MEASURE_GEMM) && PHC_MEASURE_GEMM
+#ifndef PHC_GEMM_PROBE
+#define PHC_GEMM_PROBE 0
+#endif
+#include <cstdlib>
+static inline int phc_gemm_discard() {
+  static const int mode = [] {
+    const char *e = getenv("PHC_GEMM_DISCARD");
+    return e ? (atoi(e) == 2 ? 2 : 1) : 0;
+  }();
+  return mode;
+}
+#else
+#if defined(PHC_GEMM_PROBE) && PHC_GEMM_PROBE
+#error "PHC_GEMM_PROBE is a measurement build: add -DPHC_MEASURE_GEMM=1 (tools/build_variants.sh)"
+#endif
+#undef PHC_GEMM_PROBE
+#define PHC_GEMM_PROBE 0
+static inline int phc_gemm_discard() { return 0; }
 #endif

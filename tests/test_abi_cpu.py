@@ -24,6 +24,14 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == set(_native._EXPORTS), "binding and header disagree"
 
 
+def test_product_library_has_no_measurement_paths():
+    """VERDICT r5 hygiene: the measurement aids (GEMM epilogue discard, env phase stamps) compile only
+    into measurement builds (csrc/phc_measure.h); the product library carries neither."""
+    path = os.path.join(os.path.dirname(os.path.abspath(_native.__file__)), "lib", "libphc_hip.so")
+    blob = open(path, "rb").read()
+    assert b"PHC_GEMM_DISCARD" not in blob and b"phc_env_phase_copy" not in blob and b"g_env_phase" not in blob
+
+
 def test_host_only_queries():
     lib = _native.lib()
     assert lib.phc_version() == 1

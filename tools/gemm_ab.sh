@@ -2,7 +2,8 @@
 # A/B the per-minibatch GEMM probe over library builds and run-time settings, interleaved ROUNDS
 # times in fresh processes; each step under its own timeout.  A variant is a library file name under
 # puffer-phc_amd/lib/, optionally followed by +VAR=value settings for the probe's environment:
-#   VARIANTS="libphc_hip.so libphc_hip.so+PHC_GEMM_DISCARD=1 libphc_hip.so+YONLY=1 libphc_hip.so+MAXWG=256"
+#   VARIANTS="libphc_hip.so libphc_hip_measure.so+PHC_GEMM_DISCARD=1 libphc_hip.so+YONLY=1"
+# (PHC_GEMM_DISCARD is read only by a measurement build: tools/build_variants.sh measure "-DPHC_MEASURE_GEMM=1")
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$ROOT"; OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
 for r in $(seq 1 ${ROUNDS:-1}); do

@@ -1,6 +1,6 @@
 """Same-shape library ceiling: hipBLASLt (torch.bmm / torch.mm, fp16 operands, fp16 out) on every
 trunk GEMM shape of one PPO minibatch (32768 rows), beside phc_twin_gemm with its epilogue discarded
-(PHC_GEMM_DISCARD=1 is read at library load: run this script twice, with and without it).
+(PHC_GEMM_DISCARD=1 is read at load by the measurement library only, PHC_HIP_LIB=.../libphc_hip_measure.so: run this script twice, with and without it).
 
 usage: python tools/lib_ceiling.py [rows]
 """

@@ -30,7 +30,7 @@ def timeit(fn, n=20):
 
 
 def split_costs():
-    """Main loop alone (PHC_GEMM_DISCARD=1 in the environment) vs with each epilogue."""
+    """Main loop alone (PHC_GEMM_DISCARD=1 with the measurement library, PHC_HIP_LIB=.../libphc_hip_measure.so) vs with each epilogue."""
     import os
     g = torch.Generator(device=dev).manual_seed(0)
     for name, batch, k, n in [("L2 fwd 2048->1536", 2, 2048, 1536), ("L4 fwd 1024->1024", 2, 1024, 1024)]:
