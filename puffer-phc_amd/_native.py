@@ -1138,6 +1138,21 @@ class RowCompactor:
         c, _, _, nv, tk = self._buf.tolist()
         return c, nv, tk
 
+    def snapshot(self):
+        """Queue state()'s copy into pinned host memory on the current stream, without waiting: work
+        queued after it may keep running while snapshot_read() waits for this copy only."""
+        if getattr(self, "_pinned", None) is None:
+            self._pinned = torch.empty(5, dtype=torch.int64, pin_memory=True)
+            self._pinned_done = torch.cuda.Event()
+        self._pinned.copy_(self._buf, non_blocking=True)
+        self._pinned_done.record()
+
+    def snapshot_read(self):
+        """The (cursor, sum of n_valid, sum of taken) of the last snapshot()."""
+        self._pinned_done.synchronize()
+        c, _, _, nv, tk = self._pinned.tolist()
+        return c, nv, tk
+
 
 def physics_replay(env_c, mlib, params, pos_sigma, force_scale, seed, counter):
     _check(lib().phc_physics_replay(ctypes.byref(env_c), ctypes.byref(mlib), ctypes.byref(params),

@@ -252,6 +252,24 @@ class RolloutStep:
         g.replay()
         return self.env.finish_block(steps)
 
+    def speculate(self, use_graph=True):
+        """run() whose effects speculate_undo() can take back: the policy graph writes only staging
+        buffers, the experience store (a no-op on a full buffer: the running sums it adds to are
+        reset by the next evaluate) and mu; the generator state, the noise buffer and mu are saved."""
+        if getattr(self, "_spec_mu", None) is None:
+            self._spec_mu, self._spec_noise = torch.empty_like(self.mu), torch.empty_like(self.noise)
+        self._spec_mu.copy_(self.mu)
+        self._spec_noise.copy_(self.noise)
+        saved = (torch.cuda.get_rng_state(self.noise.device), self._noise_ready)
+        self.run(use_graph)
+        return saved
+
+    def speculate_undo(self, saved):
+        self.mu.copy_(self._spec_mu)
+        self.noise.copy_(self._spec_noise)
+        torch.cuda.set_rng_state(saved[0], self.noise.device)
+        self._noise_ready = saved[1]
+
     def run(self, use_graph=True):
         if self.twin is not None:
             refresh_twin(self.twin, _compute_dtype(self.cfg))  # in-place refresh after optimizer steps
@@ -353,8 +371,28 @@ def _evaluate_graph(components, info):
                                vecenv.env_ids, vecenv.masks)
             steps = min_steps
             with profile.eval_misc:
-                cursor, n_valid, taken = rs.store.state()
+                rs.store.snapshot()  # the cursor after the block, read below without waiting for more
+            spec = None
+            if SPECULATE_STEP:
+                with profile.env:
+                    _, _, _, _, env_info, _, _ = vecenv.recv()
+                with profile.eval_forward:
+                    spec = rs.speculate(train_cfg.rollout_graph)
+            with profile.eval_misc:
+                cursor, n_valid, taken = rs.store.snapshot_read()
                 done = cursor >= experience.batch_size
+            if spec is not None:
+                if done:  # the reference stops here: take the queued policy step back
+                    rs.speculate_undo(spec)
+                else:
+                    step_infos.extend(env_info)
+                    with profile.env:
+                        vecenv.send(rs.actions)
+                    steps += 1
+                    if steps >= min_steps:
+                        with profile.eval_misc:
+                            cursor, n_valid, taken = rs.store.state()
+                            done = cursor >= experience.batch_size
         while not done:
             with profile.env:
                 _, _, _, _, env_info, _, _ = vecenv.recv()
@@ -538,6 +576,12 @@ NOISE_AHEAD = os.environ.get("PHC_NOISE_AHEAD", "0") != "0"
 # block of policy + store + env-step launches (RolloutStep.run_block); PHC_BLOCK_GRAPH=0: one graph per
 # step with the env step eager
 BLOCK_GRAPH = os.environ.get("PHC_BLOCK_GRAPH", "1") != "0"
+# rollout: after the block, the next step's policy graph is queued BEFORE the host reads whether the
+# block filled the buffer (the read waits for the block only), so the GPU runs it while the host
+# decides; when the buffer turned out full, the step's visible effects (mu, the action-noise buffer
+# and the generator state) are restored and its env step is not sent — the reference's loop would not
+# have run it (core.py:129-181).  PHC_SPECULATE_STEP=0: read first, then launch.
+SPECULATE_STEP = os.environ.get("PHC_SPECULATE_STEP", "1") != "0"
 
 
 _ADV_ATTRS = ("b_idxs_obs", "b_idxs", "b_idxs_flat", "b_obs_half", "b_obs", "b_actions", "b_logprobs", "b_dones",

@@ -1462,6 +1462,15 @@ __global__ __launch_bounds__(TL::kThreads) void k_wgrad_group(WgradGroupArgs ga)
 // tile configurations
 using Tile128x2 = Tile<128, 128, 2, 2, 2>;
 using Tile256sq = Tile<256, 256, 2, 4, 2>;
+// the twin GEMM's 256 x 256 tile: 8 waves of 128 x 64 (default), or (measurement build PHC_GEMM_TW4=1)
+// 4 waves of 128 x 128, one per SIMD, 512 registers: a third fewer LDS fragment reads per MFMA
+#ifndef PHC_GEMM_TW4
+#define PHC_GEMM_TW4 0
+#endif
+#if PHC_GEMM_TW4 && !(defined(PHC_MEASURE_GEMM) && PHC_MEASURE_GEMM)
+#error "PHC_GEMM_TW4 is a measurement build: add -DPHC_MEASURE_GEMM=1"
+#endif
+using Tile256tw = typename std::conditional<PHC_GEMM_TW4 != 0, Tile<256, 256, 2, 2, 2>, Tile256sq>::type;
 enum { kCfg128 = 0, kCfg256sq = 2 };
 
 // 256 x 256 tiles when they still give every CU a tile (the rollout's 4096-row first layer), else
@@ -1507,7 +1516,7 @@ static void launch_one(const GemmArgs &g, int64_t blocks, hipStream_t st) {
 
 template <typename T, typename OutT, int EPI>
 static void launch_cfg(int cfg, const GemmArgs &g, int64_t blocks, hipStream_t st) {
-  if (cfg == kCfg256sq) launch_one<T, OutT, EPI, Tile256sq>(g, blocks, st);
+  if (cfg == kCfg256sq) launch_one<T, OutT, EPI, Tile256tw>(g, blocks, st);
   else launch_one<T, OutT, EPI, Tile128x2>(g, blocks, st);
 }
 

@@ -327,6 +327,59 @@ def test_block_rollout_matches_single_step_graphs(monkeypatch):
             np.testing.assert_allclose(ia[k], ib[k], rtol=1e-9, atol=1e-12, err_msg=k)
 
 
+@pytest.mark.parametrize("clip_len", [(12, 40), (400, 500)])
+def test_speculative_step_after_block_matches_read_first(monkeypatch, clip_len):
+    """core.SPECULATE_STEP: the step after the block is queued before the host reads whether the block
+    filled the buffer.  Short clips: rows are masked, the step is needed and kept; long clips: no row
+    is masked, the block fills the buffer and the queued step is taken back (mu, the noise buffer and
+    the generator state restored, no env step sent).  Either way every experience row, the step and
+    tick counts, mu and the generator's next draw equal the read-first loop's, over three evaluates."""
+    from puffer_phc_amd import clean_pufferl
+    from puffer_phc_amd.clean_pufferl import core
+    from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
+    from puffer_phc_amd.config import EnvConfig, TrainConfig
+    from puffer_phc_amd.envs.state_init import StateInit
+    from puffer_phc_amd.motion_lib import PackedMotions
+    from puffer_phc_amd.policies import PHCPolicy, Policy
+    from puffer_phc_amd.synthetic import synthetic_clips
+
+    undo = {"n": 0}
+    orig_undo = core.RolloutStep.speculate_undo
+
+    def counting_undo(self, saved):
+        undo["n"] += 1
+        return orig_undo(self, saved)
+
+    monkeypatch.setattr(core.RolloutStep, "speculate_undo", counting_undo)
+    runs = []
+    for spec in (False, True):
+        monkeypatch.setattr(core, "SPECULATE_STEP", spec)
+        q, t, c, fps = synthetic_clips(64, clip_len[0], clip_len[1], seed=21, device=DEV)
+        init = StateInit.Start if clip_len[0] >= 400 else StateInit.Random  # Start: no clip ends in 72 steps
+        env = PHCPufferEnv(EnvConfig(num_envs=64, seed=8, log_interval=5, max_episode_length=10 ** 6, state_init=init),
+                           motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
+        torch.manual_seed(0)
+        policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
+        cfg = TrainConfig(batch_size=64 * 24, minibatch_size=64 * 8, bptt_horizon=8, checkpoint_interval=10 ** 9)
+        comps, info, _ = clean_pufferl.create("t", cfg, env.cfg, env, policy)
+        out = []
+        for it in range(3):
+            torch.manual_seed(10 + it)
+            clean_pufferl.evaluate(comps, info)
+            e = comps.experience
+            out.append(dict(step=info.global_step, tick=env.tick, obs=e.obs.clone(), act=e.actions.clone(),
+                            logp=e.logprobs.clone(), val=e.values.clone(), mu=comps.rollout.mu.clone(),
+                            draw=torch.randn(8, device=DEV)))
+        runs.append(out)
+    for ra, rb in zip(*runs):
+        for k in ra:
+            if isinstance(ra[k], torch.Tensor):
+                assert torch.equal(ra[k], rb[k]), k
+            else:
+                assert ra[k] == rb[k], k
+    assert (undo["n"] > 0) == (clip_len[0] >= 400)
+
+
 def _dict_clips(n, lo, hi, seed):
     from puffer_phc_amd.synthetic import synthetic_clips
 

@@ -80,7 +80,7 @@ def compare(trace, clock):
     rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
     res = json.load(open(clock))
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
-    env = [dur(r) for r in rows if "k_env_step" in r["Kernel_Name"]][-40:]
+    env = [dur(r) for r in rows if ("k_env_step" in r["Kernel_Name"] or "k_env_replay" in r["Kernel_Name"])][-40:]
     gem = [dur(r) for r in rows if "k_twin_gemm" in r["Kernel_Name"]]
     gemm_eager, gemm_graph = gem[3:23], gem[-6:]
     out = {}

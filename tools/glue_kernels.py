@@ -16,7 +16,7 @@ def short(n):
 def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     it = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_env_step") or "k_env_step" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "k_env_step" in r["Kernel_Name"] or "k_env_replay" in r["Kernel_Name"]]
     its, cur = [], [idx[0]]
     for a, b in zip(idx, idx[1:]):
         if b - a > 400:

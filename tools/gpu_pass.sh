@@ -54,12 +54,12 @@ if has trace; then
 fi
 if has pmc; then
   for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "k_twin_gemm|k_wgrad|k_env_step" -d "$O/pmc_ppo_$C" -o run \
+    timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "k_twin_gemm|k_wgrad|k_env_step|k_env_replay" -d "$O/pmc_ppo_$C" -o run \
       --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > "$O/pmc_ppo_$C.log" 2>&1 \
       || fail pmc "$O/pmc_ppo_$C.log"
   done
   python tools/pmc_summary.py "$O/pmc_ppo_FETCH_SIZE" "$O/pmc_ppo_WRITE_SIZE" train_gemm "$O/traffic_gemm_4096.json" "$O/trace_ppo" || true
-  python tools/pmc_summary.py "$O/pmc_ppo_FETCH_SIZE" "$O/pmc_ppo_WRITE_SIZE" k_env_step "$O/traffic_fused_ppo_4096.json" \
+  python tools/pmc_summary.py "$O/pmc_ppo_FETCH_SIZE" "$O/pmc_ppo_WRITE_SIZE" k_env_ "$O/traffic_fused_ppo_4096.json" \
     "$O/trace_ppo" $((13634 * 4096)) || true
 fi
 if has env; then
@@ -70,11 +70,11 @@ if has env; then
       python3 "$ROOT/bench.py" --mode env --envs $E --no-cpu-baseline > "$O/trace_env_$E.log" 2>&1 || fail envtrace "$O/trace_env_$E.log"
     stats "$O/trace_env_$E" "$O/env_${E}_kernel_stats.csv"
     for C in FETCH_SIZE WRITE_SIZE; do
-      timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "k_env_step" -d "$O/pmc_env_${E}_$C" -o run \
+      timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "k_env_step|k_env_replay" -d "$O/pmc_env_${E}_$C" -o run \
         --output-format csv -- python3 "$ROOT/bench.py" --mode env --steps 20 --warmup 5 --envs $E --no-cpu-baseline \
         > "$O/pmc_env_${E}_$C.log" 2>&1 || fail envpmc "$O/pmc_env_${E}_$C.log"
     done
-    python tools/pmc_summary.py "$O/pmc_env_${E}_FETCH_SIZE" "$O/pmc_env_${E}_WRITE_SIZE" k_env_step "$O/traffic_fused_$E.json" \
+    python tools/pmc_summary.py "$O/pmc_env_${E}_FETCH_SIZE" "$O/pmc_env_${E}_WRITE_SIZE" k_env_ "$O/traffic_fused_$E.json" \
       "$O/trace_env_$E" $((11714 * E)) || true
   done
 fi

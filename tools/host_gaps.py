@@ -14,7 +14,7 @@ def main():
     ker = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     api = sorted(csv.DictReader(open(sys.argv[2])), key=lambda r: int(r["Start_Timestamp"]))
     min_us = float(sys.argv[3]) if len(sys.argv) > 3 else 20.0
-    idx = [i for i, r in enumerate(ker) if "k_env_step" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(ker) if ("k_env_step" in r["Kernel_Name"] or "k_env_replay" in r["Kernel_Name"])]
     its, cur = [], [idx[0]]
     for a, b in zip(idx, idx[1:]):
         if b - a > 300:

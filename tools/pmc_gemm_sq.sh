@@ -10,7 +10,7 @@ P1="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_B
 P2="GRBM_GUI_ACTIVE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
 for mode in main full; do
   D="PHC_HIP_LIB=$ROOT/puffer-phc_amd/lib/${LIB:-libphc_hip.so}"
-  [ $mode = main ] && D="PHC_HIP_LIB=$ROOT/puffer-phc_amd/lib/libphc_hip_measure.so PHC_GEMM_DISCARD=1"
+  [ $mode = main ] && D="PHC_HIP_LIB=$ROOT/puffer-phc_amd/lib/${MAINLIB:-libphc_hip_measure.so} PHC_GEMM_DISCARD=1"
   i=0
   for P in "$P1" "$P2"; do
     i=$((i+1))

@@ -12,7 +12,7 @@ def main():
     path = sys.argv[1]
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 12
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "k_env_step" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if ("k_env_step" in r["Kernel_Name"] or "k_env_replay" in r["Kernel_Name"])]
     its, cur = [], [idx[0]]
     for a, b in zip(idx, idx[1:]):
         if b - a > 400:
