@@ -248,12 +248,38 @@ __device__ __forceinline__ v3 ref_dof_vel(const float *__restrict__ dvs, const B
 }
 
 // -------------------------------------------------------------- group ops --
+// On the 32-lane half-waves with one LDS-crossbar operation instead of five ds_bpermute round trips
+// (each waited on before the next): the sum is the xor butterfly 16, 8, 4, 2, 1, its xor-16 step one
+// ds_swizzle (bitmask mode: lane ^ 16 within each 32-lane group, no LDS memory access), its xor-8 / 4 /
+// 2 / 1 steps DPP row rotations (once lanes i and i ^ 16 (then ^ 8, ...) hold equal values, a rotation
+// by 8, 4, 2, 1 within the 16-lane row reads a lane holding the xor partner's value).  Every lane adds
+// the same two values at every level (own + partner; IEEE addition commutes), so the result is the
+// __shfl_xor butterfly's bit for bit and the same in all 32 lanes.  Requires every lane of the wave
+// active (uniform control flow).  (v_permlane16_swap would do the xor-16 step in the VALU, but this
+// compiler folds its two results into one register.)
+template <int N> __device__ __forceinline__ float row_ror(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + N, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int m = kGroup / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, kGroup);
+  static_assert(kGroup == 32, "half-wave groups");
+  constexpr int kXor16 = (0x10 << 10) | 0x1F;  // ds_swizzle bitmask mode: and 0x1F, or 0, xor 0x10
+  v = v + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), kXor16));
+  v = v + row_ror<8>(v);
+  v = v + row_ror<4>(v);
+  v = v + row_ror<2>(v);
+  v = v + row_ror<1>(v);
   return v;
 }
-__device__ __forceinline__ float group_bcast(float v) { return __shfl(v, 0, kGroup); }
+// lane 0's value in lanes 0-31, lane 32's in lanes 32-63 (scalar reads: no LDS round trip)
+__device__ __forceinline__ float group_bcast(float v) {
+  const int a = __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0);
+  const int b = __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32);
+  return __builtin_bit_cast(float, (__lane_id() & 32) ? b : a);
+}
+// the next lane's value (lane i gets lane i + 1 across the whole wave: DPP wave_shl:1; lane 63 gets 0)
+__device__ __forceinline__ float next_lane(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, true));
+}
 
 // ------------------------------------------------------------ observation --
 // One body's slices of the 934-float observation (common.py:23-103 self obs with

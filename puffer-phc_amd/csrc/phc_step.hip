@@ -445,21 +445,19 @@ __device__ __forceinline__ void env_bookkeeping(const EnvView &e, int64_t ei, co
   st_row[0] = o.r_pos; st_row[1] = o.r_rot; st_row[2] = o.r_vel; st_row[3] = o.r_ang; st_row[4] = o.pr;
 }
 
-// one stats row per workgroup, summed over its envs in LDS (no atomics); `prev` = the row's old
-// value, loaded at kernel start (stats_prefetch) so the read-modify-write adds no memory round trip
-// to the kernel's tail
-__device__ __forceinline__ double stats_prefetch(const EnvView &e) {
-  return (e.stats && threadIdx.x < 10) ? e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] : 0.0;
-}
-
+// one stats row per workgroup, summed over its envs in LDS, added to the row's old value by ONE vector
+// atomic add per slot: this workgroup is the row's only writer in the launch, so the result is the
+// load-add-store's bit for bit (an IEEE double add either way) — without a load of the old row at the
+// kernel's start whose value (held to the end) cost a spill and a full memory round before any other load
 template <int kEnvs, bool kSync = true>
-__device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10], double prev) {
+__device__ __forceinline__ void flush_stats(const EnvView &e, double (*sh)[10]) {
   if (kSync) __syncthreads();
   if (threadIdx.x < 10) {
     double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < kEnvs; ++j) acc += sh[j][threadIdx.x];
-    e.stats[(int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x] = prev + acc;
+    (void)__builtin_amdgcn_global_atomic_fadd_f64(
+        (__attribute__((address_space(1))) double *)(e.stats + (int64_t)blockIdx.x * PHC_STATS_SLOTS + threadIdx.x), acc);
   }
 }
 
@@ -685,7 +683,6 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
   const int64_t ei = valid ? env : 0;
 
   launch_clock_begin(c.clk);
-  const double st_prev = stats_prefetch(e);
   // per-env scalars (broadcast loads: every lane of the half-wave reads the same word); the rng
   // counter through a pointer select, so its load joins this round instead of waiting behind a
   // null check where it is used
@@ -743,7 +740,7 @@ __global__ __launch_bounds__(kBlock, PHC_ENV_WAVES) void k_env_step(EnvView e, L
       else operand_rows_out<_Float16>(e, sh_obs, env0, nv, threadIdx.x, kBlock);
     }
   }
-  if (e.stats) flush_stats<kEnvsPerBlock, false>(e, sh_stats, st_prev);
+  if (e.stats) flush_stats<kEnvsPerBlock, false>(e, sh_stats);
   launch_clock_end(c.clk);
 }
 
@@ -778,19 +775,26 @@ __global__ __launch_bounds__(64 * kWaves, PHC_ENV_WAVES) void k_env_replay(EnvVi
 
   launch_clock_begin(c.clk);
   ENV_PHASE(0);
-  const double st_prev = stats_prefetch(e);
-  // R13 for the wave's envs first (elementwise over their contiguous [nv, 69] action span, independent
-  // of everything else: its loads join the first memory round)
+  // per-env scalars (broadcast loads); the rng counter through a pointer select, so its load joins this
+  // round instead of waiting behind a null check where it is used
+  const uint32_t rng_val = *(e.rng ? (gu32 *)(e.rng + ei) : (gu32 *)&kZeroU32);
+  const int prog = (int)e.progress[ei] + 1;
+  const float st = e.start[ei];
+  const float so = e.start_off[ei];
+  const v3 go = {e.goff[3 * ei], e.goff[3 * ei + 1], e.goff[3 * ei + 2]};
+  const int64_t mid = e.motion_ids[ei];
+  // R13 for the wave's envs (elementwise over their contiguous [nv, 69] action span, independent of
+  // everything else): its loads issued with the scalars', its arithmetic and stores after the motion
+  // scalars' loads are issued (stores ahead of them would keep them behind: a memory round more)
+  constexpr int kPdIt = (kWaveEnvs * PHC_NUM_DOF + 63) / 64;
+  const int cnt = nv * PHC_NUM_DOF;
+  float av[kPdIt], ov[kPdIt], sv[kPdIt];
+  uint8_t fv[kPdIt];
   if (r.actions) {
     const float *a = r.actions + env0 * PHC_NUM_DOF;
-    float *pd = r.pd + env0 * PHC_NUM_DOF;
     // every load of the span first (clamped indices, a zero row standing in for a null frozen mask):
     // loads behind a select or a null check made hipcc wait vmcnt(0) per element
-    constexpr int kPdIt = (kWaveEnvs * PHC_NUM_DOF + 63) / 64;
-    const int cnt = nv * PHC_NUM_DOF;
     gu8 *fz = r.frozen ? (gu8 *)r.frozen : (gu8 *)kNoFrozen;
-    float av[kPdIt], ov[kPdIt], sv[kPdIt];
-    uint8_t fv[kPdIt];
 #pragma unroll
     for (int u = 0; u < kPdIt; ++u) {
       const int i = wl + 64 * u < cnt ? wl + 64 * u : (cnt > 0 ? cnt - 1 : 0);
@@ -800,6 +804,10 @@ __global__ __launch_bounds__(64 * kWaves, PHC_ENV_WAVES) void k_env_replay(EnvVi
       sv[u] = r.scale[d];
       fv[u] = fz[d];
     }
+  }
+  const MotionScalars m = load_motion(l, mid);
+  if (r.actions) {
+    float *pd = r.pd + env0 * PHC_NUM_DOF;
 #pragma unroll
     for (int u = 0; u < kPdIt; ++u) {
       const int i = wl + 64 * u;
@@ -809,14 +817,6 @@ __global__ __launch_bounds__(64 * kWaves, PHC_ENV_WAVES) void k_env_replay(EnvVi
       pd[i] = fv[u] ? 0.0f : ov[u] + sv[u] * x;  // action_to_pd's expression
     }
   }
-  // per-env scalars (broadcast loads); the rng counter through a pointer select, so its load joins this
-  // round instead of waiting behind a null check where it is used
-  const uint32_t rng_val = *(e.rng ? (gu32 *)(e.rng + ei) : (gu32 *)&kZeroU32);
-  const int prog = (int)e.progress[ei] + 1;
-  const float st = e.start[ei];
-  const float so = e.start_off[ei];
-  const v3 go = {e.goff[3 * ei], e.goff[3 * ei + 1], e.goff[3 * ei + 2]};
-  const MotionScalars m = load_motion(l, e.motion_ids[ei]);
   const float t = (float)prog * c.dt + st + so;
   const Blend bl0 = frame_blend(t, m);
   // a passing env: reset_env_state's time draw now, its observation at dt + mt (humanoid_phc.py:1061-1065)
@@ -886,7 +886,7 @@ __global__ __launch_bounds__(64 * kWaves, PHC_ENV_WAVES) void k_env_replay(EnvVi
     mine = mine + fabsf(f.y * dv.y);
     mine = mine + fabsf(f.z * dv.z);
     if (lane >= kBodies) mine = 0.0f;
-    pw_reg = __shfl_down(mine, 1, kGroup);
+    pw_reg = next_lane(mine);  // lanes >= 23 (incl. 31, which reads the other env's lane 32) zeroed below
     if (lane >= kBodies - 1) pw_reg = 0.0f;
   }
 
@@ -948,7 +948,7 @@ __global__ __launch_bounds__(64 * kWaves, PHC_ENV_WAVES) void k_env_replay(EnvVi
     }
   }
   ENV_PHASE(5);
-  if (e.stats) flush_stats<kEnvs, (kWaves > 1)>(e, sh_stats, st_prev);
+  if (e.stats) flush_stats<kEnvs, (kWaves > 1)>(e, sh_stats);
   ENV_PHASE(6);
   launch_clock_end(c.clk);
 }
