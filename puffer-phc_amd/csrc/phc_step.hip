@@ -948,7 +948,18 @@ __global__ __launch_bounds__(64 * kWaves, PHC_ENV_WAVES) void k_env_replay(EnvVi
     }
   }
   ENV_PHASE(5);
-  if (e.stats) flush_stats<kEnvs, (kWaves > 1)>(e, sh_stats);
+  if (e.stats) {  // this wave's stats row (one per wave: no workgroup barrier), its 2 envs summed in LDS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wave_lds_handoff();
+    if (wl < 10) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < kWaveEnvs; ++j) acc += sh_stats[w * kWaveEnvs + j][wl];
+      (void)__builtin_amdgcn_global_atomic_fadd_f64(
+          (__attribute__((address_space(1))) double *)(e.stats + ((int64_t)blockIdx.x * kWaves + w) * PHC_STATS_SLOTS + wl),
+          acc);
+    }
+  }
   ENV_PHASE(6);
   launch_clock_end(c.clk);
 }
@@ -1016,18 +1027,18 @@ using namespace phc;
 PHC_ENV_PHASE_COPY
 
 // the fused replay step's workgroup shape: kReplayWaves waves (2 envs each) per workgroup, one stats row
-// per workgroup
+// per wave
 #ifndef PHC_REPLAY_WAVES
 #define PHC_REPLAY_WAVES 1
 #endif
 constexpr int kReplayWaves = PHC_REPLAY_WAVES;
 constexpr int kReplayEnvs = kReplayWaves * kWaveEnvs;
 
-// stats rows: one per workgroup of whichever env kernel writes the most (k_env_replay's workgroups hold
-// kReplayEnvs envs, k_env_step's 8)
+// stats rows: as many as whichever env kernel writes the most (k_env_replay: one per wave of 2 envs,
+// k_env_step: one per 8-env workgroup)
 extern "C" int64_t phc_stats_blocks(int64_t num_envs) {
   if (num_envs <= 0) return 0;
-  const int64_t a = grid_envs(num_envs), b = (num_envs + kReplayEnvs - 1) / kReplayEnvs;
+  const int64_t a = grid_envs(num_envs), b = (num_envs + kReplayEnvs - 1) / kReplayEnvs * kReplayWaves;
   return a > b ? a : b;
 }
 
