@@ -586,7 +586,7 @@ SPECULATE_STEP = os.environ.get("PHC_SPECULATE_STEP", "1") != "0"
 
 _ADV_ATTRS = ("b_idxs_obs", "b_idxs", "b_idxs_flat", "b_obs_half", "b_obs", "b_actions", "b_logprobs", "b_dones",
               "b_truncated", "b_values", "b_advantages", "returns", "sorted_values", "b_returns", "b_adv_ms",
-              "ev_pair")
+              "ev_pair", "b_amp_idx", "b_amp_rep_idx")
 
 
 def _adv_graph_key(components, info):
@@ -600,17 +600,27 @@ def _adv_graph_key(components, info):
     # (fused policy, its twin layout) and the single-process advantage statistics
     twin = getattr(pol, "_twin", None)
     width = half_input_width(twin, _compute_dtype(cfg)) if twin is not None else None
+    amp = None
+    if info.use_amp_obs:  # the AMP buffers, the replay's fill state and draw counter, the discriminator
+        anm = getattr(pol, "amp_obs_norm", None)
+        amp = (exp.amp_obs.data_ptr(), exp.amp_obs_replay.data_ptr(), exp.amp_obs_replay_filled,
+               exp._amp_iter.data_ptr() if getattr(exp, "_amp_iter", None) is not None else None,
+               float(exp.amp_obs_update_prob), id(getattr(pol, "_disc_ops", None)),
+               (anm.running_mean.data_ptr(), anm.running_var.data_ptr()) if anm is not None else None,
+               weight_cache.layout_key(None, list(pol.parameters())))
     return (ptrs, norm, exp.batch_size, exp.minibatch_size, exp.num_minibatches, exp.bptt_horizon,
             float(cfg.gamma), float(cfg.gae_lambda), cfg.fused_obs, cfg.fused_loss, cfg.precision,
             id(components.gae), bool(getattr(pol, "fused", False)), hasattr(pol, "obs_half_input"), width,
-            D.is_dist())
+            D.is_dist(), amp)
 
 
 def _compute_advantages_train(components, info):
     """compute_advantages for train(): eager on the first call, captured on the second, replayed
-    after (re-captured when a key input changes; eager for AMP, recurrent or host tensors)."""
+    after (re-captured when a key input changes; eager for recurrent policies or host tensors).  With
+    AMP the pass holds the adversarial reward and the replay buffer's refresh (counter-based draws, a
+    select: structs.Experience.flatten_batch)."""
     exp = components.experience
-    if not (ADV_GRAPH and exp.obs.is_cuda and not info.use_amp_obs and exp.lstm_h is None):
+    if not (ADV_GRAPH and exp.obs.is_cuda and exp.lstm_h is None):
         return compute_advantages(components, info)
     st = getattr(components, "_adv_graph", None)
     if st is None:
@@ -637,7 +647,7 @@ def _compute_advantages_train(components, info):
         torch.cuda.synchronize()
         return compute_advantages(components, info)
     st["graph"], st["out"] = g, out
-    st["attrs"] = {k: getattr(exp, k) for k in _ADV_ATTRS}
+    st["attrs"] = {k: getattr(exp, k) for k in _ADV_ATTRS if hasattr(exp, k)}
     g.replay()
     return out
 
@@ -676,7 +686,8 @@ DP_TRAIN_GRAPH = os.environ.get("PHC_DP_TRAIN_GRAPH", "1") != "0"
 def _train_graph_eligible(components, info, pol):
     cfg, exp, opt = info.config, components.experience, components.optimizer
     adv = getattr(components, "_adv_graph", None)
-    if not (TRAIN_GRAPH and exp.obs.is_cuda and not info.use_amp_obs and exp.lstm_h is None
+    if not (TRAIN_GRAPH and exp.obs.is_cuda and exp.lstm_h is None
+            and (not info.use_amp_obs or (hasattr(pol, "discriminate_rows") and hasattr(exp, "b_amp_rep_idx")))
             and (not D.is_dist() or (DP_TRAIN_GRAPH and D.backend() == "nccl"))
             and isinstance(opt, FlatAdam) and opt.param_init is not None and cfg.l2_reg_coef == 0
             and cfg.target_kl is None and not cfg.bound_loss_grad and STORE_GRADS and cfg.fused_loss
@@ -688,6 +699,26 @@ def _train_graph_eligible(components, info, pol):
 
 
 _UNIT_MS = {}
+
+
+def _amp_disc_terms(cfg, pol, exp, mb, amp_obs_demo, amp_mb, loss):
+    """Minibatch mb's discriminator terms (core.py:336-347, 394-395): agent, replay and demo rows in one
+    pass; returns (disc_loss, (agent acc, demo acc), loss + disc_coef * disc_loss)."""
+    idx_agent = exp.b_amp_idx[mb][:amp_mb]
+    idx_replay = exp.b_amp_rep_idx[mb][:amp_mb]
+    with autocast(cfg):
+        d_all = pol.discriminate_rows([(exp.amp_obs, idx_agent), (exp.amp_obs_replay, idx_replay),
+                                       (amp_obs_demo, None)]).float()
+    # a minibatch may hold fewer than amp_mb rows (minibatch_size < num_envs): split at the agent +
+    # replay rows actually gathered, not at 2 * amp_mb
+    n_agent = idx_agent.numel() + idx_replay.numel()
+    d_agent, d_demo = d_all[:n_agent], d_all[n_agent:]
+    bce = torch.nn.BCEWithLogitsLoss()
+    disc_loss = 0.5 * (bce(d_agent, torch.zeros_like(d_agent)) + bce(d_demo, torch.ones_like(d_demo)))
+    disc_acc = ((d_agent.detach() < 0).float().mean(), (d_demo.detach() > 0).float().mean())
+    if cfg.disc_coef > 0:
+        loss = loss + disc_loss * cfg.disc_coef
+    return disc_loss, disc_acc, loss
 
 
 def _fused_update(components, info, pol):
@@ -710,20 +741,38 @@ def _fused_update(components, info, pol):
         if key not in _UNIT_MS:
             _UNIT_MS[key] = torch.tensor([0.0, 1.0], dtype=torch.float32, device=dev)
         unit = _UNIT_MS[key]
+    amp = info.use_amp_obs
+    acc = torch.zeros(12, dtype=torch.float64, device=dev)
+    if amp:  # the demo rows: the env's AMP demo buffer (a fixed address, refreshed by the rollout's steps)
+        amp_obs_demo = components.vecenv.fetch_amp_obs_demo()
+        amp_mb = amp_obs_demo.shape[0]
     for _epoch in range(cfg.update_epochs):
         for mb in range(exp.num_minibatches):
             obs = exp.b_obs_half[mb * mbs:(mb + 1) * mbs]
             atn = exp.b_actions[mb].reshape(-1, exp.b_actions.shape[-1])
             with autocast(cfg):  # the logged sums accumulate inside the objective / optimizer launches
+                # AMP: the general loop's launches exactly (a second gradient source: no stored
+                # gradients, the buffer zeroed; the loss row summed per minibatch as there)
                 loss, st = fused_ppo_loss(pol, obs, atn, exp.b_logprobs[mb].reshape(-1), exp.b_advantages[mb],
                                           adv_ms[mb] if cfg.norm_adv else unit, exp.b_values[mb], exp.b_returns[mb],
-                                          coefs, store_grads=True, stats_acc=acc_ppo)
+                                          coefs, store_grads=not amp, stats_acc=None if amp else acc_ppo)
+            if amp:
+                disc_loss, disc_acc, loss = _amp_disc_terms(cfg, pol, exp, mb, amp_obs_demo, amp_mb, loss)
+                flat.zero()
             flat.overlap_begin()  # data parallel: the gradient spans' all-reduces as the backward finishes them
             opt.backward(loss)
             flat.overlap_finish()
-            opt.fused_step(cfg.max_grad_norm, norm_acc=acc_opt)
+            if not amp:
+                opt.fused_step(cfg.max_grad_norm, norm_acc=acc_opt)
+                continue
+            gnorm = opt.fused_step(cfg.max_grad_norm, norm_acc=None)[0]
+            with torch.no_grad():
+                pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac, _ = st.unbind(0)
+                mbl = mbl_ref if mbl_ref is not None else torch.zeros((), device=dev)
+                acc += torch.stack([pg_loss.detach(), v_loss.detach(), entropy_loss.detach(), old_approx_kl, approx_kl,
+                                    clipfrac, gnorm, opt.norms[2].detach(), disc_loss.detach(), mbl.detach(),
+                                    disc_acc[0], disc_acc[1]]).double() / total
     with torch.no_grad():
-        acc = torch.zeros(12, dtype=torch.float64, device=dev)
         i7, i67, i02 = _row_index(dev)
         acc.index_add_(0, i7, acc_ppo / total)
         acc.index_add_(0, i67, acc_opt.index_select(0, i02) / total)
@@ -750,7 +799,16 @@ def _train_graph_key(components, info, pol):
             tuple(components.optimizer.param_groups[0]["betas"]), float(components.optimizer.param_groups[0]["eps"]),
             tuple(components.optimizer._hp_scale),
             # data parallel: the collectives are captured too (the readiness schedule of the DP mode)
-            D.is_dist(), D.world_size(), _dp_mode_key())
+            D.is_dist(), D.world_size(), _dp_mode_key(),
+            # AMP: the discriminator terms read the demo buffer and the buffers the advantage pass holds
+            info.use_amp_obs, float(getattr(cfg, "disc_coef", 0.0)), _amp_demo_ptr(components, info))
+
+
+def _amp_demo_ptr(components, info):
+    if not info.use_amp_obs:
+        return None
+    demo = components.vecenv.fetch_amp_obs_demo()
+    return None if demo is None else (demo.data_ptr(), tuple(demo.shape))
 
 
 def _train_minibatches_graphed(components, info, pol):
@@ -925,22 +983,8 @@ def train(components, info, utilization=None):
                     if info.use_amp_obs:
                         # agent rows, replay rows and demo rows through the discriminator in one
                         # pass (core.py:336-344 calls it twice; rows are independent)
-                        idx_agent = experience.b_amp_idx[mb][:amp_mb]
-                        idx_replay = experience.b_amp_rep_idx[mb][:amp_mb]
-                        with autocast(cfg):
-                            d_all = pol.discriminate_rows(
-                                [(experience.amp_obs, idx_agent), (experience.amp_obs_replay, idx_replay),
-                                 (amp_obs_demo, None)]).float()
-                        # a minibatch may hold fewer than amp_mb rows (minibatch_size < num_envs):
-                        # split at the agent + replay rows actually gathered, not at 2 * amp_mb
-                        n_agent = idx_agent.numel() + idx_replay.numel()
-                        d_agent, d_demo = d_all[:n_agent], d_all[n_agent:]
-                        bce = torch.nn.BCEWithLogitsLoss()
-                        disc_loss = 0.5 * (bce(d_agent, torch.zeros_like(d_agent)) + bce(d_demo, torch.ones_like(d_demo)))
-                        # core.py:394-395
-                        disc_acc = ((d_agent.detach() < 0).float().mean(), (d_demo.detach() > 0).float().mean())
-                        if cfg.disc_coef > 0:
-                            loss = loss + disc_loss * cfg.disc_coef
+                        disc_loss, disc_acc, loss = _amp_disc_terms(cfg, pol, experience, mb, amp_obs_demo, amp_mb,
+                                                                    loss)
                     if not cfg.bound_loss_grad:
                         mbl = mbl_ref  # constant: changes the loss value only, never a gradient
                         # (the loss value itself is not read: the logged bound term is mbl_ref, so

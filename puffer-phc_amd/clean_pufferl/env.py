@@ -132,10 +132,10 @@ class PHCPufferEnv:
     @property
     def block_steppable(self):
         """Whether steps can be captured into a rollout block graph: the fused replay launch (no
-        per-step host value) with the env's in-launch auto-reset, no AMP history."""
+        per-step host value) with the env's in-launch auto-reset; with AMP its history launch too (it
+        reads only device state)."""
         e = self.env
-        return (e.fused_env_step and hasattr(e.physics, "step_fused") and not e.flag_im_eval
-                and not self.cfg.use_amp_obs)
+        return e.fused_env_step and hasattr(e.physics, "step_fused") and not e.flag_im_eval
 
     def block_stats(self, steps):
         """[steps, blocks, slots] float64 logging rows: step k of a block writes rows k."""

@@ -15,6 +15,23 @@ import numpy as np
 import torch
 
 
+# splitmix64 on int64 tensors (wrapping products, logical right shifts): the AMP replay buffer's
+# counter-based draws
+_GOLD = -7046029254386353131  # 0x9E3779B97F4A7C15
+_M1 = -4658895280553007687    # 0xBF58476D1CE4E5B9
+_M2 = -7723592293110705685    # 0x94D049BB133111EB
+_PERM_SALT = 0x5DEECE66D
+
+
+def _lsr(z, s):
+    return (z >> s) & ((1 << (64 - s)) - 1)
+
+
+def _mix64(z):
+    z = (z ^ _lsr(z, 30)) * _M1
+    z = (z ^ _lsr(z, 27)) * _M2
+    return z ^ _lsr(z, 31)
+
 class Experience:
     """Flat on-device storage, puffer_phc/clean_pufferl/structs.py:23-176."""
 
@@ -120,15 +137,31 @@ class Experience:
             # AMP rows stay where they are: the discriminator gathers them through these indices
             # (b_amp_obs / b_amp_obs_replay below materialise the reference's tensors on demand)
             self.b_amp_idx = b_flat
+            # the replay refresh (structs.py:165-176: rand < p rows replaced, then a randperm of the
+            # replay rows) from a counter-based draw keyed by a device iteration counter, and a
+            # select instead of a boolean-mask write: no host value, no host sync, so the pass can
+            # replay from a graph and draws the same numbers graphed or eager
+            it = self._amp_draw_counter()
+            idx = torch.arange(self.batch_size, device=self.device, dtype=torch.int64)
             if not self.amp_obs_replay_filled:
                 self.amp_obs_replay[:] = self.amp_obs[:]
                 self.amp_obs_replay_filled = True
             else:
-                upd = torch.rand(self.batch_size, device=self.device) < self.amp_obs_update_prob
-                self.amp_obs_replay[upd] = self.amp_obs[upd]
-            rep = torch.randperm(self.batch_size, device=self.device).reshape(self.num_minibatches,
-                                                                               self.minibatch_size)
+                u = (_lsr(_mix64(idx + it * _GOLD), 40).float() * (1.0 / 16777216.0))
+                upd = u < self.amp_obs_update_prob
+                torch.where(upd.unsqueeze(1), self.amp_obs, self.amp_obs_replay, out=self.amp_obs_replay)
+            keys = _mix64((idx + it * _GOLD) ^ _PERM_SALT)
+            rep = torch.argsort(keys).reshape(self.num_minibatches, self.minibatch_size)
             self.b_amp_rep_idx = rep
+
+    def _amp_draw_counter(self):
+        """The AMP replay draws' device iteration counter, advanced once per flatten_batch (inside a
+        captured pass too)."""
+        c = getattr(self, "_amp_iter", None)
+        if c is None:
+            c = self._amp_iter = torch.zeros((), dtype=torch.int64, device=self.device)
+        c += 1
+        return c
 
     @property
     def b_amp_obs(self):

@@ -284,11 +284,13 @@ def test_rollout_env_written_operand_matches_obs_half():
             assert torch.equal(x, y)
 
 
-def test_block_rollout_matches_single_step_graphs(monkeypatch):
+@pytest.mark.parametrize("amp", [False, True])
+def test_block_rollout_matches_single_step_graphs(monkeypatch, amp):
     """evaluate() with its first min_steps steps replayed as ONE captured block (policy + store + fused
     env step per step, core.RolloutStep.run_block) against one graph per step with the env step eager:
     the same experience rows, the same tick, and the same mean_and_log infos — log points that fall
-    inside a block included (log_interval 5 does not divide the 24-step rollouts)."""
+    inside a block included (log_interval 5 does not divide the 24-step rollouts).  amp: the AMP
+    history launch of every step inside the block too, and the AMP rows stored."""
     from puffer_phc_amd import clean_pufferl
     from puffer_phc_amd.clean_pufferl import core
     from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
@@ -301,7 +303,7 @@ def test_block_rollout_matches_single_step_graphs(monkeypatch):
     for block in (False, True):
         monkeypatch.setattr(core, "BLOCK_GRAPH", block)
         q, t, c, fps = synthetic_clips(64, 12, 40, seed=21, device=DEV)  # short clips: many resets
-        env = PHCPufferEnv(EnvConfig(num_envs=64, seed=8, log_interval=5),
+        env = PHCPufferEnv(EnvConfig(num_envs=64, seed=8, log_interval=5, use_amp_obs=amp),
                            motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
         torch.manual_seed(0)
         policy = Policy(PHCPolicy(env, hidden_size=64, layer_sizes=(128, 64))).to(DEV)
@@ -315,11 +317,12 @@ def test_block_rollout_matches_single_step_graphs(monkeypatch):
         e = comps.experience
         runs.append(dict(step=info.global_step, tick=env.tick, obs=e.obs.clone(), rew=e.rewards.clone(),
                          done=e.dones.clone(), ids=e.env_ids.clone(), infos=infos,
+                         amp=e.amp_obs.clone() if amp else e.obs[:0].clone(),
                          blocks=len(getattr(comps.rollout, "_blocks", {}))))
     a, b = runs
     assert a["blocks"] == 0 and b["blocks"] == 1
     assert a["step"] == b["step"] and a["tick"] == b["tick"]
-    for k in ("obs", "rew", "done", "ids"):
+    for k in ("obs", "rew", "done", "ids", "amp"):
         assert torch.equal(a[k], b[k]), k
     for ia, ib in zip(a["infos"], b["infos"]):
         assert ia.keys() == ib.keys()

@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def _trainer():
+def _trainer(amp=False):
     from puffer_phc_amd import clean_pufferl
     from puffer_phc_amd.clean_pufferl.env import PHCPufferEnv
     from puffer_phc_amd.config import EnvConfig, TrainConfig
@@ -20,7 +20,8 @@ def _trainer():
     from puffer_phc_amd.synthetic import synthetic_clips
 
     q, t, c, fps = synthetic_clips(64, 20, 90, seed=7, device=DEV)
-    env = PHCPufferEnv(EnvConfig(num_envs=64, seed=4), motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
+    env = PHCPufferEnv(EnvConfig(num_envs=64, seed=4, use_amp_obs=amp),
+                       motion_data=PackedMotions.from_global_rotations(q, t, c, fps))
     env.reset()
     torch.manual_seed(0)
     policy = Policy(PHCPolicy(env, hidden_size=512, layer_sizes=(256, 128))).to(DEV)
@@ -37,15 +38,21 @@ def _iterate(cp, comps, info, policy, seed):
     torch.cuda.synchronize()
     return {k: float(getattr(losses, k)) for k in ("policy_loss", "value_loss", "entropy", "approx_kl", "clipfrac",
                                                    "before_clip_grad_norm", "l2_init_reg_loss", "mean_bound_loss",
-                                                   "explained_variance")}
+                                                   "explained_variance", "disc_loss", "disc_agent_acc",
+                                                   "disc_demo_acc")}
 
 
-def test_graphed_train_matches_eager(monkeypatch):
+@pytest.mark.parametrize("amp", [False, True])
+def test_graphed_train_matches_eager(monkeypatch, amp):
+    """amp: the C5 configuration (AMP obs): the advantage pass with the adversarial reward and the
+    replay buffer's counter-based refresh graphed, then the minibatch loop with the discriminator's
+    agent / replay / demo rows, its BCE terms and the per-minibatch loss row (core.py:229-242,
+    336-347, 394-395) — captured once that pass replays (the fourth call), replayed from the fifth."""
     from puffer_phc_amd.clean_pufferl import core
 
-    eager = _trainer()
-    graphed = _trainer()
-    for it in range(6):
+    eager = _trainer(amp)
+    graphed = _trainer(amp)
+    for it in range(8 if amp else 6):
         if it == 4:  # a schedule step between replays (scripts/train.py decays the rate each epoch)
             for tr in (eager, graphed):
                 tr[1].optimizer.param_groups[0]["lr"] *= 0.5
