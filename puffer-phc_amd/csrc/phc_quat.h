@@ -40,6 +40,47 @@ __device__ __forceinline__ float fexp_env(float x) {
 #endif
 }
 
+// PHC_FAST_ENV_TRIG (default 1): slerp's acos / sin and the rotation angle's acos as short polynomials
+// instead of the libm (OCML) routines with their range reductions: acos by Abramowitz & Stegun 4.4.46
+// (sqrt(1 - |x|) times a degree-7 polynomial, |error| <= 2e-8 before float rounding), sin on slerp's
+// [0, pi/2] by its Taylor series to x^11 (relative truncation <= 3e-8 there).  Both stay far inside
+// the 1e-5 the env's observations and rewards are held to; no flag or index depends on them (the
+// termination distance uses positions, which blend linearly).
+#ifndef PHC_FAST_ENV_TRIG
+#define PHC_FAST_ENV_TRIG 1
+#endif
+__device__ __forceinline__ float facos_env(float x) {
+#if PHC_FAST_ENV_TRIG
+  const float a = fabsf(x);
+  float p = -0.0012624911f;
+  p = fmaf(p, a, 0.0066700901f);
+  p = fmaf(p, a, -0.0170881256f);
+  p = fmaf(p, a, 0.0308918810f);
+  p = fmaf(p, a, -0.0501743046f);
+  p = fmaf(p, a, 0.0889789874f);
+  p = fmaf(p, a, -0.2145988016f);
+  p = fmaf(p, a, 1.5707963050f);
+  const float r = __builtin_amdgcn_sqrtf(1.0f - a) * p;
+  return x < 0.0f ? 3.14159265358979f - r : r;
+#else
+  return acosf(x);
+#endif
+}
+// sin(x) for x in [0, pi/2] (slerp's weights)
+__device__ __forceinline__ float fsin_half_env(float x) {
+#if PHC_FAST_ENV_TRIG
+  const float x2 = x * x;
+  float p = -2.5052108e-8f;                // -1/11!
+  p = fmaf(p, x2, 2.7557319e-6f);          // 1/9!
+  p = fmaf(p, x2, -1.9841270e-4f);         // -1/7!
+  p = fmaf(p, x2, 8.3333333e-3f);          // 1/5!
+  p = fmaf(p, x2, -1.6666667e-1f);         // -1/3!
+  return fmaf(x * x2, p, x);
+#else
+  return sinf(x);
+#endif
+}
+
 template <typename T> struct Q4 { T x, y, z, w; };
 template <typename T> struct V3 { T x, y, z; };
 
@@ -204,7 +245,7 @@ __device__ __forceinline__ float quat_angle_masked(q4 q, float *sin_theta_out) {
   const float sin_theta = fsqrt_env(1.0f - q.w * q.w);
   *sin_theta_out = sin_theta;
   if (!(fabsf(sin_theta) > 1e-5f)) return 0.0f;
-  return fold_angle_0_2pi(2.0f * acosf(q.w));
+  return fold_angle_0_2pi(2.0f * facos_env(q.w));
 }
 
 __device__ __forceinline__ v3 quat_to_exp_map(q4 q) {
@@ -225,11 +266,11 @@ __device__ __forceinline__ q4 slerp(q4 q0, q4 q1, float t) {
   if (fabsf(sin_half) < 0.001f)
     return {0.5f * q0.x + 0.5f * q1.x, 0.5f * q0.y + 0.5f * q1.y, 0.5f * q0.z + 0.5f * q1.z,
             0.5f * q0.w + 0.5f * q1.w};
-  const float half = acosf(c);
+  const float half = facos_env(c);
 #if PHC_FAST_ENV_MATH
   const float inv = fdiv_env(1.0f, sin_half);
-  const float ra = sinf((1.0f - t) * half) * inv;
-  const float rb = sinf(t * half) * inv;
+  const float ra = fsin_half_env((1.0f - t) * half) * inv;
+  const float rb = fsin_half_env(t * half) * inv;
 #else
   const float ra = sinf((1.0f - t) * half) / sin_half;
   const float rb = sinf(t * half) / sin_half;
