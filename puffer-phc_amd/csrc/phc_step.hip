@@ -523,15 +523,26 @@ static_assert(kStRec % 4 == 0 && kStRec + kWaveEnvs * kRowF <= kStWave, "obs row
 typedef const __attribute__((address_space(1))) void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
 
-// the wave's 2 x 4 frame rows into `wreg` ([env][row][312]); fr = this lane's env's frame rows
+// The slot each of the observation blend's two rows is read from: its own (2, 3), or the reward blend's
+// row it repeats (0, 1).  At 30 fps one control step advances one frame, so the t+dt blend's first row
+// is the t blend's second one: 3 distinct rows of 4 for most envs, one 1,248-B fetch fewer.
+__device__ __forceinline__ int obs_row_slot(int64_t f, int64_t r0, int64_t r1, int own) {
+  return f == r1 ? 1 : (f == r0 ? 0 : own);
+}
+
+// the wave's 2 x 4 frame rows into `wreg` ([env][row][312]); fr = this lane's env's frame rows, sl2 / sl3
+// the slots its observation rows are read from (a row that repeats one of the reward blend's is not fetched)
 __device__ __forceinline__ void stage_frame_rows(const float *__restrict__ frames, float *wreg, const int64_t fr[4],
-                                                 int wl) {
+                                                 int sl2, int sl3, int wl) {
   int f0[4], f1[4];  // the rows of the wave's envs (lanes 0 and 32), wave-uniform
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     f0[k] = __builtin_amdgcn_readlane((int)fr[k], 0);
     f1[k] = __builtin_amdgcn_readlane((int)fr[k], 32);
   }
+  // which of rows 2 / 3 each env fetches (bit 2 / 3 of the mask: rows 0 and 1 always)
+  const int need0 = 3 | (__builtin_amdgcn_readlane(sl2, 0) == 2 ? 4 : 0) | (__builtin_amdgcn_readlane(sl3, 0) == 3 ? 8 : 0);
+  const int need1 = 3 | (__builtin_amdgcn_readlane(sl2, 32) == 2 ? 4 : 0) | (__builtin_amdgcn_readlane(sl3, 32) == 3 ? 8 : 0);
 #pragma unroll
   for (int i = 0; i < kStDma; ++i) {
     const int j = i * 64 + wl;
@@ -542,7 +553,8 @@ __device__ __forceinline__ void stage_frame_rows(const float *__restrict__ frame
     const int fa = rr == 0 ? f0[0] : (rr == 1 ? f0[1] : (rr == 2 ? f0[2] : f0[3]));
     const int fb = rr == 0 ? f1[0] : (rr == 1 ? f1[1] : (rr == 2 ? f1[2] : f1[3]));
     const float *src = frames + (int64_t)(hi ? fb : fa) * kRowF + cc * 4;
-    __builtin_amdgcn_global_load_lds((gvoid *)src, (lvoid *)(wreg + i * 256), 16, 0, 0);
+    if (((hi ? need1 : need0) >> rr) & 1)
+      __builtin_amdgcn_global_load_lds((gvoid *)src, (lvoid *)(wreg + i * 256), 16, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's rows have landed (wave-local region)
 }
@@ -844,14 +856,15 @@ __global__ __launch_bounds__(64 * kWaves, PHC_ENV_WAVES) void k_env_replay(EnvVi
     dvc = {pc[0], pc[1], pc[2]};
   }
   const int64_t fr[4] = {bl0.f0, bl0.f1, bl1.f0, bl1.f1};
-  stage_frame_rows(l.frames, wreg, fr, wl);
+  const int sl2 = obs_row_slot(bl1.f0, bl0.f0, bl0.f1, 2), sl3 = obs_row_slot(bl1.f1, bl0.f0, bl0.f1, 3);
+  stage_frame_rows(l.frames, wreg, fr, sl2, sl3, wl);
   ENV_PHASE(2);
   const float *rw = wreg + gh * (4 * kRowF) + b * kRec;
   const BodyRec ref0 = blend_body(load_body(rw), load_body(rw + kRowF), bl0.b, &go);
   // the observation's reference now (13 registers instead of the two rows' 26): offset 0 for a passing
   // env (a value select: a select of two addresses would put the offsets in scratch)
   const v3 off1 = {pass ? 0.0f : go.x, pass ? 0.0f : go.y, pass ? 0.0f : go.z};
-  BodyRec ref1 = blend_body(load_body(rw + 2 * kRowF), load_body(rw + 3 * kRowF), bl1.b, &off1);
+  BodyRec ref1 = blend_body(load_body(rw + sl2 * kRowF), load_body(rw + sl3 * kRowF), bl1.b, &off1);
   // the region is reused below (reset words, replayed records, obs rows) by other lanes of this wave
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   wave_lds_handoff();
