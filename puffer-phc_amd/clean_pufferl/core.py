@@ -14,6 +14,8 @@ Differences from the reference that do not change the math:
 
 import contextlib
 import os
+import time
+import warnings
 from collections import defaultdict
 
 import numpy as np
@@ -811,9 +813,21 @@ def _amp_demo_ptr(components, info):
     return None if demo is None else (demo.data_ptr(), tuple(demo.shape))
 
 
+def _all_ranks_agree(flag, device):
+    """True when `flag` holds on every rank (the identity without data parallelism).  The train graph holds
+    collectives that every rank must replay in lockstep: a rank on another path would issue its own."""
+    if not D.is_dist():
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=device)
+    return int(D.allreduce_sum_(t).item()) == D.world_size()
+
+
 def _train_minibatches_graphed(components, info, pol):
     """The loss row of this train() call from the train graph (captured on the second eligible call
-    with an unchanged key, replayed after), or eagerly; None when not eligible."""
+    with an unchanged key, replayed after), or eagerly; None when not eligible.  Under data parallelism
+    the capture's success is agreed over the ranks (eligibility follows from the configuration and the
+    call count, the same on every rank)."""
+    dev = components.experience.obs.device
     if not _train_graph_eligible(components, info, pol):
         return None
     opt = components.optimizer
@@ -841,14 +855,25 @@ def _train_minibatches_graphed(components, info, pol):
     if st["failed"] or st["key"] != key:  # first sight of this configuration: eager
         st["graph"], st["key"] = None, key
         return _fused_update(components, info, pol)
+    ok = True
     try:
         torch.cuda.synchronize()
+        if D.is_dist():
+            # the capture makes RCCL's stream part of the capture; the process group's watchdog thread polls
+            # its pending works' events every 100 ms, and on this HIP a query of an event recorded on a stream
+            # that is capturing now fails (hipErrorCapturedEvent) and aborts the process.  Let the watchdog
+            # retire every finished work first (once per capture)
+            time.sleep(0.25)
         g = torch.cuda.CUDAGraph()
         launches0 = _native.GEMM_LAUNCHES[0]
         with _capture(g):
             row = _fused_update(components, info, pol)
         st["gemm_launches"] = _native.GEMM_LAUNCHES[0] - launches0
-    except Exception:  # noqa: BLE001  (an op that cannot be captured: stay eager)
+    except Exception as exc:  # noqa: BLE001  (an op that cannot be captured: stay eager)
+        ok = False
+        warnings.warn(f"train graph capture failed, the update stays eager: {exc!r}", RuntimeWarning, stacklevel=2)
+    # a capture executes no collective, so the ranks can still agree after it: all replay, or all stay eager
+    if not _all_ranks_agree(ok, dev):
         st["failed"] = True
         torch.cuda.synchronize()
         return _fused_update(components, info, pol)
