@@ -99,6 +99,11 @@ def _worker(rank, world, port, root):
         both = decision.clone()
         D.allreduce_sum_(both)
         assert float(both) in (0.0, float(world))
+        # (7) the train graph's capture outcome is agreed over the ranks (core._all_ranks_agree): a rank
+        # whose capture failed makes every rank stay eager (a lone eager rank would issue the graph's
+        # collectives alone)
+        assert C._all_ranks_agree(True, "cpu") is True
+        assert C._all_ranks_agree(rank == 0, "cpu") is False
     finally:
         dist.destroy_process_group()
 
