@@ -254,8 +254,10 @@ struct PdArgs {
 
 // Per-block LDS: the body table with the derived constants (row stride 79 floats: lanes b = 0..23
 // reading the same field hit 24 distinct banks), per env the tree-pass slots (FK record 13 / inward
-// contribution 27 / acceleration 6 floats) and each body's outward-pass operands K = D^-1 A,
-// L = D^-1 B, y = D^-1 u (21 floats), so they do not occupy registers between the passes.
+// contribution 27 / acceleration 6 floats) and the self-collision records.  Each body's outward-pass
+// operands K = D^-1 A, L = D^-1 B, y = D^-1 u (21 floats) stay in its lane's registers from the
+// inward pass to the outward pass (196 VGPRs, still 2 waves per SIMD): held in LDS instead, the
+// step ran 2-4 % slower (409 -> 400 us at 4096 envs, 1569 -> 1509 us at 16384; profiles/r06u).
 constexpr int kTab = 79;  // odd: the 24 lanes reading one field hit 24 distinct banks
 enum : int {
   T_PARENT = 0, T_LEVEL = 1, T_NCH = 2, T_CH = 3, T_OFF = 6, T_MASS = 9, T_COM = 10, T_A0 = 13 /* 9, full */,
@@ -265,7 +267,6 @@ enum : int {
 // per env and body, refreshed every substep for the self-collision pass: bounding sphere, world
 // segment (start, direction), radius, world angular velocity, world origin velocity, origin
 constexpr int kSeg = 20;
-constexpr int kOut = 21;
 
 __device__ __forceinline__ v3 ld3(const float *p) { return {p[0], p[1], p[2]}; }
 __device__ __forceinline__ M3 ld9(const float *p) {
@@ -279,12 +280,9 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     PhysView e, const float *__restrict__ model, const float *__restrict__ target, PdArgs pa, PhysConsts c) {
   __shared__ float tab[kBodies * kTab];
   __shared__ float slots[kPhysEnvs][kBodies][kSlot];
-  __shared__ __attribute__((aligned(16))) float outw[kPhysEnvs][kBodies][kOut];
-  // the self-collision records share the outward-pass operands' memory: written and read between
-  // the outward pass of one substep and the inward pass of the next (the block stays within 20 KB
-  // of LDS: 8 workgroups per CU, 2 waves per SIMD)
-  static_assert(kSeg <= kOut, "segw aliases outw");
-  float(*segw)[kBodies][kSeg] = reinterpret_cast<float(*)[kBodies][kSeg]>(&outw[0][0][0]);
+  // the self-collision records: written and read between the outward pass of one substep and the
+  // inward pass of the next (the block stays within 20 KB of LDS: 8 workgroups per CU, 2 waves per SIMD)
+  __shared__ __attribute__((aligned(16))) float segw[kPhysEnvs][kBodies][kSeg];
   __shared__ float fsc[kPhysEnvs][kBodies][6];  // self-contact wrench per body (world torque, force)
   __shared__ unsigned short pairs[kBodies * (kBodies - 1) / 2];  // colliding pairs i | j << 5, i < j
 #if PHC_PHYS_COMPACT
@@ -297,7 +295,6 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
   const int b = lane < kBodies ? lane : 0;
   const int64_t ev = env < e.n ? env : e.n - 1;
   float(*S)[kSlot] = slots[sub];
-  float(*O)[kOut] = outw[sub];
   launch_clock_begin(c.clk);
   const float dt = c.dt;
 
@@ -605,6 +602,8 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       }
     };
     // ---- inward pass
+    M3 oK, oL;  // this body's outward-pass operands (registers, see the LDS note above)
+    v3 oy;
     for (int L = depth; L >= 1; --L) {
       if (level == L && !(PHC_PHYS_ABLATE & 4)) {
         M3 A, B, M;
@@ -620,13 +619,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
           Lm = m3_mul(Dinv, B);
           y = m3_v(Dinv, vsub(tau, pt_));
         }
-        float *o = O[b];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-          o[i] = Ka.m[i];
-          o[9 + i] = Lm.m[i];
-        }
-        o[18] = y.x; o[19] = y.y; o[20] = y.z;
+        oK = Ka; oL = Lm; oy = y;
         // Ia = I^A - U D^-1 U^T, pa = pA + Ia c + U D^-1 u  (U = [A; B^T]); the A and M blocks are
         // symmetric, so only their upper triangles are formed
         const S6 Aa = s6_sub(s6_of(A), sym_mul(A, Ka));
@@ -719,8 +712,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         const M3 E = m3_quat(r.x, r.y, r.z, r.w);
         aw = vadd(m3_tv(E, apw), cw);
         av = vadd(m3_tv(E, vsub(ld3(ps + 3), cross3(ld3(T + T_OFF), apw))), cv);
-        const float *o = O[b];
-        qdd = vsub(vsub(ld3(o + 18), m3_v(ld9(o), aw)), m3_v(ld9(o + 9), av));
+        qdd = vsub(vsub(oy, m3_v(oK, aw)), m3_v(oL, av));
         aw = vadd(aw, qdd);
         float *s = S[b];
         s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
