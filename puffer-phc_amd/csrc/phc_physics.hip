@@ -10,7 +10,8 @@
 //      implicit PD torques tau = kp (target - e) - (kd + dt kp) qd, e = rotation vector of the joint;
 //   3. Featherstone's articulated-body algorithm: inward pass of articulated inertias / bias forces
 //      (the joint-space diagonal carries armature + dt kd + dt^2 kp, the implicit-PD term), the
-//      floating root's 6x6 solve, outward pass of accelerations;
+//      floating root's 6x6 solve, outward pass of accelerations — all three in the W frame (world
+//      orientation, reference point at each body's origin: a level hands its parent a shift only);
 //   4. semi-implicit Euler: velocities, then joint / root rotations (quaternions) and root position.
 // The CPU restatement is oracle/physics_oracle.py (generic 6x6 matrices, float64).
 //
@@ -256,7 +257,7 @@ struct PdArgs {
 // reading the same field hit 24 distinct banks), per env the tree-pass slots (FK record 13 / inward
 // contribution 27 / acceleration 6 floats) and the self-collision records.  Each body's outward-pass
 // operands K = D^-1 A, L = D^-1 B, y = D^-1 u (21 floats) stay in its lane's registers from the
-// inward pass to the outward pass (196 VGPRs, still 2 waves per SIMD): held in LDS instead, the
+// inward pass to the outward pass (209 VGPRs, still 2 waves per SIMD): held in LDS instead, the
 // step ran 2-4 % slower (409 -> 400 us at 4096 envs, 1569 -> 1509 us at 16384; profiles/r06u).
 constexpr int kTab = 79;  // odd: the 24 lanes reading one field hit 24 distinct banks
 enum : int {
@@ -396,6 +397,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
 
   q4 Q = {0.0f, 0.0f, 0.0f, 1.0f};
   v3 P = {0.0f, 0.0f, 0.0f}, w = P, v = P;
+  v3 rw = P;  // world offset of this body's origin from its parent's (P - P_parent)
   // outward pass: world quaternion / origin and body twist of every body
   auto kinematics = [&]() {
     for (int L = 0; L <= depth; ++L) {
@@ -407,7 +409,8 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
           const q4 Qp = {ps[0], ps[1], ps[2], ps[3]};
           const v3 wp = ld3(ps + 7), off = ld3(T + T_OFF);
           Q = qmul_std(Qp, r);
-          P = vadd(ld3(ps + 4), m3_v(m3_quat(Qp.x, Qp.y, Qp.z, Qp.w), off));
+          rw = m3_v(m3_quat(Qp.x, Qp.y, Qp.z, Qp.w), off);
+          P = vadd(ld3(ps + 4), rw);
           const M3 E = m3_quat(r.x, r.y, r.z, r.w);
           w = vadd(m3_tv(E, wp), om);
           v = m3_tv(E, vsub(ld3(ps + 10), cross3(off, wp)));
@@ -427,6 +430,8 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     kinematics();
     // ---- bias force pA = V x* (I V) - f_ext (gravity + ground contact), body coordinates
     v3 pt_, pb_, tau = {0.0f, 0.0f, 0.0f}, cw = {0.0f, 0.0f, 0.0f}, cv = {0.0f, 0.0f, 0.0f};
+    v3 uw, mcw;  // W frame: the joint torque, mass x centre of mass
+    S6 A0w, Dxw;  // W frame: rotational inertia about the origin, the joint-space diagonal R diag(d) R^T
     {
       const M3 R = m3_quat(Q.x, Q.y, Q.z, Q.w);
       const float mass = T[T_MASS];
@@ -581,12 +586,33 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         cw = cross3(w, om);
         cv = cross3(v, om);
       }
+      // The tree passes run in the W frame: world orientation, reference point at the body's own
+      // origin.  A child's quantities then reach its parent by the shift P - P_parent alone, with no
+      // rotation inside the level-serial passes (body coordinates needed E (.) E^T on every articulated
+      // inertia block once per level); the per-body rotations into W happen here, once per substep, all
+      // lanes at once.  The joint's motion subspace is [R; 0], so its joint-space inertia
+      // R^T A R + diag(d) becomes A + R diag(d) R^T for the W-frame joint acceleration R qdd.
+      pt_ = m3_v(R, pt_);
+      pb_ = m3_v(R, pb_);
+      uw = m3_v(R, tau);
+      cw = m3_v(R, cw);
+      cv = m3_v(R, cv);
+      A0w = sandwich(R, s6_of(ld9(T + T_A0)));
+      mcw = vscale(m3_v(R, com), mass);
+      const v3 dx = ld3(T + T_DEXT);
+      const float *m = R.m;
+      Dxw = {dx.x * m[0] * m[0] + dx.y * m[1] * m[1] + dx.z * m[2] * m[2],
+             dx.x * m[3] * m[3] + dx.y * m[4] * m[4] + dx.z * m[5] * m[5],
+             dx.x * m[6] * m[6] + dx.y * m[7] * m[7] + dx.z * m[8] * m[8],
+             dx.x * m[0] * m[3] + dx.y * m[1] * m[4] + dx.z * m[2] * m[5],
+             dx.x * m[0] * m[6] + dx.y * m[1] * m[7] + dx.z * m[2] * m[8],
+             dx.x * m[3] * m[6] + dx.y * m[4] * m[7] + dx.z * m[5] * m[8]};
     }
     // articulated inertia [[A, B], [B^T, M]]: the body's own plus its children's contributions
     auto gather = [&](M3 &A, M3 &B, M3 &M) {
       const float mass = T[T_MASS];
-      A = ld9(T + T_A0);
-      B = m3_skew(vscale(ld3(T + T_COM), mass));
+      A = s6_full(A0w);
+      B = m3_skew(mcw);
       M = {{mass, 0.0f, 0.0f, 0.0f, mass, 0.0f, 0.0f, 0.0f, mass}};
       for (int k = 0; k < nch; ++k) {
         const float *s = S[k == 0 ? ch0 : (k == 1 ? ch1 : ch2)];
@@ -611,13 +637,10 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         M3 Ka, Lm;
         v3 y;
         {
-          M3 D = A;
-          const v3 dx = ld3(T + T_DEXT);
-          D.m[0] += dx.x; D.m[4] += dx.y; D.m[8] += dx.z;
-          const M3 Dinv = m3_inv(D);
+          const M3 Dinv = m3_inv(m3_add(A, s6_full(Dxw)));
           Ka = m3_mul(Dinv, A);
           Lm = m3_mul(Dinv, B);
-          y = m3_v(Dinv, vsub(tau, pt_));
+          y = m3_v(Dinv, vsub(uw, pt_));
         }
         oK = Ka; oL = Lm; oy = y;
         // Ia = I^A - U D^-1 U^T, pa = pA + Ia c + U D^-1 u  (U = [A; B^T]); the A and M blocks are
@@ -627,28 +650,22 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         const S6 Ma = s6_sub(s6_of(M), sym_tmul(B, Lm));
         const v3 pat = vadd(vadd(pt_, vadd(m3_v(s6_full(Aa), cw), m3_v(Ba, cv))), m3_v(A, y));
         const v3 pab = vadd(vadd(pb_, vadd(m3_tv(Ba, cw), m3_v(s6_full(Ma), cv))), m3_tv(B, y));
-        // to parent coordinates: rotate by E, then shift by the joint offset
-        const M3 E = m3_quat(r.x, r.y, r.z, r.w);
-        const v3 off = ld3(T + T_OFF);
-        const M3 Br = m3_mul_t(m3_mul(E, Ba), E);
-        const S6 Mr = sandwich(E, Ma);
-        const M3 RM = skew_mul(off, s6_full(Mr));
-        // A_p = E Aa E^T - Br [r]x + [r]x Br^T - [r]x Mr [r]x, with [r]x Br^T = -(Br [r]x)^T
-        const M3 X = mul_skew(Br, off), Z = mul_skew(RM, off);
-        const S6 Ar = sandwich(E, Aa);
-        const S6 Ap = {Ar.xx - 2.0f * X.m[0] - Z.m[0], Ar.yy - 2.0f * X.m[4] - Z.m[4], Ar.zz - 2.0f * X.m[8] - Z.m[8],
-                       Ar.xy - (X.m[1] + X.m[3]) - Z.m[1], Ar.xz - (X.m[2] + X.m[6]) - Z.m[2],
-                       Ar.yz - (X.m[5] + X.m[7]) - Z.m[5]};
-        const M3 Bp = m3_add(Br, RM);
-        const v3 Fp = m3_v(E, pab);
-        const v3 Np = vadd(m3_v(E, pat), cross3(off, Fp));
+        // to the parent's W frame: the shift by r = P - P_parent,
+        // A_p = Aa - Ba [r]x + [r]x Ba^T - [r]x Ma [r]x, with [r]x Ba^T = -(Ba [r]x)^T
+        const M3 RM = skew_mul(rw, s6_full(Ma));
+        const M3 X = mul_skew(Ba, rw), Z = mul_skew(RM, rw);
+        const S6 Ap = {Aa.xx - 2.0f * X.m[0] - Z.m[0], Aa.yy - 2.0f * X.m[4] - Z.m[4], Aa.zz - 2.0f * X.m[8] - Z.m[8],
+                       Aa.xy - (X.m[1] + X.m[3]) - Z.m[1], Aa.xz - (X.m[2] + X.m[6]) - Z.m[2],
+                       Aa.yz - (X.m[5] + X.m[7]) - Z.m[5]};
+        const M3 Bp = m3_add(Ba, RM);
+        const v3 Np = vadd(pat, cross3(rw, pab));
         float *s = S[b];
         store_s6(Ap, s);
 #pragma unroll
         for (int i = 0; i < 9; ++i) s[6 + i] = Bp.m[i];
-        store_s6(Mr, s + 15);
+        store_s6(Ma, s + 15);
         s[21] = Np.x; s[22] = Np.y; s[23] = Np.z;
-        s[24] = Fp.x; s[25] = Fp.y; s[26] = Fp.z;
+        s[24] = pab.x; s[25] = pab.y; s[26] = pab.z;
       }
       phys_sync();
     }
@@ -709,10 +726,9 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       if (level == L && !(PHC_PHYS_ABLATE & 8)) {  // ablation builds only (timing breakdown)
         const float *ps = S[parent];
         const v3 apw = ld3(ps);
-        const M3 E = m3_quat(r.x, r.y, r.z, r.w);
-        aw = vadd(m3_tv(E, apw), cw);
-        av = vadd(m3_tv(E, vsub(ld3(ps + 3), cross3(ld3(T + T_OFF), apw))), cv);
-        qdd = vsub(vsub(oy, m3_v(oK, aw)), m3_v(oL, av));
+        aw = vadd(apw, cw);
+        av = vadd(vsub(ld3(ps + 3), cross3(rw, apw)), cv);
+        qdd = vsub(vsub(oy, m3_v(oK, aw)), m3_v(oL, av));  // W frame: R times the joint's qdd
         aw = vadd(aw, qdd);
         float *s = S[b];
         s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
@@ -721,6 +737,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
     }
     // ---- semi-implicit Euler
     if (act && b > 0) {
+      qdd = m3_tv(m3_quat(Q.x, Q.y, Q.z, Q.w), qdd);  // to joint (body) coordinates
       const v3 kp = ld3(T + T_KP), kd = ld3(T + T_KD);
       applied = {tau.x - dt * (kd.x + dt * kp.x) * qdd.x, tau.y - dt * (kd.y + dt * kp.y) * qdd.y,
                  tau.z - dt * (kd.z + dt * kp.z) * qdd.z};
@@ -729,11 +746,14 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       if (wn2 > c.max_w * c.max_w) om = vscale(om, c.max_w * rsqrtf(wn2));  // max_angular_velocity
       r = qnormalize(qmul_std(r, quat_exp_increment(vscale(om, dt))));
     } else if (act) {
+      const M3 R0 = m3_quat(Q.x, Q.y, Q.z, Q.w);  // the root's acceleration, W frame -> body coordinates
+      aw = m3_tv(R0, aw);
+      av = m3_tv(R0, av);
       w0 = vadd(w0, vscale(aw, dt));
       const float wn2 = w0.x * w0.x + w0.y * w0.y + w0.z * w0.z;
       if (wn2 > c.max_w * c.max_w) w0 = vscale(w0, c.max_w * rsqrtf(wn2));
       v0 = vadd(v0, vscale(av, dt));
-      p0 = vadd(p0, vscale(m3_v(m3_quat(Q.x, Q.y, Q.z, Q.w), v0), dt));
+      p0 = vadd(p0, vscale(m3_v(R0, v0), dt));
       q0 = qnormalize(qmul_std(q0, quat_exp_increment(vscale(w0, dt))));
     }
   }
