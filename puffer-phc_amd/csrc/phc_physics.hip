@@ -133,13 +133,15 @@ __device__ __forceinline__ v3 m3_tv(const M3 &a, v3 v) {  // a^T v
   return {a.m[0] * v.x + a.m[3] * v.y + a.m[6] * v.z, a.m[1] * v.x + a.m[4] * v.y + a.m[7] * v.z,
           a.m[2] * v.x + a.m[5] * v.y + a.m[8] * v.z};
 }
-__device__ __forceinline__ M3 m3_inv(const M3 &a) {  // adjugate / determinant
+// inverse of a symmetric 3x3 (adjugate / determinant): the six distinct entries only
+__device__ __forceinline__ M3 m3_inv_sym(const M3 &a) {
   const float *m = a.m;
-  const float c0 = m[4] * m[8] - m[5] * m[7], c1 = m[5] * m[6] - m[3] * m[8], c2 = m[3] * m[7] - m[4] * m[6];
+  const float c0 = m[4] * m[8] - m[5] * m[5], c1 = m[5] * m[2] - m[1] * m[8], c2 = m[1] * m[5] - m[4] * m[2];
   const float id = rcp(m[0] * c0 + m[1] * c1 + m[2] * c2);
-  return {{c0 * id, (m[2] * m[7] - m[1] * m[8]) * id, (m[1] * m[5] - m[2] * m[4]) * id, c1 * id,
-           (m[0] * m[8] - m[2] * m[6]) * id, (m[2] * m[3] - m[0] * m[5]) * id, c2 * id,
-           (m[1] * m[6] - m[0] * m[7]) * id, (m[0] * m[4] - m[1] * m[3]) * id}};
+  const float i00 = c0 * id, i01 = c1 * id, i02 = c2 * id;
+  const float i11 = (m[0] * m[8] - m[2] * m[2]) * id, i12 = (m[2] * m[1] - m[0] * m[5]) * id;
+  const float i22 = (m[0] * m[4] - m[1] * m[1]) * id;
+  return {{i00, i01, i02, i01, i11, i12, i02, i12, i22}};
 }
 __device__ __forceinline__ v3 cross3(v3 a, v3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 // [r]x M (column j = r x M_col j) and M [r]x (row i = M_row i x r) without the skew matrix's zeros
@@ -637,7 +639,7 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         M3 Ka, Lm;
         v3 y;
         {
-          const M3 Dinv = m3_inv(m3_add(A, s6_full(Dxw)));
+          const M3 Dinv = m3_inv_sym(m3_add(A, s6_full(Dxw)));
           Ka = m3_mul(Dinv, A);
           Lm = m3_mul(Dinv, B);
           y = m3_v(Dinv, vsub(uw, pt_));
@@ -669,53 +671,19 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       }
       phys_sync();
     }
-    // ---- floating root: a0 = -IA^-1 pA (6x6 Cholesky on lane 0)
+    // ---- floating root: a0 = -IA^-1 pA, IA = [[A, B], [B^T, M]], by 3x3 blocks on lane 0:
+    // T = B M^-1, (A - T B^T) a_w = -pt + T pb, M a_v = -pb - B^T a_w (two closed-form symmetric
+    // inverses: independent products instead of a 6x6 Cholesky's serial chain of square roots)
     v3 aw = {0.0f, 0.0f, 0.0f}, av = {0.0f, 0.0f, 0.0f};
     if (level == 0 && !(PHC_PHYS_ABLATE & 16)) {
       M3 A, B, M;
       gather(A, B, M);
-      float G[6][6], rhs[6];
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          G[i][j] = A.m[3 * i + j];
-          G[i][3 + j] = B.m[3 * i + j];
-          G[3 + i][j] = B.m[3 * j + i];
-          G[3 + i][3 + j] = M.m[3 * i + j];
-        }
-      rhs[0] = -pt_.x; rhs[1] = -pt_.y; rhs[2] = -pt_.z; rhs[3] = -pb_.x; rhs[4] = -pb_.y; rhs[5] = -pb_.z;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        float d = G[j][j];
-#pragma unroll
-        for (int k = 0; k < j; ++k) d -= G[j][k] * G[j][k];
-        const float ljj = sqrtf(fmaxf(d, 1e-20f)), il = rcp(ljj);
-        G[j][j] = il;  // the diagonal holds 1 / l_jj
-#pragma unroll
-        for (int i = j + 1; i < 6; ++i) {
-          float s = G[i][j];
-#pragma unroll
-          for (int k = 0; k < j; ++k) s -= G[i][k] * G[j][k];
-          G[i][j] = s * il;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {  // L y = rhs
-        float s = rhs[i];
-#pragma unroll
-        for (int k = 0; k < i; ++k) s -= G[i][k] * rhs[k];
-        rhs[i] = s * G[i][i];
-      }
-#pragma unroll
-      for (int i = 5; i >= 0; --i) {  // L^T x = y
-        float s = rhs[i];
-#pragma unroll
-        for (int k = i + 1; k < 6; ++k) s -= G[k][i] * rhs[k];
-        rhs[i] = s * G[i][i];
-      }
-      aw = {rhs[0], rhs[1], rhs[2]};
-      av = {rhs[3], rhs[4], rhs[5]};
+      const M3 Mi = m3_inv_sym(M);
+      const M3 Tm = m3_mul(B, Mi);
+      const S6 Sc = s6_sub(s6_of(A), S6{row_row(Tm, 0, B, 0), row_row(Tm, 1, B, 1), row_row(Tm, 2, B, 2),
+                                        row_row(Tm, 0, B, 1), row_row(Tm, 0, B, 2), row_row(Tm, 1, B, 2)});
+      aw = m3_v(m3_inv_sym(s6_full(Sc)), vsub(m3_v(Tm, pb_), pt_));
+      av = m3_v(Mi, vscale(vadd(pb_, m3_tv(B, aw)), -1.0f));
       float *s = S[0];
       s[0] = aw.x; s[1] = aw.y; s[2] = aw.z; s[3] = av.x; s[4] = av.y; s[5] = av.z;
     }
