@@ -15,13 +15,14 @@
 //   4. semi-implicit Euler: velocities, then joint / root rotations (quaternions) and root position.
 // The CPU restatement is oracle/physics_oracle.py (generic 6x6 matrices, float64).
 //
-// Decomposition (MI355X): one 32-lane half-wave per env, lane b = body b (24 of 32 lanes), 8 envs
-// per 256-thread workgroup, as k_env_step.  The tree passes run level-synchronously (depth 8 for
-// SMPL): at level L the lanes of that level read their parent's (outward) or children's (inward)
-// record from the env's LDS slots and write their own; a workgroup barrier separates levels.  All
-// per-body state stays in registers across the substeps; HBM is touched once per env step (read the
-// root record, dof_state and targets; write the 24 rigid-body records, dof_state, dof_force).  The
-// kernel is VALU-latency bound (about 3k VALU instructions per body per substep).
+// Decomposition (MI355X): one 32-lane half-wave per env, lane b = body b (24 of 32 lanes), 2 envs
+// per single-wave workgroup.  The tree passes run level-synchronously (depth 8 for SMPL): at level L
+// the lanes of that level read their parent's (outward) or children's (inward) record from the env's
+// LDS slots and write their own; the wave's LDS operations complete in issue order, so a compiler
+// barrier separates the levels (phys_sync).  All per-body state stays in registers across the
+// substeps; HBM is touched once per env step (read the root record, dof_state and targets; write the
+// 24 rigid-body records, dof_state, dof_force).  The kernel is VALU-latency bound: about 6.1 k VALU
+// wave-instructions per wave per substep at 2 waves per SIMD.
 //
 // Body model row (floats, PHC_BODY_MODEL_STRIDE = 80):
 //   0 parent  1 level  2 num_children  3..5 children  6..8 joint offset (parent coords)  9 mass
