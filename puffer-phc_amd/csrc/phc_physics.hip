@@ -62,7 +62,7 @@ __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x);
 constexpr int kModel = PHC_BODY_MODEL_STRIDE;
 constexpr int kPhysEnvs = PHC_PHYS_EPB;
 constexpr int kPhysBlock = kPhysEnvs * kGroup;
-constexpr int kSlot = 27;  // LDS floats per body: A(6, sym) B(9) M(6, sym) f(6)
+constexpr int kSlot = 28;  // LDS floats per body: A(6, sym) B(9) M(6, sym) f(6), padded to 16 B (b128 reads)
 
 // The hand-offs between the tree levels (and the table / pair-list / self-contact exchanges) go
 // through LDS between the lanes of ONE wave (one workgroup = one wave of 2 envs): a wave's LDS
@@ -283,7 +283,7 @@ __device__ __forceinline__ M3 ld9(const float *p) {
 __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_PHYS_WAVES_PER_SIMD, PHC_PHYS_WAVES_PER_SIMD))) void k_physics_step(
     PhysView e, const float *__restrict__ model, const float *__restrict__ target, PdArgs pa, PhysConsts c) {
   __shared__ float tab[kBodies * kTab];
-  __shared__ float slots[kPhysEnvs][kBodies][kSlot];
+  __shared__ __attribute__((aligned(16))) float slots[kPhysEnvs][kBodies][kSlot];
   // the self-collision records: written and read between the outward pass of one substep and the
   // inward pass of the next (the block stays within 20 KB of LDS: 8 workgroups per CU, 2 waves per SIMD)
   __shared__ __attribute__((aligned(16))) float segw[kPhysEnvs][kBodies][kSeg];
