@@ -266,8 +266,11 @@ constexpr int kTab = 79;  // odd: the 24 lanes reading one field hit 24 distinct
 enum : int {
   T_PARENT = 0, T_LEVEL = 1, T_NCH = 2, T_CH = 3, T_OFF = 6, T_MASS = 9, T_COM = 10, T_A0 = 13 /* 9, full */,
   T_KP = 22, T_KD = 25, T_DEXT = 28, T_NPTS = 31, T_PTS = 32 /* 32 */, T_IC = 64 /* 6, sym */,
-  T_SEG = 70 /* p0 3, p1 3, radius */, T_MASK = 77
+  T_SEG = 70 /* p0 3, p1 3, radius */, T_MASK = 77, T_OWN = 78 /* contact points the body's lane walks itself */
 };
+// the lanes past the bodies (kGroup - kBodies per env) walk the contact points of the many-point bodies
+// beyond their first kOwnPts (launch table spr_*): a wave walks at most kSparePts points instead of kMaxPoints
+constexpr int kSpare = kGroup - kBodies, kOwnPts = 2, kSparePts = 3;
 // per env and body, refreshed every substep for the self-collision pass: bounding sphere, world
 // segment (start, direction), radius, world angular velocity, world origin velocity, origin
 constexpr int kSeg = 20;
@@ -293,6 +296,9 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
   __shared__ unsigned short hits[kPhysEnvs][kBodies * (kBodies - 1) / 2];  // this substep's broad-phase hits
 #endif
   __shared__ int npairs_s;
+  __shared__ int spr_b[kSpare], spr_k0[kSpare], spr_k1[kSpare];  // spare lane s: points [k0, k1) of body b (-1: none)
+  __shared__ int spr_of[kBodies][2];                                 // the spare lanes walking body b's points
+  __shared__ __attribute__((aligned(16))) float spw[kPhysEnvs][kSpare][8];  // their wrenches (torque, force)
   const int lane = threadIdx.x % kGroup, sub = threadIdx.x / kGroup;
   const int64_t env = (int64_t)blockIdx.x * kPhysEnvs + sub;
   const bool act = env < e.n && lane < kBodies;
@@ -350,6 +356,21 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
       pairs[off++] = (unsigned short)(t | (j << 5));
     }
     if (t == kBodies - 1) npairs_s = off;
+  }
+  if (threadIdx.x == 0) {  // contact-point split: each spare lane takes <= kSparePts of a body's last points
+    int sl = 0;
+    for (int i = 0; i < kSpare; ++i) spr_b[i] = -1, spr_k0[i] = spr_k1[i] = 0;
+    for (int i = 0; i < kBodies; ++i) {
+      int own = (int)tab[i * kTab + T_NPTS];
+      spr_of[i][0] = spr_of[i][1] = -1;
+      for (int j = 0; j < 2 && own > kOwnPts && sl < kSpare; ++j, ++sl) {
+        const int take = min(kSparePts, own - kOwnPts);
+        spr_b[sl] = i, spr_k0[sl] = own - take, spr_k1[sl] = own;
+        spr_of[i][j] = sl;
+        own -= take;
+      }
+      tab[i * kTab + T_OWN] = (float)own;
+    }
   }
   phys_sync();
   const int npairs = npairs_s;
@@ -559,22 +580,58 @@ __global__ __launch_bounds__(kPhysBlock) __attribute__((amdgpu_waves_per_eu(PHC_
         }
         phys_sync();  // segw / fsc are rewritten next substep
       }
-      const v3 zb = {R.m[6], R.m[7], R.m[8]};  // R^T z
-      const int npts = (int)T[T_NPTS];
-      for (int k = 0; k < ((PHC_PHYS_ABLATE & 2) ? 0 : npts); ++k) {
-        const float *pt = T + T_PTS + 4 * k;
+      // penalty ground contact: this lane's body's first T_OWN points, and on a spare lane (lane >= kBodies)
+      // the points [k0, k1) of the body spr_b assigns it (its pose from that body's kinematics record); the
+      // spare lanes hand their wrenches to the body lanes through LDS
+      const int sp = lane - kBodies;
+      const bool spare = sp >= 0 && env < e.n && !(PHC_PHYS_ABLATE & 2);
+      int cb = b, k0 = 0, k1 = (PHC_PHYS_ABLATE & 2) ? 0 : (int)T[T_OWN];
+      M3 Rc = R;
+      v3 Pc = P, wc = w, vc = v;
+      if (spare) {
+        cb = spr_b[sp];
+        k0 = spr_k0[sp];
+        k1 = cb >= 0 ? spr_k1[sp] : 0;
+        cb = cb >= 0 ? cb : 0;
+        const float *ks = S[cb];
+        Rc = m3_quat(ks[0], ks[1], ks[2], ks[3]);
+        Pc = ld3(ks + 4);
+        wc = ld3(ks + 7);
+        vc = ld3(ks + 10);
+      }
+      const float *Tc = tab + cb * kTab;
+      const v3 zb = {Rc.m[6], Rc.m[7], Rc.m[8]};  // R^T z
+      v3 tq = {0.0f, 0.0f, 0.0f}, fq = {0.0f, 0.0f, 0.0f};
+      for (int k = k0; k < k1; ++k) {
+        const float *pt = Tc + T_PTS + 4 * k;
         const v3 cp = ld3(pt);
         const float rho = pt[3];
-        const float d = rho - (P.z + R.m[6] * cp.x + R.m[7] * cp.y + R.m[8] * cp.z);
+        const float d = rho - (Pc.z + Rc.m[6] * cp.x + Rc.m[7] * cp.y + Rc.m[8] * cp.z);
         if (d > 0.0f) {
           const v3 a = vsub(cp, vscale(zb, rho));
-          const v3 vw = m3_v(R, vadd(v, cross3(w, a)));
+          const v3 vw = m3_v(Rc, vadd(vc, cross3(wc, a)));
           const float fn = fmaxf(0.0f, c.kn * d - c.cn * vw.z);
           const float vt = sqrtf(vw.x * vw.x + vw.y * vw.y);
           const float kt = fminf(c.ct, c.mu * fn * rcp(fmaxf(vt, 1e-12f)));
-          const v3 Fb = m3_tv(R, v3{-kt * vw.x, -kt * vw.y, fn});
-          fn_ = vadd(fn_, cross3(a, Fb));
-          ff = vadd(ff, Fb);
+          const v3 Fb = m3_tv(Rc, v3{-kt * vw.x, -kt * vw.y, fn});
+          tq = vadd(tq, cross3(a, Fb));
+          fq = vadd(fq, Fb);
+        }
+      }
+      if (spare) {
+        float *o = spw[sub][sp];
+        o[0] = tq.x; o[1] = tq.y; o[2] = tq.z; o[3] = fq.x; o[4] = fq.y; o[5] = fq.z;
+      }
+      phys_sync();
+      fn_ = vadd(fn_, tq);
+      ff = vadd(ff, fq);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q = spr_of[b][j];
+        if (q >= 0) {
+          const float *o = spw[sub][q];
+          fn_ = vadd(fn_, ld3(o));
+          ff = vadd(ff, ld3(o + 3));
         }
       }
       // I V = [A0 w + m com x v; m (v - com x w)]
